@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Headline benchmark: USE_BF Bloom-filter probe throughput on MI355X (BASELINE.json metric
+"bloom probe keys/sec (whole node)", config C2).
+
+One step = one probe pass of the hot path (PTBloomFilter::LookupSel, reference
+src/bloom_filter.cpp:60-68, as PhysicalUseBF::ExecuteInternal drives it) over this rank's batch of
+1e9 device-resident int64 keys against the filter CREATE_BF built from 1e7 keys: hash, gather,
+ascending uint32 selection vector + survivor count. Multi-GPU (torch.distributed.run, one process
+per GPU): the build rows are split by row range, partial filters are OR-merged over RCCL, and
+every rank probes its own 1e9-row slice of the global probe column (weak scaling, no data-path
+collective in the probe).
+
+Prints ONE JSON line on rank 0. `roofline` prices the dominant kernel (probe phase 1) from HIP
+events recorded on the launch stream; `cpu_baseline` times the C++ restatement (oracle/) on a
+bounded sample on rank 0's host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "duckdb-robust-predicate-transfer_amd"))
+
+HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+KEY_BYTES = 8           # int64 key read per probed row (algorithmic)
+SEL_BYTES = 4           # uint32 sel entry written per survivor (algorithmic)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--probe-rows", type=float, default=1e9, help="probe rows per GPU")
+    ap.add_argument("--build-rows", type=float, default=1e7, help="global build rows")
+    ap.add_argument("--p", type=float, default=0.10, help="fraction of probe rows drawn from the build keys")
+    ap.add_argument("--cpu-sample", type=float, default=1e8, help="probe rows in the CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "16")))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int) -> dict:
+    """The C++ restatement of the reference CPU path, morsel-parallel in 2048-row vectors."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import rpt_oracle as orc
+
+    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
+    lnb = orc.log_num_blocks(n_build)
+    words = orc.new_words(lnb)
+    build_keys = orc.synth_build_keys(n_build)
+    build_s = orc.build_mt(words, lnb, build_keys, threads)
+    del build_keys
+    keys = orc.synth_probe_keys(sample, n_build, p_permille)
+    orc.probe_mt(words, lnb, keys, threads)  # warm-up
+    runs = [orc.probe_mt(words, lnb, keys, threads) for _ in range(5)]
+    med = statistics.median(r[0] for r in runs)
+    return {
+        "value": sample / med,
+        "unit": "keys/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"probe of the first {sample:.0e} rows of the same synthetic probe stream against the same "
+                   f"{n_build:.0e}-key filter (2^{lnb} blocks), {threads} std::threads, 2048-row vectors, "
+                   f"hash included; median of 5 after 1 warm-up; build of the filter {n_build / build_s:.3e} keys/s"),
+        "cpu_model": _cpu_model(),
+        "survivors": runs[0][1],
+    }
+
+
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    import rpt_amd
+    from rpt_amd.distributed import allreduce_or_filter, shard_range
+
+    n_probe = int(args.probe_rows)
+    n_build = int(args.build_rows)
+    p_permille = int(round(args.p * 1000))
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[local])
+
+    # ---- CREATE_BF: sharded build + OR merge (reported, not the headline) -------------------------
+    lo, hi = shard_range(n_build, rank, world)
+    build_keys = rpt_amd.synth_build_keys(hi - lo, start=lo, device=device)
+    bf = rpt_amd.BloomFilter(n_build, device=device)
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    bf.insert(build_keys)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    allreduce_or_filter(bf) if world > 1 else None
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    bf.finalized = True
+    del build_keys
+
+    # ---- USE_BF probe workload: this rank's slice of the global probe column --------------------
+    keys = rpt_amd.synth_probe_keys(n_probe, n_build, p_permille, start=rank * n_probe, device=device)
+    out_sel = torch.empty(n_probe, dtype=torch.int32, device=device)
+    out_count = torch.zeros(1, dtype=torch.int64, device=device)
+    ws = torch.empty(rpt_amd.load().rpt_probe_workspace_bytes(n_probe), dtype=torch.uint8, device=device)
+    stream = torch.cuda.current_stream(device)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        bf.probe_phase1(keys, ws, n=n_probe)
+        if ev is not None:
+            ev[1].record(stream)
+        bf.probe_phase2(n_probe, out_sel, out_count, ws)
+        if ev is not None:
+            ev[2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - ts
+
+    survivors = int(out_count.item())
+    p1_ms = statistics.mean(e[0].elapsed_time(e[1]) for e in events)
+    probe_ms = statistics.mean(e[0].elapsed_time(e[2]) for e in events)
+
+    t = torch.tensor([elapsed, t1 - t0, t2 - t1], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, insert_s, merge_s = t.tolist()
+
+    if rank == 0:
+        ms_per_step = elapsed / args.steps * 1e3
+        value = world * n_probe * args.steps / elapsed
+        p1_bytes = KEY_BYTES * n_probe
+        achieved = p1_bytes / (p1_ms * 1e-3)
+        probe_bytes = KEY_BYTES * n_probe + SEL_BYTES * survivors
+        line = {
+            "metric": "bloom probe keys/sec (whole node)",
+            "value": value,
+            "unit": "keys/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic: seeded splitmix64 int64 key columns generated on device (SURVEY §8d)",
+            "config": {
+                "workload": (f"C2: USE_BF probe of {n_probe:.0e} int64 keys per GPU against a blocked Bloom filter "
+                             f"built from {n_build:.0e} keys (2^{bf.log_num_blocks} blocks = "
+                             f"{bf.num_blocks * 8 / 2**20:.0f} MiB), p={args.p}"),
+                "probe_rows_per_gpu": n_probe,
+                "build_rows": n_build,
+                "filter_bytes": bf.num_blocks * 8,
+                "pass_fraction": survivors / n_probe,
+                "parallelism": f"row-range shards over {world} GPU(s), filter replicated (RCCL OR-merge)",
+                "job_geomean": "not measured: needs DuckDB v1.4.4 + job.duckdb (SURVEY §8f row 1)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "probe_bits_kernel<I64,dense> (probe phase 1)",
+                "achieved": achieved / 1e9,
+                "peak": HBM_PEAK_BPS / 1e9,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_BPS,
+                "traffic": None,
+                "avg_launch_ms": p1_ms,
+                "algorithmic_bytes_per_launch": p1_bytes,
+            },
+            "probe_total": {
+                "avg_ms": probe_ms,
+                "algorithmic_bytes": probe_bytes,
+                "achieved_GBps": probe_bytes / (probe_ms * 1e-3) / 1e9,
+                "frac": probe_bytes / (probe_ms * 1e-3) / HBM_PEAK_BPS,
+            },
+            "build": {
+                "rows": n_build,
+                "insert_ms": insert_s * 1e3,
+                "insert_keys_per_s": (n_build / world) / insert_s if insert_s > 0 else None,
+                "or_merge_ms": merge_s * 1e3,
+            },
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(n_build, p_permille, int(args.cpu_sample), args.cpu_threads)
+        print(json.dumps(line), flush=True)
+
+    if world > 1:
+        dist.barrier(device_ids=[local])
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,905 @@
+// rpt_gpu.hip — HIP kernels (gfx950) and the C-ABI of librpt_gpu.so (include/rpt_gpu.h).
+//
+// Hot path: PTBloomFilter::Insert / LookupSel (reference src/bloom_filter.cpp:60-78),
+// called per DataChunk by PhysicalCreateBF::Sink (physical_create_bf.cpp:221-227) and
+// PhysicalUseBF::ExecuteInternal (physical_use_bf.cpp:163). Re-designed for MI355X:
+//
+//   insert   : one pass over the key column, 16-B coalesced loads, hash in registers, mask from an
+//              8 KiB LDS table, one device-scope 64-bit atomic OR per key (k2).
+//   probe    : P1 hash + gather + wave ballot -> result bit vector (Arrow Find layout) + one
+//              survivor count per 512-row wave segment;  P2 two-level scan of the counts;
+//              P3 expand bits into an ascending uint32 selection vector (k1).
+//   merge    : OR of partial filters / peer slices (k4);  fold (k3);  popcount.
+//
+// All kernels are persistent grid-stride loops over 512-row wave segments: a wave owns a segment
+// end to end, so P1 needs no barrier after the LDS mask-table fill.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "rpt_bloom_device.hpp"
+#include "rpt_gpu.h"
+#include "rpt_gpu_synth.h"
+
+namespace rpt {
+
+constexpr int kBlockThreads = 256;
+constexpr int kWavesPerBlock = kBlockThreads / 64;
+constexpr uint64_t kSegRows = 512;                 // rows per wave segment (8 per lane)
+constexpr uint64_t kWordsPerSeg = kSegRows / 64;   // result-bit words per segment
+constexpr uint64_t kGroupSegs = 1024;              // segments per scan group
+constexpr int kBlocksPerCU = 8;
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct KeyArgs {
+  const void* keys;
+  const uint32_t* key_sel;
+  const uint64_t* validity;
+  const uint32_t* row_sel;
+};
+
+__device__ __forceinline__ bool valid_at(const uint64_t* validity, uint64_t idx) {
+  return validity == nullptr || ((validity[idx >> 6] >> (idx & 63)) & 1ULL);
+}
+
+// Hashes of the 8 rows a lane owns in a segment.
+//  DENSE   (flat column, no selections, 16-B aligned): row(c, e) = base + c*64*V + lane*V + e,
+//          one 16-byte load per (c): fully coalesced 1 KiB per wave instruction.
+//  GENERAL (dictionary key_sel and/or row_sel):        row(c) = base + c*64 + lane.
+template <int K, bool DENSE>
+__device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uint64_t n, uint32_t lane,
+                                            uint64_t (&h)[8], bool (&ok)[8]) {
+  using Tr = KeyTraits<K>;
+  using T = typename Tr::T;
+  const T* keys = static_cast<const T*>(a.keys);
+  if constexpr (DENSE) {
+    constexpr int V = Tr::kVec;
+#pragma unroll
+    for (int c = 0; c < 8 / V; c++) {
+      const uint64_t row0 = base + static_cast<uint64_t>(c) * 64 * V + static_cast<uint64_t>(lane) * V;
+      T v[V];
+      if (row0 + V <= n) {
+        if constexpr (V == 2) {
+          const u64x2 x = *reinterpret_cast<const u64x2*>(keys + row0);
+          v[0] = static_cast<T>(x[0]);
+          v[1] = static_cast<T>(x[1]);
+        } else {
+          const u32x4 x = *reinterpret_cast<const u32x4*>(keys + row0);
+#pragma unroll
+          for (int e = 0; e < V; e++) v[e] = static_cast<T>(x[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; e++) v[e] = (row0 + e < n) ? keys[row0 + e] : T(0);
+      }
+      uint64_t vw = 0;
+      if (K != kKeyHash && a.validity != nullptr) vw = a.validity[row0 >> 6];  // V | 64: one word
+#pragma unroll
+      for (int e = 0; e < V; e++) {
+        const uint64_t row = row0 + e;
+        ok[c * V + e] = row < n;
+        uint64_t hv = Tr::hash(v[e]);
+        if (K != kKeyHash && a.validity != nullptr && !((vw >> (row & 63)) & 1ULL)) hv = kNullHash;
+        h[c * V + e] = hv;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint64_t i = base + static_cast<uint64_t>(c) * 64 + lane;
+      ok[c] = i < n;
+      uint64_t hv = 0;
+      if (ok[c]) {
+        const uint64_t r = a.row_sel ? a.row_sel[i] : i;
+        const uint64_t k = a.key_sel ? a.key_sel[r] : r;
+        hv = Tr::hash(keys[k]);
+        if (K != kKeyHash && !valid_at(a.validity, k)) hv = kNullHash;
+      }
+      h[c] = hv;
+    }
+  }
+}
+
+// ---- P1: probe -> result bits + per-segment survivor counts ------------------------------------
+template <int K, bool DENSE>
+__global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_t* __restrict__ words,
+                                                                  uint64_t block_mask, KeyArgs a, uint64_t n,
+                                                                  uint64_t n_segs, uint64_t* __restrict__ out_bits,
+                                                                  uint32_t* __restrict__ seg_counts) {
+  __shared__ uint64_t s_masks[kNumMasks];
+  fill_mask_table(s_masks);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6); seg < n_segs;
+       seg += total_waves) {
+    const uint64_t base = seg * kSegRows;
+    uint64_t h[8];
+    bool ok[8];
+    load_hashes<K, DENSE>(a, base, n, lane, h, ok);
+    uint64_t w[8], m[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      m[j] = mask_of(s_masks, h[j]);
+      w[j] = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
+    }
+    uint64_t word[8];
+    uint32_t cnt = 0;
+    if constexpr (DENSE) {
+      constexpr int V = KeyTraits<K>::kVec;
+      uint64_t b[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        b[j] = ballot64(ok[j] && (w[j] & m[j]) == m[j]);
+        cnt += __popcll(b[j]);
+      }
+#pragma unroll
+      for (int c = 0; c < 8 / V; c++) {
+#pragma unroll
+        for (int q = 0; q < V; q++) {
+          uint64_t x = 0;
+          if constexpr (V == 2) {
+            x = spread2(b[c * 2 + 0] >> (32 * q)) | (spread2(b[c * 2 + 1] >> (32 * q)) << 1);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; e++) x |= spread4(b[c * 4 + e] >> (16 * q)) << e;
+          }
+          word[c * V + q] = x;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        word[j] = ballot64(ok[j] && (w[j] & m[j]) == m[j]);
+        cnt += __popcll(word[j]);
+      }
+    }
+    uint64_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) mine = (lane == static_cast<uint32_t>(j)) ? word[j] : mine;
+    if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
+    if (seg_counts != nullptr && lane == 0) seg_counts[seg] = cnt;
+  }
+}
+
+// ---- P2a: survivor count per group of 1024 segments --------------------------------------------
+__global__ __launch_bounds__(kBlockThreads) void group_sum_kernel(const uint32_t* __restrict__ seg_counts,
+                                                                 uint64_t n_segs, uint32_t* __restrict__ group_sums) {
+  __shared__ uint32_t s_part[kWavesPerBlock];
+  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * kGroupSegs + threadIdx.x * 4;
+  uint32_t s = 0;
+  if (first + 4 <= n_segs) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(seg_counts + first);
+    s = v[0] + v[1] + v[2] + v[3];
+  } else {
+    for (uint64_t i = first; i < n_segs && i < first + 4; i++) s += seg_counts[i];
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) group_sums[blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+}
+
+// ---- P2b: exclusive scan of the group sums (one 1024-thread workgroup; <= 8192 groups) ----------
+__global__ __launch_bounds__(1024) void group_scan_kernel(const uint32_t* __restrict__ group_sums, uint32_t n_groups,
+                                                         uint32_t* __restrict__ group_offs,
+                                                         uint64_t* __restrict__ out_count) {
+  __shared__ uint32_t s_wave[16];
+  const uint32_t per = (n_groups + 1023) / 1024;
+  const uint32_t first = threadIdx.x * per;
+  uint32_t local = 0;
+  for (uint32_t i = first; i < first + per && i < n_groups; i++) local += group_sums[i];
+  const uint32_t incl = wave_inclusive_sum(local);
+  const uint32_t wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) s_wave[wave] = incl;
+  __syncthreads();
+  uint32_t wave_off = 0;
+  for (uint32_t w = 0; w < wave; w++) wave_off += s_wave[w];
+  uint32_t run = wave_off + incl - local;
+  for (uint32_t i = first; i < first + per && i < n_groups; i++) {
+    group_offs[i] = run;
+    run += group_sums[i];
+  }
+  if (threadIdx.x == 1023) {
+    uint32_t total = 0;
+    for (int w = 0; w < 16; w++) total += s_wave[w];
+    *out_count = total;
+  }
+}
+
+// ---- P3: expand result bits into an ascending selection vector ----------------------------------
+__global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* __restrict__ bits,
+                                                               const uint32_t* __restrict__ seg_counts, uint64_t n_segs,
+                                                               const uint32_t* __restrict__ group_offs,
+                                                               const uint32_t* __restrict__ row_sel,
+                                                               uint32_t* __restrict__ out_sel) {
+  __shared__ uint32_t s_off[kGroupSegs];
+  __shared__ uint32_t s_wave[kWavesPerBlock];
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kGroupSegs;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t c[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint64_t s = g0 + threadIdx.x * 4 + i;
+    c[i] = s < n_segs ? seg_counts[s] : 0u;
+  }
+  const uint32_t tsum = c[0] + c[1] + c[2] + c[3];
+  const uint32_t incl = wave_inclusive_sum(tsum);
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  uint32_t off = group_offs[blockIdx.x] + incl - tsum;
+  for (uint32_t w = 0; w < wave; w++) off += s_wave[w];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    s_off[threadIdx.x * 4 + i] = off;
+    off += c[i];
+  }
+  __syncthreads();
+  const uint64_t n_words = n_segs * kWordsPerSeg;
+  for (uint32_t b = wave; b < kGroupSegs / 8; b += kWavesPerBlock) {
+    const uint64_t seg0 = g0 + b * 8;
+    if (seg0 >= n_segs) break;
+    const uint64_t wi = seg0 * kWordsPerSeg + lane;
+    uint64_t word = wi < n_words ? bits[wi] : 0ULL;
+    const uint32_t pc = __popcll(word);
+    uint32_t pos = s_off[b * 8] + wave_inclusive_sum(pc) - pc;
+    const uint64_t row_base = wi * 64;
+    while (word) {
+      const uint32_t j = __builtin_ctzll(word);
+      const uint64_t row = row_base + j;
+      out_sel[pos++] = row_sel ? row_sel[row] : static_cast<uint32_t>(row);
+      word &= word - 1;
+    }
+  }
+}
+
+// ---- k2: insert ----------------------------------------------------------------------------------
+template <int K, bool DENSE>
+__global__ __launch_bounds__(kBlockThreads) void insert_kernel(uint64_t* __restrict__ words, uint64_t block_mask,
+                                                              KeyArgs a, uint64_t n, uint64_t n_segs) {
+  __shared__ uint64_t s_masks[kNumMasks];
+  fill_mask_table(s_masks);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6); seg < n_segs;
+       seg += total_waves) {
+    uint64_t h[8];
+    bool ok[8];
+    load_hashes<K, DENSE>(a, seg * kSegRows, n, lane, h, ok);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (ok[j]) {
+        __hip_atomic_fetch_or(words + block_of(h[j], block_mask), mask_of(s_masks, h[j]), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+}
+
+// ---- hashing only (parity / debugging) ---------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(kBlockThreads) void hash_kernel(KeyArgs a, uint64_t n, uint64_t* __restrict__ out) {
+  using Tr = KeyTraits<K>;
+  const typename Tr::T* keys = static_cast<const typename Tr::T*>(a.keys);
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t k = a.key_sel ? a.key_sel[i] : i;
+    uint64_t hv = Tr::hash(keys[k]);
+    if (K != kKeyHash && !valid_at(a.validity, k)) hv = kNullHash;
+    out[i] = hv;
+  }
+}
+
+// ---- k4: OR merge --------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlockThreads) void or_slices_kernel(uint64_t* __restrict__ dst,
+                                                                 const uint64_t* __restrict__ srcs, uint32_t k,
+                                                                 uint64_t n_words, int accumulate) {
+  const uint64_t n_pairs = n_words / 2;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_pairs; i += stride) {
+    u64x2 acc = accumulate ? reinterpret_cast<const u64x2*>(dst)[i] : u64x2{0, 0};
+    for (uint32_t s = 0; s < k; s++) acc |= reinterpret_cast<const u64x2*>(srcs + s * n_words)[i];
+    reinterpret_cast<u64x2*>(dst)[i] = acc;
+  }
+  if ((n_words & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t acc = accumulate ? dst[n_words - 1] : 0ULL;
+    for (uint32_t s = 0; s < k; s++) acc |= srcs[s * n_words + n_words - 1];
+    dst[n_words - 1] = acc;
+  }
+}
+
+// ---- popcount ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlockThreads) void popcount_kernel(const uint64_t* __restrict__ w, uint64_t n_words,
+                                                                unsigned long long* __restrict__ out) {
+  __shared__ uint32_t s_part[kWavesPerBlock];
+  uint32_t s = 0;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_words;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    s += __popcll(w[i]);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(out, static_cast<unsigned long long>(s_part[0]) + s_part[1] + s_part[2] + s_part[3]);
+  }
+}
+
+// ---- synthetic workload (bench / tests) ----------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t sm64(uint64_t seed, uint64_t i) { return mix64(seed + (i + 1) * 0x9e3779b97f4a7c15ULL); }
+
+__global__ __launch_bounds__(kBlockThreads) void synth_build_kernel(int64_t* __restrict__ out, uint64_t start,
+                                                                   uint64_t n) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    out[i] = static_cast<int64_t>(sm64(RPT_SYNTH_SEED_BUILD, start + i));
+}
+
+__global__ __launch_bounds__(kBlockThreads) void synth_probe_kernel(int64_t* __restrict__ out, uint64_t n_build,
+                                                                   uint32_t p_permille, uint64_t start, uint64_t n) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t r = start + i;
+    const uint64_t u = sm64(RPT_SYNTH_SEED_PROBE_SEL, r);
+    out[i] = (n_build > 0 && (u % 1000) < p_permille)
+                 ? static_cast<int64_t>(sm64(RPT_SYNTH_SEED_BUILD, (u >> 20) % n_build))
+                 : static_cast<int64_t>(sm64(RPT_SYNTH_SEED_PROBE_MISS, r));
+  }
+}
+
+}  // namespace rpt
+
+// =================================================================================================
+// Host side
+// =================================================================================================
+struct rpt_bf {
+  int device = 0;
+  int log_num_blocks = 0;
+  uint64_t* words = nullptr;
+  uint64_t alloc_words = 0;
+  uint64_t sized_for_rows = 0;
+  std::atomic<int> has_data{0};
+  std::atomic<int> finalized{0};
+};
+
+namespace {
+
+thread_local std::string t_last_error;
+
+int fail(int status, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  t_last_error = buf;
+  return status;
+}
+
+#define RPT_HIP(expr)                                                                              \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess) return fail(RPT_ERR_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define RPT_LAUNCHED(name)                                                                          \
+  do {                                                                                              \
+    hipError_t e_ = hipGetLastError();                                                              \
+    if (e_ != hipSuccess) return fail(RPT_ERR_HIP, "launch of %s failed: %s", name, hipGetErrorString(e_)); \
+  } while (0)
+
+// Run device work on `device` and restore the caller's current device afterwards.
+struct DeviceGuard {
+  int prev = -1, target;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int d) : target(d) {
+    err = hipGetDevice(&prev);
+    if (err == hipSuccess && prev != d) err = hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0 && prev != target) (void)hipSetDevice(prev);
+  }
+};
+
+#define RPT_ON_DEVICE(dev)                                                                        \
+  DeviceGuard guard_(dev);                                                                        \
+  if (guard_.err != hipSuccess)                                                                   \
+    return fail(RPT_ERR_HIP, "hipSetDevice(%d) failed: %s", (dev), hipGetErrorString(guard_.err))
+
+int num_cus(int device) {
+  static std::mutex mu;
+  static std::vector<int> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  if (device >= static_cast<int>(cache.size())) cache.resize(device + 1, 0);
+  if (cache[device] == 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c <= 0) c = 256;
+    cache[device] = c;
+  }
+  return cache[device];
+}
+
+inline hipStream_t as_stream(rpt_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }
+inline size_t align256(size_t x) { return (x + 255) & ~static_cast<size_t>(255); }
+
+int log_blocks_for_rows(uint64_t n_rows) {
+  const uint64_t bits = std::max<uint64_t>(512, n_rows > (UINT64_MAX >> 4) ? (UINT64_MAX >> 1) : n_rows * 8);
+  int lg = 0;
+  while (lg < 63 && (1ULL << lg) < bits) lg++;
+  return lg - 6;
+}
+
+struct ProbeWorkspace {
+  uint64_t* bits;
+  uint32_t* seg_counts;
+  uint32_t* group_sums;
+  uint32_t* group_offs;
+};
+
+size_t workspace_layout(uint64_t n, void* base, ProbeWorkspace* ws) {
+  const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
+  const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
+  const size_t b0 = align256(n_segs * rpt::kWordsPerSeg * 8);
+  const size_t b1 = align256(n_groups * rpt::kGroupSegs * 4);
+  const size_t b2 = align256(n_groups * 4);
+  if (ws) {
+    char* p = static_cast<char*>(base);
+    ws->bits = reinterpret_cast<uint64_t*>(p);
+    ws->seg_counts = reinterpret_cast<uint32_t*>(p + b0);
+    ws->group_sums = reinterpret_cast<uint32_t*>(p + b0 + b1);
+    ws->group_offs = reinterpret_cast<uint32_t*>(p + b0 + b1 + b2);
+  }
+  return b0 + b1 + 2 * b2;
+}
+
+int check_col(const rpt_key_column* col) {
+  if (!col) return fail(RPT_ERR_INVALID_ARGUMENT, "null key column");
+  if (col->key_type < RPT_KEY_I64 || col->key_type > RPT_KEY_HASH)
+    return fail(RPT_ERR_INVALID_ARGUMENT, "bad key_type %d", col->key_type);
+  if (!col->keys) return fail(RPT_ERR_INVALID_ARGUMENT, "null keys pointer");
+  return RPT_OK;
+}
+
+bool dense_ok(const rpt_key_column* col, const uint32_t* row_sel) {
+  return row_sel == nullptr && col->key_sel == nullptr && (reinterpret_cast<uintptr_t>(col->keys) & 15) == 0;
+}
+
+unsigned persistent_grid(int device, uint64_t n_segs) {
+  const uint64_t want = ceil_div(n_segs, rpt::kWavesPerBlock);
+  const uint64_t cap = static_cast<uint64_t>(num_cus(device)) * rpt::kBlocksPerCU;
+  return static_cast<unsigned>(std::max<uint64_t>(1, std::min(want, cap)));
+}
+
+template <int K, bool D>
+void launch_probe_bits_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
+                         uint64_t n_segs, uint64_t* bits, uint32_t* counts) {
+  hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
+                     (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+}
+
+template <int K, bool D>
+void launch_insert_t(unsigned grid, hipStream_t s, rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n, uint64_t n_segs) {
+  hipLaunchKernelGGL((rpt::insert_kernel<K, D>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
+                     (1ULL << bf->log_num_blocks) - 1, a, n, n_segs);
+}
+
+#define RPT_DISPATCH_KD(fn, kt, dense, ...)                  \
+  do {                                                       \
+    switch (kt) {                                            \
+      case RPT_KEY_I64:                                      \
+        if (dense) fn<rpt::kKeyI64, true>(__VA_ARGS__);      \
+        else fn<rpt::kKeyI64, false>(__VA_ARGS__);           \
+        break;                                               \
+      case RPT_KEY_I32:                                      \
+        if (dense) fn<rpt::kKeyI32, true>(__VA_ARGS__);      \
+        else fn<rpt::kKeyI32, false>(__VA_ARGS__);           \
+        break;                                               \
+      default:                                               \
+        if (dense) fn<rpt::kKeyHash, true>(__VA_ARGS__);     \
+        else fn<rpt::kKeyHash, false>(__VA_ARGS__);          \
+        break;                                               \
+    }                                                        \
+  } while (0)
+
+int alloc_words(rpt_bf* bf, int log_nb) {
+  const uint64_t nw = 1ULL << log_nb;
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, nw * 8);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(RPT_ERR_OUT_OF_MEMORY, "hipMalloc(%llu bytes) failed: %s", static_cast<unsigned long long>(nw * 8),
+                hipGetErrorString(e));
+  }
+  e = hipMemset(p, 0, nw * 8);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return fail(RPT_ERR_HIP, "hipMemset failed: %s", hipGetErrorString(e));
+  }
+  bf->words = static_cast<uint64_t*>(p);
+  bf->alloc_words = nw;
+  bf->log_num_blocks = log_nb;
+  return RPT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rpt_abi_version(void) { return RPT_GPU_ABI_VERSION; }
+
+const char* rpt_status_string(int status) {
+  switch (status) {
+    case RPT_OK: return "ok";
+    case RPT_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case RPT_ERR_HIP: return "HIP runtime error";
+    case RPT_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case RPT_ERR_WORKSPACE: return "workspace too small";
+    case RPT_ERR_SHAPE_MISMATCH: return "filter shape mismatch";
+    default: return "unknown status";
+  }
+}
+
+const char* rpt_last_error(void) { return t_last_error.c_str(); }
+
+int rpt_bf_log_num_blocks_for_rows(uint64_t n_rows) { return log_blocks_for_rows(n_rows); }
+
+int rpt_bf_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows) {
+  if (actual_rows == 0) return 0;
+  const uint64_t min_bits = std::max<uint64_t>(512, sized_for_rows * 12);
+  uint64_t alloc = 1;
+  while (alloc < min_bits) alloc <<= 1;
+  return actual_rows * 8 > alloc ? 1 : 0;
+}
+
+size_t rpt_probe_workspace_bytes(uint64_t n_rows) { return workspace_layout(n_rows, nullptr, nullptr); }
+
+int rpt_bf_create_log_blocks(int device, int log_num_blocks, rpt_bf** out) {
+  if (!out) return fail(RPT_ERR_INVALID_ARGUMENT, "null out");
+  *out = nullptr;
+  if (log_num_blocks < 0 || log_num_blocks > 40) return fail(RPT_ERR_INVALID_ARGUMENT, "log_num_blocks %d", log_num_blocks);
+  RPT_ON_DEVICE(device);
+  rpt_bf* bf = new rpt_bf();
+  bf->device = device;
+  int st = alloc_words(bf, log_num_blocks);
+  if (st != RPT_OK) {
+    delete bf;
+    return st;
+  }
+  *out = bf;
+  return RPT_OK;
+}
+
+int rpt_bf_create(int device, uint64_t est_num_rows, rpt_bf** out) {
+  int st = rpt_bf_create_log_blocks(device, log_blocks_for_rows(est_num_rows), out);
+  if (st == RPT_OK) (*out)->sized_for_rows = est_num_rows;
+  return st;
+}
+
+int rpt_bf_destroy(rpt_bf* bf) {
+  if (!bf) return RPT_OK;
+  {
+    DeviceGuard g(bf->device);
+    if (bf->words) (void)hipFree(bf->words);
+  }
+  delete bf;
+  return RPT_OK;
+}
+
+int rpt_bf_get_info(const rpt_bf* bf, rpt_bf_info* out) {
+  if (!bf || !out) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  out->device = bf->device;
+  out->log_num_blocks = bf->log_num_blocks;
+  out->num_blocks = 1ULL << bf->log_num_blocks;
+  out->sized_for_rows = bf->sized_for_rows;
+  out->has_data = bf->has_data.load();
+  out->finalized = bf->finalized.load();
+  out->words = bf->words;
+  return RPT_OK;
+}
+
+int rpt_bf_reinitialize(rpt_bf* bf, uint64_t actual_rows) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  RPT_ON_DEVICE(bf->device);
+  RPT_HIP(hipDeviceSynchronize());
+  if (bf->words) RPT_HIP(hipFree(bf->words));
+  bf->words = nullptr;
+  int st = alloc_words(bf, log_blocks_for_rows(actual_rows));
+  if (st != RPT_OK) return st;
+  bf->sized_for_rows = actual_rows;
+  bf->has_data.store(0);
+  return RPT_OK;
+}
+
+int rpt_bf_set_finalized(rpt_bf* bf, int value) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  bf->finalized.store(value ? 1 : 0);
+  return RPT_OK;
+}
+
+int rpt_bf_set_has_data(rpt_bf* bf, int value) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  bf->has_data.store(value ? 1 : 0);
+  return RPT_OK;
+}
+
+int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  RPT_ON_DEVICE(bf->device);
+  RPT_HIP(hipMemsetAsync(bf->words, 0, (1ULL << bf->log_num_blocks) * 8, as_stream(stream)));
+  bf->has_data.store(0);
+  return RPT_OK;
+}
+
+int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_t stream) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  if (n == 0) return RPT_OK;  // bloom_filter.cpp:72-74
+  int st = check_col(col);
+  if (st != RPT_OK) return st;
+  RPT_ON_DEVICE(bf->device);
+  bf->has_data.store(1);  // bloom_filter.cpp:75
+  const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
+  const unsigned grid = persistent_grid(bf->device, n_segs);
+  const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  RPT_DISPATCH_KD(launch_insert_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n, n_segs);
+  RPT_LAUNCHED("insert_kernel");
+  return RPT_OK;
+}
+
+int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, uint64_t* out_bits,
+                     rpt_stream_t stream) {
+  if (!bf || !out_bits) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n == 0) return RPT_OK;
+  int st = check_col(col);
+  if (st != RPT_OK) return st;
+  RPT_ON_DEVICE(bf->device);
+  const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
+  const unsigned grid = persistent_grid(bf->device, n_segs);
+  const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n,
+                  n_segs, out_bits, static_cast<uint32_t*>(nullptr));
+  RPT_LAUNCHED("probe_bits_kernel");
+  return RPT_OK;
+}
+
+int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
+                        void* workspace, size_t workspace_bytes, rpt_stream_t stream) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  if (n >= (1ULL << 32)) return fail(RPT_ERR_INVALID_ARGUMENT, "n=%llu rows exceeds uint32 sel_t", (unsigned long long)n);
+  if (n == 0) return RPT_OK;
+  int st = check_col(col);
+  if (st != RPT_OK) return st;
+  const size_t need = rpt_probe_workspace_bytes(n);
+  if (!workspace || workspace_bytes < need)
+    return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
+  RPT_ON_DEVICE(bf->device);
+  ProbeWorkspace ws;
+  workspace_layout(n, workspace, &ws);
+  const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
+  const unsigned grid = persistent_grid(bf->device, n_segs);
+  const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, row_sel};
+  RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense_ok(col, row_sel), grid, as_stream(stream), bf, a, n,
+                  n_segs, ws.bits, ws.seg_counts);
+  RPT_LAUNCHED("probe_bits_kernel");
+  return RPT_OK;
+}
+
+int rpt_bf_probe_phase2(const uint32_t* row_sel, uint64_t n, uint32_t* out_sel, uint64_t* out_count_dev,
+                        void* workspace, size_t workspace_bytes, rpt_stream_t stream) {
+  if (!out_count_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_count");
+  if (n >= (1ULL << 32)) return fail(RPT_ERR_INVALID_ARGUMENT, "n=%llu rows exceeds uint32 sel_t", (unsigned long long)n);
+  hipStream_t s = as_stream(stream);
+  if (n == 0) {  // bloom_filter.cpp:63-65
+    RPT_HIP(hipMemsetAsync(out_count_dev, 0, sizeof(uint64_t), s));
+    return RPT_OK;
+  }
+  if (!out_sel) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_sel");
+  const size_t need = rpt_probe_workspace_bytes(n);
+  if (!workspace || workspace_bytes < need)
+    return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
+  ProbeWorkspace ws;
+  workspace_layout(n, workspace, &ws);
+  const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
+  const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
+  hipLaunchKernelGGL(rpt::group_sum_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,
+                     ws.seg_counts, n_segs, ws.group_sums);
+  RPT_LAUNCHED("group_sum_kernel");
+  hipLaunchKernelGGL(rpt::group_scan_kernel, dim3(1), dim3(1024), 0, s, ws.group_sums,
+                     static_cast<uint32_t>(n_groups), ws.group_offs, out_count_dev);
+  RPT_LAUNCHED("group_scan_kernel");
+  hipLaunchKernelGGL(rpt::compact_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,
+                     ws.bits, ws.seg_counts, n_segs, ws.group_offs, row_sel, out_sel);
+  RPT_LAUNCHED("compact_kernel");
+  return RPT_OK;
+}
+
+int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
+                 uint32_t* out_sel, uint64_t* out_count_dev, void* workspace, size_t workspace_bytes,
+                 rpt_stream_t stream) {
+  if (!bf || !out_count_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  RPT_ON_DEVICE(bf->device);
+  int st = rpt_bf_probe_phase1(bf, col, row_sel, n, workspace, workspace_bytes, stream);
+  if (st != RPT_OK) return st;
+  return rpt_bf_probe_phase2(row_sel, n, out_sel, out_count_dev, workspace, workspace_bytes, stream);
+}
+
+int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, rpt_stream_t stream) {
+  if (!out_hashes) return fail(RPT_ERR_INVALID_ARGUMENT, "null out");
+  if (n == 0) return RPT_OK;
+  int st = check_col(col);
+  if (st != RPT_OK) return st;
+  int dev = 0;
+  RPT_HIP(hipGetDevice(&dev));
+  const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 4096));
+  const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  hipStream_t s = as_stream(stream);
+  switch (col->key_type) {
+    case RPT_KEY_I64: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyI64>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
+    case RPT_KEY_I32: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyI32>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
+    default: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyHash>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
+  }
+  RPT_LAUNCHED("hash_kernel");
+  return RPT_OK;
+}
+
+int rpt_words_or_slices(uint64_t* dst, const uint64_t* srcs, uint32_t k, uint64_t n_words, rpt_stream_t stream) {
+  if (!dst || (!srcs && k > 0)) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_words == 0) return RPT_OK;
+  const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n_words / 2, rpt::kBlockThreads), 8192)));
+  hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), dst, srcs, k,
+                     n_words, 0);
+  RPT_LAUNCHED("or_slices_kernel");
+  return RPT_OK;
+}
+
+int rpt_words_or(uint64_t* dst, const uint64_t* src, uint64_t n_words, rpt_stream_t stream) {
+  if (!dst || !src) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_words == 0) return RPT_OK;
+  const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n_words / 2, rpt::kBlockThreads), 8192)));
+  hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), dst, src, 1u,
+                     n_words, 1);
+  RPT_LAUNCHED("or_slices_kernel");
+  return RPT_OK;
+}
+
+int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
+  if (!dst || !src) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  if (dst->log_num_blocks != src->log_num_blocks || dst->device != src->device)
+    return fail(RPT_ERR_SHAPE_MISMATCH, "merge of log_num_blocks %d (dev %d) with %d (dev %d)", dst->log_num_blocks,
+                dst->device, src->log_num_blocks, src->device);
+  RPT_ON_DEVICE(dst->device);
+  int st = rpt_words_or(dst->words, src->words, 1ULL << dst->log_num_blocks, stream);
+  if (st == RPT_OK && src->has_data.load()) dst->has_data.store(1);
+  return st;
+}
+
+int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out) {
+  if (!bf || !out) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  RPT_ON_DEVICE(bf->device);
+  unsigned long long* d = nullptr;
+  RPT_HIP(hipMalloc(&d, sizeof(unsigned long long)));
+  hipError_t e = hipMemset(d, 0, sizeof(unsigned long long));
+  const uint64_t nw = 1ULL << bf->log_num_blocks;
+  const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(nw, rpt::kBlockThreads), 4096)));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(rpt::popcount_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, nullptr, bf->words, nw, d);
+    e = hipGetLastError();
+  }
+  unsigned long long h = 0;
+  if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(RPT_ERR_HIP, "count_bits: %s", hipGetErrorString(e));
+  *out = h;
+  return RPT_OK;
+}
+
+int rpt_bf_fold(rpt_bf* bf, int* out_new_log_num_blocks) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  RPT_ON_DEVICE(bf->device);
+  RPT_HIP(hipDeviceSynchronize());
+  constexpr int kMinLog = 4;  // bloom_filter.h Fold: log_num_blocks_min
+  for (;;) {
+    if (bf->log_num_blocks <= kMinLog) break;
+    uint64_t set = 0;
+    int st = rpt_bf_count_bits(bf, &set);
+    if (st != RPT_OK) return st;
+    const uint64_t nb = 1ULL << bf->log_num_blocks;
+    const uint64_t num_bits = nb * 64;
+    if (4 * set >= num_bits) break;
+    int folds = 1;
+    while ((bf->log_num_blocks - folds) > kMinLog && (4 * set) < (num_bits >> folds)) ++folds;
+    const uint64_t slice = nb >> folds;
+    // target slice 0 accumulates slices 1 .. 2^folds-1 (they never overlap the target)
+    const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(slice / 2, rpt::kBlockThreads), 8192)));
+    hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, nullptr, bf->words,
+                       bf->words + slice, static_cast<uint32_t>((1u << folds) - 1), slice, 1);
+    RPT_LAUNCHED("or_slices_kernel(fold)");
+    RPT_HIP(hipDeviceSynchronize());
+    bf->log_num_blocks -= folds;
+  }
+  if (out_new_log_num_blocks) *out_new_log_num_blocks = bf->log_num_blocks;
+  return RPT_OK;
+}
+
+int rpt_bf_export_words(const rpt_bf* bf, uint64_t* host_words, uint64_t n_words) {
+  if (!bf || !host_words) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_words != (1ULL << bf->log_num_blocks))
+    return fail(RPT_ERR_SHAPE_MISMATCH, "export of %llu words from a %llu-word filter", (unsigned long long)n_words,
+                (unsigned long long)(1ULL << bf->log_num_blocks));
+  RPT_ON_DEVICE(bf->device);
+  RPT_HIP(hipDeviceSynchronize());
+  RPT_HIP(hipMemcpy(host_words, bf->words, n_words * 8, hipMemcpyDeviceToHost));
+  return RPT_OK;
+}
+
+int rpt_bf_import_words(rpt_bf* bf, const uint64_t* host_words, uint64_t n_words) {
+  if (!bf || !host_words) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_words != (1ULL << bf->log_num_blocks))
+    return fail(RPT_ERR_SHAPE_MISMATCH, "import of %llu words into a %llu-word filter", (unsigned long long)n_words,
+                (unsigned long long)(1ULL << bf->log_num_blocks));
+  RPT_ON_DEVICE(bf->device);
+  RPT_HIP(hipDeviceSynchronize());
+  RPT_HIP(hipMemcpy(bf->words, host_words, n_words * 8, hipMemcpyHostToDevice));
+  int any = 0;
+  for (uint64_t i = 0; i < n_words && !any; i++) any = host_words[i] != 0;
+  bf->has_data.store(any);
+  return RPT_OK;
+}
+
+int rpt_bf_copy_words_to(const rpt_bf* bf, uint64_t* dst_dev, uint64_t n_words, rpt_stream_t stream) {
+  if (!bf || !dst_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_words != (1ULL << bf->log_num_blocks))
+    return fail(RPT_ERR_SHAPE_MISMATCH, "copy of %llu words from a %llu-word filter", (unsigned long long)n_words,
+                (unsigned long long)(1ULL << bf->log_num_blocks));
+  RPT_ON_DEVICE(bf->device);
+  RPT_HIP(hipMemcpyAsync(dst_dev, bf->words, n_words * 8, hipMemcpyDeviceToDevice, as_stream(stream)));
+  return RPT_OK;
+}
+
+int rpt_bf_copy_words_from(rpt_bf* bf, const uint64_t* src_dev, uint64_t n_words, rpt_stream_t stream) {
+  if (!bf || !src_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_words != (1ULL << bf->log_num_blocks))
+    return fail(RPT_ERR_SHAPE_MISMATCH, "copy of %llu words into a %llu-word filter", (unsigned long long)n_words,
+                (unsigned long long)(1ULL << bf->log_num_blocks));
+  RPT_ON_DEVICE(bf->device);
+  RPT_HIP(hipMemcpyAsync(bf->words, src_dev, n_words * 8, hipMemcpyDeviceToDevice, as_stream(stream)));
+  return RPT_OK;
+}
+
+// ---- bench / test workload generators (include/rpt_gpu_synth.h) ---------------------------------
+int rpt_synth_build_keys(int64_t* out, uint64_t start, uint64_t n, rpt_stream_t stream) {
+  if (!out) return fail(RPT_ERR_INVALID_ARGUMENT, "null out");
+  if (n == 0) return RPT_OK;
+  const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 8192));
+  hipLaunchKernelGGL(rpt::synth_build_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), out, start, n);
+  RPT_LAUNCHED("synth_build_kernel");
+  return RPT_OK;
+}
+
+int rpt_synth_probe_keys(int64_t* out, uint64_t n_build, uint32_t p_permille, uint64_t start, uint64_t n,
+                         rpt_stream_t stream) {
+  if (!out) return fail(RPT_ERR_INVALID_ARGUMENT, "null out");
+  if (p_permille > 1000) return fail(RPT_ERR_INVALID_ARGUMENT, "p_permille %u > 1000", p_permille);
+  if (n == 0) return RPT_OK;
+  const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 8192));
+  hipLaunchKernelGGL(rpt::synth_probe_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), out, n_build,
+                     p_permille, start, n);
+  RPT_LAUNCHED("synth_probe_kernel");
+  return RPT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,122 @@
+"""ctypes binding of librpt_gpu.so (the C-ABI declared in include/rpt_gpu.h).
+
+The library is built in-tree (``make -C duckdb-robust-predicate-transfer_amd``) and loaded from
+``duckdb-robust-predicate-transfer_amd/build/librpt_gpu.so``. There is no fallback: if the library
+is missing, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_int32, c_size_t, c_uint32, c_uint64, c_void_p
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "build", "librpt_gpu.so")
+
+RPT_OK = 0
+RPT_ERR_INVALID_ARGUMENT = 1
+RPT_ERR_HIP = 2
+RPT_ERR_OUT_OF_MEMORY = 3
+RPT_ERR_WORKSPACE = 4
+RPT_ERR_SHAPE_MISMATCH = 5
+
+RPT_KEY_I64 = 0
+RPT_KEY_I32 = 1
+RPT_KEY_HASH = 2
+
+
+class RptError(RuntimeError):
+    def __init__(self, status: int, message: str):
+        super().__init__(f"rpt status {status}: {message}")
+        self.status = status
+
+
+class KeyColumn(ctypes.Structure):
+    """rpt_key_column (include/rpt_gpu.h)."""
+
+    _fields_ = [
+        ("key_type", c_int32),
+        ("keys", c_void_p),
+        ("key_sel", c_void_p),
+        ("validity", c_void_p),
+    ]
+
+
+class BfInfo(ctypes.Structure):
+    """rpt_bf_info (include/rpt_gpu.h)."""
+
+    _fields_ = [
+        ("device", c_int32),
+        ("log_num_blocks", c_int32),
+        ("num_blocks", c_uint64),
+        ("sized_for_rows", c_uint64),
+        ("has_data", c_int32),
+        ("finalized", c_int32),
+        ("words", c_void_p),
+    ]
+
+
+# name -> (restype, argtypes); every symbol include/rpt_gpu.h and include/rpt_gpu_synth.h declare.
+SIGNATURES = {
+    "rpt_abi_version": (c_int, []),
+    "rpt_status_string": (c_char_p, [c_int]),
+    "rpt_last_error": (c_char_p, []),
+    "rpt_bf_log_num_blocks_for_rows": (c_int, [c_uint64]),
+    "rpt_bf_needs_resize": (c_int, [c_uint64, c_uint64]),
+    "rpt_probe_workspace_bytes": (c_size_t, [c_uint64]),
+    "rpt_bf_create": (c_int, [c_int, c_uint64, POINTER(c_void_p)]),
+    "rpt_bf_create_log_blocks": (c_int, [c_int, c_int, POINTER(c_void_p)]),
+    "rpt_bf_destroy": (c_int, [c_void_p]),
+    "rpt_bf_get_info": (c_int, [c_void_p, POINTER(BfInfo)]),
+    "rpt_bf_reinitialize": (c_int, [c_void_p, c_uint64]),
+    "rpt_bf_set_finalized": (c_int, [c_void_p, c_int]),
+    "rpt_bf_clear": (c_int, [c_void_p, c_void_p]),
+    "rpt_bf_insert": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p]),
+    "rpt_bf_probe": (
+        c_int,
+        [c_void_p, POINTER(KeyColumn), c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
+    ),
+    "rpt_bf_probe_phase1": (
+        c_int, [c_void_p, POINTER(KeyColumn), c_void_p, c_uint64, c_void_p, c_size_t, c_void_p]
+    ),
+    "rpt_bf_probe_phase2": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rpt_bf_find_bits": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
+    "rpt_hash_keys": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
+    "rpt_bf_merge_or": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "rpt_words_or": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_words_or_slices": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p]),
+    "rpt_bf_count_bits": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "rpt_bf_fold": (c_int, [c_void_p, POINTER(c_int)]),
+    "rpt_bf_export_words": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "rpt_bf_import_words": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "rpt_bf_copy_words_to": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_bf_copy_words_from": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_bf_set_has_data": (c_int, [c_void_p, c_int]),
+    "rpt_synth_build_keys": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
+    "rpt_synth_probe_keys": (c_int, [c_void_p, c_uint64, c_uint32, c_uint64, c_uint64, c_void_p]),
+}
+
+_lib = None
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and return librpt_gpu.so. Raises if it is missing: there is no CPU fallback."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or os.environ.get("RPT_GPU_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise RptError(-1, f"librpt_gpu.so not found at {p}; build it with `make -C {PKG_DIR}`")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int) -> None:
+    if status != RPT_OK:
+        lib = load()
+        raise RptError(status, lib.rpt_last_error().decode(errors="replace"))

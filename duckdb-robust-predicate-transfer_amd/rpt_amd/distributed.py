@@ -1,0 +1,93 @@
+"""Multi-GPU build: per-rank partial filters OR-merged over RCCL (xGMI), one process per GPU.
+
+The reference has no distributed path (DuckDB morsel threads only); this is the
+MI355X-native scale-out of PhysicalCreateBF's parallel sink (physical_create_bf.hpp:43-45):
+
+  * build rows are split by contiguous row range across ranks; every rank sizes its partial filter
+    by the GLOBAL row count, so all partials share log_num_blocks;
+  * OR is commutative and idempotent, so OR-ing the partials gives exactly the single-GPU filter;
+  * RCCL has no bitwise-OR reduction (rccl.h ncclRedOp_t = sum/prod/max/min/avg), so the OR
+    all-reduce is composed as a reduce-scatter by OR + all-gather:
+        1. all_to_all_single: rank j receives slice j of every peer's filter (all xGMI links busy),
+        2. local HIP kernel ORs the W received slices (rpt_words_or_slices),
+        3. all_gather_into_tensor replicates the merged slices.
+    Per-GPU traffic is 2(W-1)/W * S bytes, spread over the point-to-point links.
+  * the probe is sharded by row range with a replicated filter: each rank's ascending local sel plus
+    its row offset, concatenated in rank order, is the global ascending sel — no exchange.
+
+`or_slices` is injectable so the collective choreography runs on CPU (gloo) in tests.
+"""
+from __future__ import annotations
+
+import functools
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+OrSlices = Callable[[torch.Tensor, torch.Tensor, int, int], None]
+
+
+def cpu_or_slices(dst: torch.Tensor, srcs: torch.Tensor, k: int, n_words: int) -> None:
+    """Reference OR of k slices (torch, any device) — used by the gloo tests."""
+    v = srcs[: k * n_words].view(k, n_words)
+    dst[:n_words] = functools.reduce(torch.bitwise_or, [v[i] for i in range(k)])
+
+
+def gpu_or_slices(dst: torch.Tensor, srcs: torch.Tensor, k: int, n_words: int) -> None:
+    from .bloom import words_or_slices
+
+    words_or_slices(dst, srcs, k, n_words)
+
+
+def padded_words(num_words: int, world: int) -> int:
+    """Smallest multiple of `world` >= num_words (filters are 2^k words; world may be any size)."""
+    return ((num_words + world - 1) // world) * world
+
+
+def or_allreduce_words(full: torch.Tensor, group=None, or_slices: Optional[OrSlices] = None) -> None:
+    """In-place bitwise-OR all-reduce of an int64 word tensor whose length is a multiple of world size."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return
+    if full.numel() % world:
+        raise ValueError("word count must be a multiple of the world size (use padded_words)")
+    if or_slices is None:
+        or_slices = gpu_or_slices if full.is_cuda else cpu_or_slices
+    slice_words = full.numel() // world
+    recv = torch.empty_like(full)
+    dist.all_to_all_single(recv, full, group=group)  # recv[j] = peer j's slice <my rank>
+    mine = torch.empty(slice_words, dtype=full.dtype, device=full.device)
+    or_slices(mine, recv, world, slice_words)
+    dist.all_gather_into_tensor(full, mine, group=group)
+
+
+def allreduce_or_filter(bf, group=None) -> None:
+    """OR-merge a BloomFilter across all ranks (all ranks must hold the same log_num_blocks)."""
+    world = dist.get_world_size(group)
+    nw = bf.num_blocks
+    buf = torch.zeros(padded_words(nw, world), dtype=torch.int64, device=bf.device)
+    bf.copy_words_to(buf)
+    or_allreduce_words(buf, group)
+    bf.copy_words_from(buf)
+    flag = torch.tensor([0 if bf.is_empty() else 1], dtype=torch.int64, device=bf.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    bf.set_has_data(bool(flag.item()))
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous row range [lo, hi) of rank `rank` (remainder spread over the first ranks)."""
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def build_sharded(local_keys: torch.Tensor, n_global: int, group=None, **insert_kw):
+    """Per-rank partial filter sized by the global row count, then OR all-reduce."""
+    from .bloom import BloomFilter
+
+    bf = BloomFilter(n_global, device=local_keys.device)
+    if local_keys.numel():
+        bf.insert(local_keys, **insert_kw)
+    allreduce_or_filter(bf, group)
+    return bf

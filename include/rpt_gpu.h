@@ -1,0 +1,171 @@
+/*
+ * rpt_gpu.h — C-ABI of the MI355X-native predicate-transfer Bloom filter (librpt_gpu.so).
+ *
+ * This is the drop-in boundary for the reference's PTBloomFilter seam
+ * (/root/reference/src/include/bloom_filter.hpp:22-57, src/bloom_filter.cpp:11-78): the DuckDB
+ * operators PhysicalCreateBF::Sink/Finalize (src/operators/physical_create_bf.cpp:201-242,352-419)
+ * and PhysicalUseBF::ExecuteInternal (src/operators/physical_use_bf.cpp:60-198) call these entry
+ * points instead of the DuckDB-native BloomFilter. Plain pointers and sizes only; no exceptions
+ * cross the ABI (every entry point returns an rpt_status); device work is enqueued on the caller's
+ * HIP stream and is asynchronous unless stated otherwise.
+ *
+ * Filter spec: the Arrow Acero BlockedBloomFilter the reference README ports (README.md:23-32):
+ * 2^k 64-bit blocks, a 1024-entry table of 57-bit masks (4-5 bits set), mask rotation by hash bits
+ * 10..15, block id from hash bits 16... Key hash: DuckDB VectorOperations::Hash semantics
+ * (MurmurHash64 finalizer; int32 zero-extended through uint32; NULL rows hash to NULL_HASH).
+ *
+ * Key columns follow DuckDB's Vector model (see rpt_key_column):
+ *   FLAT        keys[row]
+ *   DICTIONARY  keys[key_sel[row]]        (validity indexed by the physical index key_sel[row])
+ *   CONSTANT    flatten on the host first (PTBloomFilter's HashColumns flattens, bloom_filter.cpp:19-21)
+ * Validity is DuckDB's ValidityMask layout: uint64 words, bit (i % 64) of word (i / 64) set = valid;
+ * NULL pointer = all rows valid.
+ */
+#ifndef RPT_GPU_H
+#define RPT_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RPT_GPU_ABI_VERSION 1
+
+typedef enum rpt_status {
+  RPT_OK = 0,
+  RPT_ERR_INVALID_ARGUMENT = 1, /* null handle/pointer, bad key type, n too large for uint32 sel */
+  RPT_ERR_HIP = 2,              /* a HIP runtime call failed; rpt_last_error() has the text */
+  RPT_ERR_OUT_OF_MEMORY = 3,    /* device allocation failed */
+  RPT_ERR_WORKSPACE = 4,        /* caller workspace smaller than rpt_probe_workspace_bytes(n) */
+  RPT_ERR_SHAPE_MISMATCH = 5    /* merge of filters with different log_num_blocks / devices */
+} rpt_status;
+
+typedef enum rpt_key_type {
+  RPT_KEY_I64 = 0,  /* BIGINT / int64 keys */
+  RPT_KEY_I32 = 1,  /* INTEGER / int32 keys (JOB join keys) */
+  RPT_KEY_HASH = 2  /* pre-computed 64-bit hashes (HashColumns output); validity/NULLs not applied */
+} rpt_key_type;
+
+/* A hipStream_t, passed opaquely so this header needs no HIP include. NULL = the null stream. */
+typedef void* rpt_stream_t;
+
+/* Opaque filter handle: owns its device memory (PTBloomFilter + its BufferManager allocation,
+ * bloom_filter.hpp:27-28,56; bloom_filter.cpp:27-32). */
+typedef struct rpt_bf rpt_bf;
+
+/* A key column on the device (DuckDB Vector shape; see header comment). */
+typedef struct rpt_key_column {
+  int32_t key_type;         /* rpt_key_type */
+  const void* keys;         /* device pointer */
+  const uint32_t* key_sel;  /* device pointer or NULL (DICTIONARY selection) */
+  const uint64_t* validity; /* device pointer or NULL (all valid) */
+} rpt_key_column;
+
+typedef struct rpt_bf_info {
+  int32_t device;          /* HIP device ordinal the words live on */
+  int32_t log_num_blocks;  /* filter has 2^log_num_blocks uint64 blocks */
+  uint64_t num_blocks;
+  uint64_t sized_for_rows; /* PTBloomFilter::SizedForRows (bloom_filter.hpp:41-43) */
+  int32_t has_data;        /* !PTBloomFilter::IsEmpty (bloom_filter.hpp:45-47) */
+  int32_t finalized;       /* PTBloomFilter::finalized_ (bloom_filter.hpp:30) */
+  uint64_t* words;         /* device pointer to the blocks */
+} rpt_bf_info;
+
+/* ---- library ---------------------------------------------------------------------------- */
+int rpt_abi_version(void);
+const char* rpt_status_string(int status);
+/* Text of the last error raised on the calling thread ("" if none). */
+const char* rpt_last_error(void);
+
+/* ---- host-only sizing rules (no device work) ----------------------------------------------- */
+/* log2 of the block count for a filter sized for n rows: log2ceil(max(512, 8n)) - 6 (Arrow
+ * BlockedBloomFilter::CreateEmpty; the filter PTBloomFilter::Initialize allocates, bloom_filter.cpp:27-32). */
+int rpt_bf_log_num_blocks_for_rows(uint64_t n_rows);
+/* PhysicalCreateBF::Finalize resize rule, verbatim (physical_create_bf.cpp:394-398):
+ * 1 iff actual_rows > 0 and actual_rows*8 > NextPow2(max(512, sized_for_rows*12)). */
+int rpt_bf_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows);
+/* Device workspace the probe needs for n rows (bytes, 256-aligned). */
+size_t rpt_probe_workspace_bytes(uint64_t n_rows);
+
+/* ---- lifecycle --------------------------------------------------------------------------- */
+/* PTBloomFilter::Initialize(context, est_num_rows) (bloom_filter.cpp:27-32): allocate and zero a
+ * filter sized for est_num_rows on `device`. Synchronous. */
+int rpt_bf_create(int device, uint64_t est_num_rows, rpt_bf** out);
+/* Same with an explicit size (2^log_num_blocks blocks, 0 <= log_num_blocks <= 40). */
+int rpt_bf_create_log_blocks(int device, int log_num_blocks, rpt_bf** out);
+int rpt_bf_destroy(rpt_bf* bf);
+int rpt_bf_get_info(const rpt_bf* bf, rpt_bf_info* out);
+/* First half of PTBloomFilter::ReinitializeAndRehash (bloom_filter.cpp:34-43): reallocate for
+ * actual_rows, zero, sized_for_rows = actual_rows, has_data = 0. The caller then re-inserts the
+ * materialized rows with rpt_bf_insert. Synchronous. */
+int rpt_bf_reinitialize(rpt_bf* bf, uint64_t actual_rows);
+/* PTBloomFilter::finalized_ = value (physical_create_bf.cpp:409-413). */
+int rpt_bf_set_finalized(rpt_bf* bf, int value);
+/* Zero every block and clear has_data (stream-ordered). */
+int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
+
+/* ---- build ------------------------------------------------------------------------------- */
+/* PTBloomFilter::Insert (bloom_filter.cpp:70-78): hash each of n rows of `col` and OR its mask into
+ * its block with a device-scope atomic OR. Thread-safe: any number of host threads / streams may
+ * insert into one filter concurrently (parallel Sink, physical_create_bf.hpp:43-45). n == 0 is a
+ * no-op; otherwise has_data becomes 1. */
+int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_t stream);
+
+/* ---- probe ------------------------------------------------------------------------------- */
+/* PTBloomFilter::LookupSel (bloom_filter.cpp:60-68) for a batch of rows: writes the ids of rows
+ * whose key may be in the filter to out_sel in ASCENDING order and the survivor count to
+ * *out_count_dev (device uint64). Rows are 0..n-1, or row_sel[0..n) when row_sel != NULL (the
+ * already-sliced chunk of PhysicalUseBF's multi-filter loop, physical_use_bf.cpp:137-183); the
+ * written ids are then the row_sel values. n must be < 2^32 (sel_t is uint32). out_sel capacity n.
+ * workspace: device memory of rpt_probe_workspace_bytes(n) bytes, exclusively owned by this call
+ * until it completes on `stream`. */
+int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
+                 uint32_t* out_sel, uint64_t* out_count_dev, void* workspace, size_t workspace_bytes,
+                 rpt_stream_t stream);
+/* rpt_bf_probe in its two stream-ordered phases (same workspace, same stream), for callers that
+ * time or overlap them: phase 1 = hash + gather + result bits + per-segment counts (the
+ * HBM-streaming kernel); phase 2 = scan of the counts + expansion into out_sel / *out_count_dev. */
+int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
+                        void* workspace, size_t workspace_bytes, rpt_stream_t stream);
+int rpt_bf_probe_phase2(const uint32_t* row_sel, uint64_t n, uint32_t* out_sel, uint64_t* out_count_dev,
+                        void* workspace, size_t workspace_bytes, rpt_stream_t stream);
+/* Arrow BlockedBloomFilter::Find(…, result_bit_vector) shape: bit i (LSB-first in uint64 words) of
+ * out_bits = row i passes. out_bits must hold ceil(n/512)*8 words. */
+int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, uint64_t* out_bits,
+                     rpt_stream_t stream);
+/* Key hashes exactly as the filter sees them (DuckDB HashColumns restatement). */
+int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, rpt_stream_t stream);
+
+/* ---- merge / fold / export ----------------------------------------------------------------- */
+/* dst |= src (same log_num_blocks, same device): merging per-thread or per-GPU partial filters
+ * built over disjoint row ranges gives the filter of the union, bit-identical to one build. */
+int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream);
+/* dst[i] |= src[i] for n_words words (device pointers): the local step of the multi-GPU
+ * OR all-reduce (reduce-scatter slices). */
+int rpt_words_or(uint64_t* dst, const uint64_t* src, uint64_t n_words, rpt_stream_t stream);
+/* dst[i] = src_0[i] | src_1[i] | ... | src_{k-1}[i], srcs given as k contiguous slices of
+ * n_words words starting at `srcs` (a receive buffer of k peer slices). */
+int rpt_words_or_slices(uint64_t* dst, const uint64_t* srcs, uint32_t k, uint64_t n_words, rpt_stream_t stream);
+/* Number of set bits (BlockedBloomFilter::NumBitsSet). Synchronous. */
+int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out);
+/* BlockedBloomFilter::Fold (bloom_filter.h:135-158): while fewer than 1/4 of the bits are set and
+ * the filter has more than 2^4 blocks, OR its upper slices into the lowest one. Synchronous. */
+int rpt_bf_fold(rpt_bf* bf, int* out_new_log_num_blocks);
+/* Copy the blocks to/from host memory (parity, checkpoint of a finished filter). Synchronous.
+ * import sets has_data = (any bit set). */
+int rpt_bf_export_words(const rpt_bf* bf, uint64_t* host_words, uint64_t n_words);
+int rpt_bf_import_words(rpt_bf* bf, const uint64_t* host_words, uint64_t n_words);
+/* Stream-ordered device-to-device copies of all 2^log_num_blocks blocks to / from a caller buffer
+ * (the staging buffer of the multi-GPU OR all-reduce). n_words must equal the block count. */
+int rpt_bf_copy_words_to(const rpt_bf* bf, uint64_t* dst_dev, uint64_t n_words, rpt_stream_t stream);
+int rpt_bf_copy_words_from(rpt_bf* bf, const uint64_t* src_dev, uint64_t n_words, rpt_stream_t stream);
+/* Mark has_data after words were filled by a device-side exchange (multi-GPU merge). */
+int rpt_bf_set_has_data(rpt_bf* bf, int value);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RPT_GPU_H */

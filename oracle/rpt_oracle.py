@@ -1,0 +1,165 @@
+"""numpy/ctypes front end of the CPU restatement (oracle/rpt_oracle.cpp).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+leg, always as the checker / reported baseline, never as the measured or shipped path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_double, c_int, c_uint8, c_uint32, c_uint64, c_void_p
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "librpt_oracle.so")
+
+_SIG = {
+    "rpt_oracle_mask_table": (None, [c_void_p]),
+    "rpt_oracle_mask": (c_uint64, [c_uint32]),
+    "rpt_oracle_mask_of_hash": (c_uint64, [c_uint64]),
+    "rpt_oracle_log_num_blocks": (c_int, [c_uint64]),
+    "rpt_oracle_needs_resize": (c_int, [c_uint64, c_uint64]),
+    "rpt_oracle_murmur64": (c_uint64, [c_uint64]),
+    "rpt_oracle_null_hash": (c_uint64, []),
+    "rpt_oracle_hash_i64": (None, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_hash_i32": (None, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_insert_hashes": (None, [c_void_p, c_int, c_void_p, c_uint64]),
+    "rpt_oracle_insert_i64": (None, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64]),
+    "rpt_oracle_insert_i32": (None, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64]),
+    "rpt_oracle_find_hashes": (None, [c_void_p, c_int, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_lookup_sel_hashes": (c_uint64, [c_void_p, c_int, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_probe_i64": (c_uint64, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_probe_i32": (c_uint64, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_count_bits": (c_uint64, [c_void_p, c_uint64]),
+    "rpt_oracle_fold": (c_int, [c_void_p, c_int]),
+    "rpt_oracle_sm64": (c_uint64, [c_uint64, c_uint64]),
+    "rpt_oracle_synth_build_keys": (None, [c_uint64, c_uint64, c_void_p]),
+    "rpt_oracle_synth_probe_keys": (None, [c_uint64, c_uint32, c_uint64, c_uint64, c_void_p]),
+    "rpt_oracle_build_mt": (c_double, [c_void_p, c_int, c_void_p, c_uint64, c_int]),
+    "rpt_oracle_probe_mt": (c_double, [c_void_p, c_int, c_void_p, c_uint64, c_int, POINTER(c_uint64)]),
+}
+
+_lib = None
+
+
+def build() -> None:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIG.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data
+
+
+def mask_table() -> bytes:
+    b = (c_uint8 * 136)()
+    lib().rpt_oracle_mask_table(b)
+    return bytes(b)
+
+
+def log_num_blocks(n: int) -> int:
+    return lib().rpt_oracle_log_num_blocks(n)
+
+
+def needs_resize(sized_for: int, actual: int) -> bool:
+    return bool(lib().rpt_oracle_needs_resize(sized_for, actual))
+
+
+def hash_keys(keys: np.ndarray, key_sel=None, validity=None) -> np.ndarray:
+    keys = np.ascontiguousarray(keys)
+    n = key_sel.size if key_sel is not None else keys.size
+    out = np.empty(n, dtype=np.uint64)
+    fn = lib().rpt_oracle_hash_i64 if keys.dtype.itemsize == 8 else lib().rpt_oracle_hash_i32
+    fn(_p(keys), _p(key_sel), _p(validity), n, _p(out))
+    return out
+
+
+def new_words(log_nb: int) -> np.ndarray:
+    return np.zeros(1 << log_nb, dtype=np.uint64)
+
+
+def insert_hashes(words: np.ndarray, log_nb: int, hashes: np.ndarray) -> None:
+    h = np.ascontiguousarray(hashes, dtype=np.uint64)
+    lib().rpt_oracle_insert_hashes(_p(words), log_nb, _p(h), h.size)
+
+
+def insert_keys(words: np.ndarray, log_nb: int, keys: np.ndarray, key_sel=None, validity=None) -> None:
+    keys = np.ascontiguousarray(keys)
+    n = key_sel.size if key_sel is not None else keys.size
+    fn = lib().rpt_oracle_insert_i64 if keys.dtype.itemsize == 8 else lib().rpt_oracle_insert_i32
+    fn(_p(words), log_nb, _p(keys), _p(key_sel), _p(validity), n)
+
+
+def find_hashes(words: np.ndarray, log_nb: int, hashes: np.ndarray) -> np.ndarray:
+    h = np.ascontiguousarray(hashes, dtype=np.uint64)
+    bv = np.zeros((h.size + 7) // 8, dtype=np.uint8)
+    lib().rpt_oracle_find_hashes(_p(words), log_nb, _p(h), h.size, _p(bv))
+    return bv
+
+
+def lookup_sel_hashes(words: np.ndarray, log_nb: int, hashes: np.ndarray) -> np.ndarray:
+    h = np.ascontiguousarray(hashes, dtype=np.uint64)
+    sel = np.empty(max(h.size, 1), dtype=np.uint32)
+    c = lib().rpt_oracle_lookup_sel_hashes(_p(words), log_nb, _p(h), h.size, _p(sel))
+    return sel[:c]
+
+
+def probe_keys(words: np.ndarray, log_nb: int, keys: np.ndarray, key_sel=None, validity=None) -> np.ndarray:
+    keys = np.ascontiguousarray(keys)
+    n = key_sel.size if key_sel is not None else keys.size
+    sel = np.empty(max(n, 1), dtype=np.uint32)
+    fn = lib().rpt_oracle_probe_i64 if keys.dtype.itemsize == 8 else lib().rpt_oracle_probe_i32
+    c = fn(_p(words), log_nb, _p(keys), _p(key_sel), _p(validity), n, _p(sel))
+    return sel[:c]
+
+
+def count_bits(words: np.ndarray) -> int:
+    return int(lib().rpt_oracle_count_bits(_p(words), words.size))
+
+
+def fold(words: np.ndarray, log_nb: int) -> int:
+    return lib().rpt_oracle_fold(_p(words), log_nb)
+
+
+def sm64(seed: int, i: int) -> int:
+    return int(lib().rpt_oracle_sm64(seed, i))
+
+
+def synth_build_keys(n: int, start: int = 0) -> np.ndarray:
+    out = np.empty(max(n, 1), dtype=np.int64)
+    lib().rpt_oracle_synth_build_keys(start, n, _p(out))
+    return out[:n]
+
+
+def synth_probe_keys(n: int, n_build: int, p_permille: int = 100, start: int = 0) -> np.ndarray:
+    out = np.empty(max(n, 1), dtype=np.int64)
+    lib().rpt_oracle_synth_probe_keys(n_build, p_permille, start, n, _p(out))
+    return out[:n]
+
+
+def build_mt(words: np.ndarray, log_nb: int, keys: np.ndarray, threads: int) -> float:
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    return float(lib().rpt_oracle_build_mt(_p(words), log_nb, _p(keys), keys.size, threads))
+
+
+def probe_mt(words: np.ndarray, log_nb: int, keys: np.ndarray, threads: int) -> tuple[float, int]:
+    keys = np.ascontiguousarray(keys, dtype=np.int64)
+    cnt = c_uint64()
+    s = lib().rpt_oracle_probe_mt(_p(words), log_nb, _p(keys), keys.size, threads, ctypes.byref(cnt))
+    return float(s), int(cnt.value)

@@ -1,0 +1,84 @@
+"""C-ABI library checks that need no GPU: it loads, exports every symbol include/*.h declares,
+its host-only rules agree with the oracle, and argument errors are reported (not crashed on)."""
+import ctypes
+import glob
+import os
+import re
+
+import numpy as np
+import pytest
+
+import rpt_oracle as orc
+from conftest import REPO
+from rpt_amd import _lib
+
+
+def declared_functions():
+    names = set()
+    for h in glob.glob(os.path.join(REPO, "include", "*.h")):
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(rpt_\w+)\s*\(", src, flags=re.M))
+    return names
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    declared = declared_functions()
+    assert len(declared) >= 25
+    missing = [n for n in sorted(declared) if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes table binds exactly the declared surface
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+
+
+def test_library_is_gfx950_code_object():
+    path = _lib.LIB_PATH
+    blob = open(path, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_abi_version_and_status_strings():
+    lib = _lib.load()
+    assert lib.rpt_abi_version() == 1
+    assert lib.rpt_status_string(0) == b"ok"
+    assert lib.rpt_status_string(4) == b"workspace too small"
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 100, 129, 1000, 4096, 10**5, 10**6, 10**7, 10**8, 10**9,
+                               8 * 10**9, 2**40])
+def test_sizing_rule_matches_oracle(n):
+    assert _lib.load().rpt_bf_log_num_blocks_for_rows(n) == orc.log_num_blocks(n)
+
+
+def test_resize_rule_matches_oracle():
+    lib = _lib.load()
+    rng = np.random.default_rng(1)
+    for _ in range(2000):
+        s = int(rng.integers(0, 10**8))
+        a = int(rng.integers(0, 10**9))
+        assert lib.rpt_bf_needs_resize(s, a) == orc.lib().rpt_oracle_needs_resize(s, a)
+    for s in [0, 1, 42, 1000, 10**7]:
+        for a in [0, 1, 64, 65, s * 8, s * 12, s * 16, s * 16 + 1]:
+            assert lib.rpt_bf_needs_resize(s, a) == orc.lib().rpt_oracle_needs_resize(s, a)
+
+
+def test_workspace_size_grows_with_rows():
+    lib = _lib.load()
+    prev = 0
+    for n in [1, 512, 513, 10**6, 10**9, 2**32 - 1]:
+        b = lib.rpt_probe_workspace_bytes(n)
+        assert b % 256 == 0 and b >= prev and b >= n // 8
+        prev = b
+
+
+def test_argument_errors_are_reported():
+    lib = _lib.load()
+    col = _lib.KeyColumn(0, None, None, None)
+    assert lib.rpt_bf_insert(None, ctypes.byref(col), 10, None) == _lib.RPT_ERR_INVALID_ARGUMENT
+    assert b"null" in lib.rpt_last_error()
+    assert lib.rpt_bf_probe(None, ctypes.byref(col), None, 10, None, None, None, 0, None) == _lib.RPT_ERR_INVALID_ARGUMENT
+    out = ctypes.c_void_p()
+    assert lib.rpt_bf_create_log_blocks(0, 41, ctypes.byref(out)) == _lib.RPT_ERR_INVALID_ARGUMENT
+    assert lib.rpt_bf_destroy(None) == 0
+    assert lib.rpt_synth_probe_keys(None, 1, 10, 0, 10, None) == _lib.RPT_ERR_INVALID_ARGUMENT

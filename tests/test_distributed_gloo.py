@@ -1,0 +1,87 @@
+"""Multi-process (gloo, CPU) tests of the multi-GPU choreography in rpt_amd.distributed:
+row-range sharding, the OR all-reduce composed from all_to_all + local OR + all_gather, and the
+"OR of partials == single build" invariant, with the oracle doing the per-rank filter work."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, REPO
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_build, q):
+    import sys
+
+    for p in (PKG, os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")):
+        sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import rpt_oracle as orc
+        from rpt_amd.distributed import cpu_or_slices, or_allreduce_words, padded_words, shard_range
+
+        lnb = orc.log_num_blocks(n_build)  # every rank sizes by the GLOBAL row count
+        lo, hi = shard_range(n_build, rank, world)
+        words = orc.new_words(lnb)
+        orc.insert_keys(words, lnb, orc.synth_build_keys(hi - lo, start=lo))
+        buf = torch.zeros(padded_words(words.size, world), dtype=torch.int64)
+        buf[: words.size] = torch.from_numpy(words.view(np.int64))
+        or_allreduce_words(buf, or_slices=cpu_or_slices)
+        merged = buf[: words.size].numpy().view(np.uint64)
+        # probe sharded by row range with the replicated filter: local sel + offset
+        n_probe = 40000
+        plo, phi = shard_range(n_probe, rank, world)
+        keys = orc.synth_probe_keys(phi - plo, n_build, 250, start=plo)
+        sel = orc.probe_keys(merged, lnb, keys).astype(np.int64) + plo
+        gathered = [None] * world
+        dist.all_gather_object(gathered, sel.tolist())
+        if rank == 0:
+            q.put((merged.copy(), np.concatenate([np.array(g, dtype=np.int64) for g in gathered])))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_build_or_merge_and_probe(world):
+    n_build = 30011
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_build, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    merged, sel = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+
+    import rpt_oracle as orc
+
+    lnb = orc.log_num_blocks(n_build)
+    single = orc.new_words(lnb)
+    orc.insert_keys(single, lnb, orc.synth_build_keys(n_build))
+    assert np.array_equal(merged, single)  # bit-identical to the 1-GPU build
+    ref = orc.probe_keys(single, lnb, orc.synth_probe_keys(40000, n_build, 250)).astype(np.int64)
+    assert np.array_equal(sel, ref)  # concatenated per-rank sel == global ascending sel
+
+
+def test_shard_range_partitions_rows():
+    from rpt_amd.distributed import padded_words, shard_range
+
+    for n in [0, 1, 7, 1000, 10**7 + 3]:
+        for w in [1, 2, 3, 8]:
+            rs = [shard_range(n, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
+            assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+    assert padded_words(1 << 21, 8) == 1 << 21 and padded_words(16, 3) == 18

@@ -1,0 +1,261 @@
+"""HIP path (librpt_gpu.so on cuda:0) vs the oracle and the Arrow golden vectors. Bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+import rpt_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+KEY_CASES = ["kat16", "raw_hash_100k", "k64_n1", "k64_n100", "k64_n1000", "k64_n50000", "k64_n300000",
+             "k32_n5000", "k64_n3000_nulls7", "k32_n3000_nulls5", "k64_n20000_over"]
+
+
+@pytest.fixture(scope="module")
+def rpt():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test run without a visible GPU")
+    import rpt_amd
+
+    rpt_amd.load()
+    torch.cuda.set_device(0)
+    return rpt_amd
+
+
+def dev(a: np.ndarray) -> torch.Tensor:
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+
+
+def bits_of(words: torch.Tensor, n: int) -> np.ndarray:
+    w = words.cpu().numpy().view(np.uint64)
+    return np.unpackbits(w.view(np.uint8), bitorder="little")[:n].astype(bool)
+
+
+@pytest.mark.parametrize("case", KEY_CASES)
+def test_golden_hash_path(rpt, golden, case):
+    c = golden.cases[case]
+    h, p, _ = golden.inputs(case)
+    bf = rpt.BloomFilter(log_num_blocks=c["log_num_blocks"])
+    bf.insert(dev(h), key_type=rpt.RPT_KEY_HASH)
+    torch.cuda.synchronize()
+    assert np.array_equal(bf.export_words(), golden.words(case))
+    assert bf.count_bits() == c["num_bits_set"]
+    ref = golden.find_bits(case, p.size)
+    assert np.array_equal(bits_of(bf.find_bits(dev(p), key_type=rpt.RPT_KEY_HASH), p.size), ref)
+    sel = bf.lookup_sel(dev(p), key_type=rpt.RPT_KEY_HASH).cpu().numpy()
+    assert np.array_equal(sel, np.flatnonzero(ref).astype(np.int32))
+
+
+@pytest.mark.parametrize("case", [k for k in KEY_CASES if k.startswith("k") and k != "kat16"])
+def test_golden_key_path(rpt, golden, case):
+    c = golden.cases[case]
+    _, _, kc = golden.inputs(case)
+    bf = rpt.BloomFilter(kc.size_rows)
+    assert bf.log_num_blocks == c["log_num_blocks"]
+    v = dev(gu.validity_words(kc.valid)) if kc.valid is not None else None
+    bf.insert(dev(kc.keys), validity=v)
+    assert np.array_equal(bf.export_words(), golden.words(case))
+    pv = dev(gu.validity_words(kc.probe_valid)) if kc.probe_valid is not None else None
+    sel = bf.lookup_sel(dev(kc.probe), validity=pv).cpu().numpy()
+    assert np.array_equal(sel, np.flatnonzero(golden.find_bits(case, kc.probe.size)).astype(np.int32))
+    assert np.array_equal(rpt.hash_keys(dev(kc.probe), validity=pv).cpu().numpy().view(np.uint64),
+                          kc.hashes(kc.probe, kc.probe_valid))
+
+
+@pytest.mark.parametrize("case", ["fold_200k_dup1000", "fold_100k_3keys", "fold_dense_noop"])
+def test_golden_fold(rpt, golden, case):
+    c = golden.cases[case]
+    h, p, _ = golden.inputs(case)
+    bf = rpt.BloomFilter(golden.size_rows(case))
+    bf.insert(dev(h), key_type=rpt.RPT_KEY_HASH)
+    assert bf.fold() == c["log_num_blocks"]
+    assert np.array_equal(bf.export_words(), golden.words(case))
+    if p is not None:
+        assert np.array_equal(bits_of(bf.find_bits(dev(p), key_type=rpt.RPT_KEY_HASH), p.size),
+                              golden.find_bits(case, p.size))
+
+
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+@pytest.mark.parametrize("n", [0, 1, 7, 511, 512, 513, 2048, 100003])
+def test_ragged_sizes_vs_oracle(rpt, dtype, n):
+    rng = np.random.default_rng(n + (dtype == np.int32))
+    build = rng.integers(-2**31, 2**31, size=max(n // 3, 1), dtype=np.int64).astype(dtype)
+    probe = np.concatenate([build[: n // 2], rng.integers(-2**31, 2**31, size=n - n // 2).astype(dtype)])
+    rng.shuffle(probe)
+    lnb = orc.log_num_blocks(build.size)
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, build)
+    bf = rpt.BloomFilter(build.size)
+    bf.insert(dev(build))
+    assert np.array_equal(bf.export_words(), w)
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32) if n else np.zeros(0, np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, lnb, probe))
+
+
+def test_dictionary_validity_rowsel_vs_oracle(rpt):
+    rng = np.random.default_rng(7)
+    dict_vals = rng.integers(-10**12, 10**12, size=3000, dtype=np.int64)
+    n = 20000
+    key_sel = rng.integers(0, dict_vals.size, size=n).astype(np.uint32)
+    valid = rng.random(dict_vals.size) > 0.05
+    vw = gu.validity_words(valid)
+    lnb = orc.log_num_blocks(n)
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, dict_vals, key_sel=key_sel[:5000], validity=vw)
+    bf = rpt.BloomFilter(n)
+    bf.insert(dev(dict_vals), key_sel=dev(key_sel[:5000]), validity=dev(vw))
+    assert np.array_equal(bf.export_words(), w)
+    # probe a dictionary vector through a row selection (an already-sliced chunk)
+    row_sel = np.sort(rng.choice(n, size=12000, replace=False)).astype(np.uint32)
+    ref_rows = set(orc.probe_keys(w, lnb, dict_vals, key_sel=key_sel, validity=vw).tolist())
+    exp = np.array([r for r in row_sel if r in ref_rows], dtype=np.uint32)
+    got = bf.lookup_sel(dev(dict_vals), key_sel=dev(key_sel), validity=dev(vw), row_sel=dev(row_sel))
+    assert np.array_equal(got.cpu().numpy().view(np.uint32), exp)
+
+
+def test_unaligned_column_takes_general_path(rpt):
+    keys = orc.synth_build_keys(5001)
+    bf = rpt.BloomFilter(5000)
+    t = dev(keys)
+    bf.insert(t[1:])  # 8-byte aligned, not 16: GENERAL loads
+    lnb = orc.log_num_blocks(5000)
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, keys[1:])
+    assert np.array_equal(bf.export_words(), w)
+    probe = orc.synth_probe_keys(7001, 5001, 300)
+    sel = bf.lookup_sel(dev(probe)[1:]).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, lnb, probe[1:]))
+
+
+def test_multi_filter_chain_is_and(rpt):
+    """PhysicalUseBF's loop (physical_use_bf.cpp:137-183): each filter probes the previous slice."""
+    rng = np.random.default_rng(3)
+    a_keys = rng.integers(0, 10**6, size=30000, dtype=np.int64)
+    b_keys = rng.integers(0, 10**6, size=30000, dtype=np.int32)
+    fa_keys = rng.integers(0, 10**6, size=20000, dtype=np.int64)
+    fb_keys = rng.integers(0, 10**6, size=5000, dtype=np.int32)
+    fa, fb = rpt.BloomFilter(fa_keys.size), rpt.BloomFilter(fb_keys.size)
+    fa.insert(dev(fa_keys))
+    fb.insert(dev(fb_keys))
+    s1 = fa.lookup_sel(dev(a_keys))
+    s2 = fb.lookup_sel(dev(b_keys), row_sel=s1)
+    la, lb = orc.log_num_blocks(fa_keys.size), orc.log_num_blocks(fb_keys.size)
+    wa, wb = orc.new_words(la), orc.new_words(lb)
+    orc.insert_keys(wa, la, fa_keys)
+    orc.insert_keys(wb, lb, fb_keys)
+    exp = np.intersect1d(orc.probe_keys(wa, la, a_keys), orc.probe_keys(wb, lb, b_keys))
+    assert np.array_equal(s2.cpu().numpy().view(np.uint32), exp)
+
+
+def test_merge_of_partials_equals_single_build(rpt):
+    keys = orc.synth_build_keys(300000)
+    whole = rpt.BloomFilter(keys.size)
+    whole.insert(dev(keys))
+    parts = [rpt.BloomFilter(keys.size) for _ in range(4)]
+    for i, p in enumerate(parts):
+        lo, hi = i * 75000, (i + 1) * 75000
+        p.insert(dev(keys[lo:hi]))
+    for p in parts[1:]:
+        parts[0].merge_or(p)
+    assert np.array_equal(parts[0].export_words(), whole.export_words())
+    # slice OR kernel (the local step of the multi-GPU all-reduce)
+    nw = whole.num_blocks
+    stack = torch.cat([torch.from_numpy(p.export_words().view(np.int64)) for p in parts[1:]]).cuda()
+    dst = torch.zeros(nw, dtype=torch.int64, device="cuda")
+    rpt.words_or_slices(dst, stack, 3, nw)
+    ref = parts[1].export_words() | parts[2].export_words() | parts[3].export_words()
+    assert np.array_equal(dst.cpu().numpy().view(np.uint64), ref)
+
+
+def test_concurrent_inserts_on_two_streams(rpt):
+    keys = orc.synth_build_keys(400000)
+    bf = rpt.BloomFilter(keys.size)
+    t = dev(keys)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    bf.insert(t[:200000], stream=s1)
+    bf.insert(t[200000:], stream=s2)
+    torch.cuda.synchronize()
+    lnb = orc.log_num_blocks(keys.size)
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, keys)
+    assert np.array_equal(bf.export_words(), w)
+
+
+def test_empty_filter_and_empty_input(rpt):
+    bf = rpt.BloomFilter(1000)
+    assert bf.is_empty()
+    probe = dev(orc.synth_probe_keys(10000, 1000, 500))
+    assert bf.lookup_sel(probe).numel() == 0  # empty filter: no survivors (physical_use_bf.cpp:144-155)
+    bf.insert(probe[:0])
+    assert bf.is_empty()  # zero-row insert keeps IsEmpty (bloom_filter.cpp:72-74)
+    bf.insert(probe[:1])
+    assert not bf.is_empty()
+    assert bf.lookup_sel(probe[:0]).numel() == 0
+
+
+def test_reinitialize_and_rehash_resize_rule(rpt):
+    """PhysicalCreateBF::Finalize: undersized filter -> ReinitializeAndRehash(actual) (cpp:386-406)."""
+    est, actual = 1000, 50000
+    keys = orc.synth_build_keys(actual)
+    bf = rpt.BloomFilter(est)
+    chunks = [dict(keys=dev(keys[i:i + 2048])) for i in range(0, actual, 2048)]
+    for ch in chunks:
+        bf.insert(**ch)
+    assert rpt.needs_resize(bf.sized_for_rows(), actual)
+    bf.reinitialize_and_rehash(actual, chunks)
+    assert bf.sized_for_rows() == actual and bf.log_num_blocks == orc.log_num_blocks(actual)
+    lnb = orc.log_num_blocks(actual)
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, keys)
+    assert np.array_equal(bf.export_words(), w)
+
+
+def test_synthetic_generators_match_oracle(rpt):
+    b = rpt.synth_build_keys(100000, start=123).cpu().numpy()
+    assert np.array_equal(b, orc.synth_build_keys(100000, start=123))
+    p = rpt.synth_probe_keys(100000, 10**7, 100, start=10**9 - 100000).cpu().numpy()
+    assert np.array_equal(p, orc.synth_probe_keys(100000, 10**7, 100, start=10**9 - 100000))
+
+
+def _window_check(bf, w, lnb, probe_dev, sel, lo, hi):
+    win = probe_dev[lo:hi].cpu().numpy()
+    exp = orc.probe_keys(w, lnb, win).astype(np.int64) + lo
+    a = np.searchsorted(sel, lo)
+    b = np.searchsorted(sel, hi)
+    assert np.array_equal(sel[a:b], exp)
+
+
+@pytest.mark.parametrize("n_probe,n_build,p", [(10**8, 10**7, 100), (10**9, 10**7, 100)])
+def test_full_size_probe_properties(rpt, n_probe, n_build, p):
+    """BASELINE sizes: sortedness, count == popcount(find bits), windows vs oracle, no false negatives."""
+    build = rpt.synth_build_keys(n_build)
+    bf = rpt.BloomFilter(n_build)
+    bf.insert(build)
+    lnb = bf.log_num_blocks
+    w = bf.export_words()
+    # oracle builds the same filter from the same stream
+    ow = orc.new_words(lnb)
+    orc.insert_keys(ow, lnb, orc.synth_build_keys(n_build))
+    assert np.array_equal(w, ow)
+    assert bf.lookup_sel(build).numel() == n_build  # no false negatives
+    probe = rpt.synth_probe_keys(n_probe, n_build, p)
+    sel_t, cnt = bf.probe_async(probe)
+    count = int(cnt.item())
+    bits = bf.find_bits(probe)
+    pop = int(np.bitwise_count(bits.cpu().numpy().view(np.uint64)).sum())
+    assert count == pop
+    sel = sel_t[:count]  # int32: n_probe < 2^31
+    assert bool((sel[1:] > sel[:-1]).all())
+    sel_np = sel.cpu().numpy().astype(np.int64)
+    for lo, hi in [(0, 10**6), (n_probe // 2 - 777, n_probe // 2 + 10**6), (n_probe - 10**6, n_probe)]:
+        _window_check(bf, w, lnb, probe, sel_np, lo, hi)
+    rate = count / n_probe
+    assert p / 1000 < rate < p / 1000 + 0.05
+    del probe, sel_t, bits, sel
+    torch.cuda.empty_cache()
