@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=float, default=1e8, help="probe rows in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--strategy", default="auto", choices=["auto", "gather", "lds", "partitioned"],
+                    help="probe strategy (auto picks by filter size)")
     return ap.parse_args()
 
 
@@ -123,13 +125,15 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     bf.finalized = True
+    bf.probe_strategy = {"auto": 0, "gather": 1, "lds": 2, "partitioned": 3}[args.strategy]
+    strategy_name = {1: "gather", 2: "lds", 3: "partitioned"}[bf.probe_strategy]
     del build_keys
 
     # ---- USE_BF probe workload: this rank's slice of the global probe column --------------------
     keys = rpt_amd.synth_probe_keys(n_probe, n_build, p_permille, start=rank * n_probe, device=device)
     out_sel = torch.empty(n_probe, dtype=torch.int32, device=device)
     out_count = torch.zeros(1, dtype=torch.int64, device=device)
-    ws = torch.empty(rpt_amd.load().rpt_probe_workspace_bytes(n_probe), dtype=torch.uint8, device=device)
+    ws = torch.empty(bf.workspace_bytes(n_probe), dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream(device)
 
     def step(ev=None):
@@ -192,11 +196,12 @@ def main():
                 "filter_bytes": bf.num_blocks * 8,
                 "pass_fraction": survivors / n_probe,
                 "parallelism": f"row-range shards over {world} GPU(s), filter replicated (RCCL OR-merge)",
+                "probe_strategy": strategy_name,
                 "job_geomean": "not measured: needs DuckDB v1.4.4 + job.duckdb (SURVEY §8f row 1)",
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "probe_bits_kernel<I64,dense> (probe phase 1)",
+                "kernel": f"probe phase 1 ({strategy_name} strategy)",
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK_BPS / 1e9,
                 "unit": "GB/s",

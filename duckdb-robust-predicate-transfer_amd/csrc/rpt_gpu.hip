@@ -37,6 +37,19 @@ constexpr uint64_t kWordsPerSeg = kSegRows / 64;   // result-bit words per segme
 constexpr uint64_t kGroupSegs = 1024;              // segments per scan group
 constexpr int kBlocksPerCU = 8;
 
+// Partitioned ("routed") probe: the filter is cut into 64 KiB slices that fit in LDS; probe rows are
+// bucketed by slice per 16 Ki-row tile so that every filter access is an LDS read.
+constexpr int kSliceLog = 13;                          // 2^13 blocks = 64 KiB per slice
+constexpr uint64_t kSliceWords = 1ULL << kSliceLog;
+constexpr int kMaxSliceCount = 256;                    // P <= 256 slices (filters <= 16 MiB)
+constexpr uint64_t kTileRows = 16384;                  // rows per partition tile
+constexpr int kTileThreads = 1024;                     // 16 waves x 1024 rows
+constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
+constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
+#ifndef RPT_PARTITION_MIN_WAVES
+#define RPT_PARTITION_MIN_WAVES 8                      // 2 partition workgroups per CU (64 VGPRs)
+#endif
+
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -110,13 +123,18 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
 }
 
 // ---- P1: probe -> result bits + per-segment survivor counts ------------------------------------
-template <int K, bool DENSE>
+// FILTER_IN_LDS: the whole filter (<= 64 KiB) is staged in LDS and every gather is an LDS read.
+template <int K, bool DENSE, bool FILTER_IN_LDS>
 __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_t* __restrict__ words,
                                                                   uint64_t block_mask, KeyArgs a, uint64_t n,
                                                                   uint64_t n_segs, uint64_t* __restrict__ out_bits,
                                                                   uint32_t* __restrict__ seg_counts) {
   __shared__ uint64_t s_masks[kNumMasks];
+  extern __shared__ uint64_t s_filter[];
   fill_mask_table(s_masks);
+  if constexpr (FILTER_IN_LDS) {
+    for (uint64_t i = threadIdx.x; i <= block_mask; i += blockDim.x) s_filter[i] = words[i];
+  }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
@@ -130,7 +148,11 @@ __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       m[j] = mask_of(s_masks, h[j]);
-      w[j] = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
+      if constexpr (FILTER_IN_LDS) {
+        w[j] = s_filter[block_of(h[j], block_mask)];
+      } else {
+        w[j] = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
+      }
     }
     uint64_t word[8];
     uint32_t cnt = 0;
@@ -168,6 +190,227 @@ __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_
     for (int j = 0; j < 8; j++) mine = (lane == static_cast<uint32_t>(j)) ? word[j] : mine;
     if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
     if (seg_counts != nullptr && lane == 0) seg_counts[seg] = cnt;
+  }
+}
+
+// ---- partitioned probe, A: bucket a 16 Ki-row tile by filter slice --------------------------------
+// Row r of the tile gets record rec = (uint32)hash (mask id, rotation and block-in-slice bits) stored
+// at position pos(r) of the tile's slice-sorted record array; pos(r) is written per row (u16) so the
+// unpermute step can restore row order; per (slice, tile) the run (start << 16 | count) is written
+// slice-major for the slice kernel.
+template <int K, bool DENSE>
+__global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(KeyArgs a, uint64_t n, uint32_t slice_mask,
+                                                                uint64_t n_tiles, uint32_t* __restrict__ recs,
+                                                                uint16_t* __restrict__ pos_out,
+                                                                uint32_t* __restrict__ runs) {
+  __shared__ uint32_t s_rec[kTileRows];
+  __shared__ uint32_t s_cnt[kMaxSliceCount];
+  __shared__ uint32_t s_base[kMaxSliceCount];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t n_slices = slice_mask + 1;
+  for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    if (threadIdx.x < kMaxSliceCount) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t tile_base = tile * kTileRows;
+    // per row: rec = low 32 hash bits; key = slice << 16 | rank-in-slice (0xFFFFFFFF: row >= n)
+    uint32_t rec[16], key[16];
+#pragma unroll
+    for (int sg = 0; sg < 2; sg++) {
+      uint64_t hh[8];
+      bool oo[8];
+      load_hashes<K, DENSE>(a, tile_base + wave * 1024 + sg * kSegRows, n, lane, hh, oo);
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
+        rec[sg * 8 + j] = static_cast<uint32_t>(hh[j]);
+        key[sg * 8 + j] = oo[j] ? ((sl << 16) | atomicAdd(&s_cnt[sl], 1u)) : 0xFFFFFFFFu;
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {  // exclusive scan of <= 256 slice counts: 4 per lane
+      uint32_t c[4], t = 0;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t idx = lane * 4 + i;
+        c[i] = idx < n_slices ? s_cnt[idx] : 0u;
+        t += c[i];
+      }
+      uint32_t off = wave_inclusive_sum(t) - t;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        s_base[lane * 4 + i] = off;
+        off += c[i];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sg = 0; sg < 2; sg++) {
+      const uint64_t base = tile_base + wave * 1024 + sg * kSegRows;
+      uint16_t pv[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t kk = key[sg * 8 + j];
+        uint32_t p = 0;
+        if (kk != 0xFFFFFFFFu) {
+          p = s_base[kk >> 16] + (kk & 0xFFFFu);
+          s_rec[p] = rec[sg * 8 + j];
+        }
+        pv[j] = static_cast<uint16_t>(p);
+      }
+      // pos is padded to whole tiles: rows >= n get don't-care values.
+      if constexpr (DENSE) {
+        constexpr int V = KeyTraits<K>::kVec;
+#pragma unroll
+        for (int c = 0; c < 8 / V; c++) {
+          const uint64_t row0 = base + static_cast<uint64_t>(c) * 64 * V + static_cast<uint64_t>(lane) * V;
+          if constexpr (V == 2) {
+            *reinterpret_cast<uint32_t*>(pos_out + row0) =
+                static_cast<uint32_t>(pv[c * 2]) | (static_cast<uint32_t>(pv[c * 2 + 1]) << 16);
+          } else {
+            *reinterpret_cast<uint64_t*>(pos_out + row0) =
+                static_cast<uint64_t>(pv[c * 4]) | (static_cast<uint64_t>(pv[c * 4 + 1]) << 16) |
+                (static_cast<uint64_t>(pv[c * 4 + 2]) << 32) | (static_cast<uint64_t>(pv[c * 4 + 3]) << 48);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; c++) pos_out[base + c * 64 + lane] = pv[c];
+      }
+    }
+    __syncthreads();
+    const uint64_t tile_rows = (tile_base + kTileRows <= n) ? kTileRows : (n - tile_base);
+    u32x4* dst = reinterpret_cast<u32x4*>(recs + tile_base);
+    const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
+    for (uint32_t i = threadIdx.x; i < (tile_rows + 3) / 4; i += kTileThreads) dst[i] = src[i];
+    if (threadIdx.x < n_slices)
+      runs[static_cast<uint64_t>(threadIdx.x) * n_tiles + tile] = (s_base[threadIdx.x] << 16) | s_cnt[threadIdx.x];
+    __syncthreads();
+  }
+}
+
+// ---- partitioned probe, B: one workgroup per (slice, tile range) probes its records from LDS -------
+__device__ __forceinline__ uint8_t probe_rec(const uint64_t* s_slice, const uint64_t* s_masks, uint32_t rec) {
+  const uint64_t m = rotl64(s_masks[rec & (kNumMasks - 1)], (rec >> kLogNumMasks) & 63u);
+  const uint64_t w = s_slice[(rec >> (kLogNumMasks + 6)) & (kSliceWords - 1)];
+  return (w & m) == m ? 1 : 0;
+}
+
+// The runs of 64 consecutive tiles are walked as ONE flattened record stream per wave: record k of
+// the stream belongs to the tile whose inclusive run-length prefix first exceeds k. The (uniform)
+// tile cursor advances in scalar registers, so every load covers 64 consecutive records (coalesced
+// except at run boundaries) and kUnroll loads are in flight per wave.
+__global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64_t* __restrict__ words,
+                                                                   uint32_t splits, uint64_t n_tiles,
+                                                                   const uint32_t* __restrict__ recs,
+                                                                   const uint32_t* __restrict__ runs,
+                                                                   uint8_t* __restrict__ passb) {
+  constexpr int kUnroll = 8;
+  __shared__ uint64_t s_slice[kSliceWords];
+  __shared__ uint64_t s_masks[kNumMasks];
+  const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
+  const uint64_t t_lo = n_tiles * part / splits, t_hi = n_tiles * (part + 1) / splits;
+  {
+    const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(slice) * kSliceWords);
+    u64x2* dst = reinterpret_cast<u64x2*>(s_slice);
+    for (uint32_t i = threadIdx.x; i < kSliceWords / 2; i += kSliceThreads) dst[i] = src[i];
+  }
+  fill_mask_table(s_masks);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr uint32_t kWaves = kSliceThreads / 64;
+  const uint32_t* my_runs = runs + static_cast<uint64_t>(slice) * n_tiles;
+  for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
+    const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
+    const uint32_t cnt = info & 0xFFFFu;
+    const uint64_t base = (tb + lane) * kTileRows + (info >> 16);
+    const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
+    const uint32_t incl = wave_inclusive_sum(cnt);
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    uint32_t j = 0;  // uniform: first tile of the batch whose inclusive prefix exceeds the group start
+    for (uint32_t k0 = 0; k0 < total; k0 += 64 * kUnroll) {
+      uint64_t addr[kUnroll];
+      uint32_t rec[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        const uint32_t kf = k0 + u * 64;
+        const uint32_t k = kf + lane;
+        addr[u] = ~0ULL;
+        if (kf < total) {
+          while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
+          const uint32_t kl = (kf + 63 < total) ? kf + 63 : total - 1;
+          for (uint32_t jj = j;; jj++) {
+            const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
+            const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
+            const uint64_t b =
+                static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_lo), jj))) |
+                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_hi), jj))) << 32);
+            if (k >= inc - c && k < inc) addr[u] = b + (k - (inc - c));
+            if (inc > kl) break;
+          }
+        }
+        rec[u] = addr[u] != ~0ULL ? recs[addr[u]] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        if (addr[u] != ~0ULL) passb[addr[u]] = probe_rec(s_slice, s_masks, rec[u]);
+      }
+    }
+  }
+}
+
+// ---- partitioned probe, C: restore row order -> result bits + per-segment counts (P1's format) -----
+// Double-buffered: the next tile's pass bytes are in flight (registers) while this tile's are read
+// from LDS; one barrier per tile.
+__global__ __launch_bounds__(kTileThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
+                                                                const uint8_t* __restrict__ passb, uint64_t n,
+                                                                uint64_t n_tiles, uint64_t* __restrict__ out_bits,
+                                                                uint32_t* __restrict__ seg_counts) {
+  __shared__ uint8_t s_pass[2][kTileRows];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
+  uint64_t tile = blockIdx.x;
+  u32x4 pre = tile < n_tiles ? reinterpret_cast<const u32x4*>(passb + tile * kTileRows)[threadIdx.x] : u32x4{0, 0, 0, 0};
+  for (uint32_t buf = 0; tile < n_tiles; tile += gridDim.x, buf ^= 1) {
+    reinterpret_cast<u32x4*>(s_pass[buf])[threadIdx.x] = pre;  // 1024 x 16 B = one tile
+    const uint64_t next = tile + gridDim.x;
+    if (next < n_tiles) pre = reinterpret_cast<const u32x4*>(passb + next * kTileRows)[threadIdx.x];
+    uint32_t pp[2][4];
+#pragma unroll
+    for (int sg = 0; sg < 2; sg++) {
+      const uint64_t base = (tile * (kTileRows / kSegRows) + wave * 2 + sg) * kSegRows;
+#pragma unroll
+      for (int c = 0; c < 4; c++) pp[sg][c] = *reinterpret_cast<const uint32_t*>(pos + base + c * 128 + lane * 2);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sg = 0; sg < 2; sg++) {
+      const uint64_t seg = tile * (kTileRows / kSegRows) + wave * 2 + sg;
+      if (seg < n_segs) {
+        const uint64_t base = seg * kSegRows;
+        uint64_t b[8];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+          const uint64_t row0 = base + c * 128 + lane * 2;
+          const bool p0 = row0 < n && s_pass[buf][pp[sg][c] & 0xFFFFu];
+          const bool p1 = row0 + 1 < n && s_pass[buf][pp[sg][c] >> 16];
+          b[c * 2] = ballot64(p0);
+          b[c * 2 + 1] = ballot64(p1);
+          cnt += __popcll(b[c * 2]) + __popcll(b[c * 2 + 1]);
+        }
+        uint64_t mine = 0;
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            const uint64_t x = spread2(b[c * 2] >> (32 * q)) | (spread2(b[c * 2 + 1] >> (32 * q)) << 1);
+            mine = (lane == static_cast<uint32_t>(c * 2 + q)) ? x : mine;
+          }
+        }
+        if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
+        if (lane == 0) seg_counts[seg] = cnt;
+      }
+    }
   }
 }
 
@@ -374,6 +617,7 @@ struct rpt_bf {
   uint64_t sized_for_rows = 0;
   std::atomic<int> has_data{0};
   std::atomic<int> finalized{0};
+  std::atomic<int> probe_strategy{RPT_PROBE_AUTO};
 };
 
 namespace {
@@ -449,22 +693,68 @@ struct ProbeWorkspace {
   uint32_t* seg_counts;
   uint32_t* group_sums;
   uint32_t* group_offs;
+  // partitioned strategy only
+  uint32_t* recs;
+  uint16_t* pos;
+  uint8_t* passb;
+  uint32_t* runs;
 };
 
-size_t workspace_layout(uint64_t n, void* base, ProbeWorkspace* ws) {
+uint32_t slice_count(int log_num_blocks) {
+  return log_num_blocks <= rpt::kSliceLog ? 1u : (1u << (log_num_blocks - rpt::kSliceLog));
+}
+
+// Strategy a probe of this filter will run: explicit choice, else by filter size
+// (<= 64 KiB: LDS-resident filter; <= 16 MiB: partitioned into LDS slices; larger: direct gather).
+int resolve_strategy(int requested, int log_num_blocks) {
+  if (requested != RPT_PROBE_AUTO) return requested;
+  if (log_num_blocks <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
+  if (slice_count(log_num_blocks) <= static_cast<uint32_t>(rpt::kMaxSliceCount)) return RPT_PROBE_PARTITIONED;
+  return RPT_PROBE_GATHER;
+}
+
+int strategy_supported(int strategy, int log_num_blocks) {
+  switch (strategy) {
+    case RPT_PROBE_GATHER: return 1;
+    case RPT_PROBE_LDS: return log_num_blocks <= rpt::kLdsDirectMaxLog;
+    case RPT_PROBE_PARTITIONED:
+      return log_num_blocks >= rpt::kSliceLog && slice_count(log_num_blocks) <= static_cast<uint32_t>(rpt::kMaxSliceCount);
+    default: return 0;
+  }
+}
+
+// Layout (all 256-aligned): bits | seg_counts | group_sums | group_offs [| recs | pos | passb | runs].
+// The partitioned part is sized for whole 16 Ki-row tiles and only present when `partitioned`.
+size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* base, ProbeWorkspace* ws) {
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
-  const size_t b0 = align256(n_segs * rpt::kWordsPerSeg * 8);
-  const size_t b1 = align256(n_groups * rpt::kGroupSegs * 4);
-  const size_t b2 = align256(n_groups * 4);
+  const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
+  const uint64_t padded = n_tiles * rpt::kTileRows;
+  size_t sz[8] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
+                  align256(n_groups * 4), align256(n_groups * 4), 0, 0, 0, 0};
+  if (partitioned) {
+    sz[4] = align256(padded * 4);
+    sz[5] = align256(padded * 2);
+    sz[6] = align256(padded);
+    sz[7] = align256(static_cast<uint64_t>(slice_count(log_num_blocks)) * n_tiles * 4);
+  }
+  size_t off[8], total = 0;
+  for (int i = 0; i < 8; i++) {
+    off[i] = total;
+    total += sz[i];
+  }
   if (ws) {
     char* p = static_cast<char*>(base);
-    ws->bits = reinterpret_cast<uint64_t*>(p);
-    ws->seg_counts = reinterpret_cast<uint32_t*>(p + b0);
-    ws->group_sums = reinterpret_cast<uint32_t*>(p + b0 + b1);
-    ws->group_offs = reinterpret_cast<uint32_t*>(p + b0 + b1 + b2);
+    ws->bits = reinterpret_cast<uint64_t*>(p + off[0]);
+    ws->seg_counts = reinterpret_cast<uint32_t*>(p + off[1]);
+    ws->group_sums = reinterpret_cast<uint32_t*>(p + off[2]);
+    ws->group_offs = reinterpret_cast<uint32_t*>(p + off[3]);
+    ws->recs = partitioned ? reinterpret_cast<uint32_t*>(p + off[4]) : nullptr;
+    ws->pos = partitioned ? reinterpret_cast<uint16_t*>(p + off[5]) : nullptr;
+    ws->passb = partitioned ? reinterpret_cast<uint8_t*>(p + off[6]) : nullptr;
+    ws->runs = partitioned ? reinterpret_cast<uint32_t*>(p + off[7]) : nullptr;
   }
-  return b0 + b1 + 2 * b2;
+  return total;
 }
 
 int check_col(const rpt_key_column* col) {
@@ -488,8 +778,24 @@ unsigned persistent_grid(int device, uint64_t n_segs) {
 template <int K, bool D>
 void launch_probe_bits_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
                          uint64_t n_segs, uint64_t* bits, uint32_t* counts) {
-  hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
+  hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, false>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
                      (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+}
+
+// Whole filter in LDS (dynamic LDS = filter bytes); as many workgroups per CU as LDS allows.
+template <int K, bool D>
+void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
+                             uint64_t n_segs, uint64_t* bits, uint32_t* counts) {
+  const size_t lds = 8ULL << bf->log_num_blocks;
+  hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, true>), dim3(grid), dim3(rpt::kBlockThreads), lds, s, bf->words,
+                     (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+}
+
+template <int K, bool D>
+void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
+                        uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs) {
+  hipLaunchKernelGGL((rpt::partition_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n, slice_mask,
+                     n_tiles, recs, pos, runs);
 }
 
 template <int K, bool D>
@@ -566,7 +872,24 @@ int rpt_bf_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows) {
   return actual_rows * 8 > alloc ? 1 : 0;
 }
 
-size_t rpt_probe_workspace_bytes(uint64_t n_rows) { return workspace_layout(n_rows, nullptr, nullptr); }
+size_t rpt_probe_workspace_bytes(uint64_t n_rows, int log_num_blocks) {
+  // enough for any strategy the filter may run (the partitioned one needs the most)
+  const bool part = strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks);
+  return workspace_layout(n_rows, log_num_blocks, part, nullptr, nullptr);
+}
+
+int rpt_bf_set_probe_strategy(rpt_bf* bf, int strategy) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  if (strategy < RPT_PROBE_AUTO || strategy > RPT_PROBE_PARTITIONED)
+    return fail(RPT_ERR_INVALID_ARGUMENT, "unknown probe strategy %d", strategy);
+  bf->probe_strategy.store(strategy);
+  return RPT_OK;
+}
+
+int rpt_bf_probe_strategy(const rpt_bf* bf) {
+  if (!bf) return -fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  return resolve_strategy(bf->probe_strategy.load(), bf->log_num_blocks);
+}
 
 int rpt_bf_create_log_blocks(int device, int log_num_blocks, rpt_bf** out) {
   if (!out) return fail(RPT_ERR_INVALID_ARGUMENT, "null out");
@@ -683,18 +1006,50 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
   if (n == 0) return RPT_OK;
   int st = check_col(col);
   if (st != RPT_OK) return st;
-  const size_t need = rpt_probe_workspace_bytes(n);
+  const int L = bf->log_num_blocks;
+  const int strategy = resolve_strategy(bf->probe_strategy.load(), L);
+  if (!strategy_supported(strategy, L))
+    return fail(RPT_ERR_INVALID_ARGUMENT, "probe strategy %d unsupported for a 2^%d-block filter", strategy, L);
+  const bool part = strategy == RPT_PROBE_PARTITIONED;
+  const size_t need = workspace_layout(n, L, part, nullptr, nullptr);
   if (!workspace || workspace_bytes < need)
     return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   RPT_ON_DEVICE(bf->device);
   ProbeWorkspace ws;
-  workspace_layout(n, workspace, &ws);
+  workspace_layout(n, L, part, workspace, &ws);
+  hipStream_t s = as_stream(stream);
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
-  const unsigned grid = persistent_grid(bf->device, n_segs);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, row_sel};
-  RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense_ok(col, row_sel), grid, as_stream(stream), bf, a, n,
-                  n_segs, ws.bits, ws.seg_counts);
-  RPT_LAUNCHED("probe_bits_kernel");
+  const bool dense = dense_ok(col, row_sel);
+  if (strategy == RPT_PROBE_GATHER) {
+    const unsigned grid = persistent_grid(bf->device, n_segs);
+    RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
+    RPT_LAUNCHED("probe_bits_kernel");
+  } else if (strategy == RPT_PROBE_LDS) {
+    const uint64_t lds = (8ULL << L) + 8ULL * rpt::kNumMasks;
+    const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(rpt::kBlocksPerCU, (160ULL << 10) / lds));
+    const unsigned grid = static_cast<unsigned>(
+        std::max<uint64_t>(1, std::min(ceil_div(n_segs, rpt::kWavesPerBlock), num_cus(bf->device) * per_cu)));
+    RPT_DISPATCH_KD(launch_probe_bits_lds_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
+    RPT_LAUNCHED("probe_bits_kernel<lds>");
+  } else {
+    const uint32_t slices = slice_count(L);
+    const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
+    const int cus = num_cus(bf->device);
+    const unsigned g_tiles = static_cast<unsigned>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) * 2));
+    RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense, g_tiles, s, a, n, slices - 1, n_tiles, ws.recs, ws.pos,
+                    ws.runs);
+    RPT_LAUNCHED("partition_kernel");
+    // >= 2 workgroups per CU in total, but never more splits than tiles
+    const uint32_t splits = static_cast<uint32_t>(std::max<uint64_t>(
+        1, std::min<uint64_t>(n_tiles, ceil_div(static_cast<uint64_t>(cus) * 2, slices))));
+    hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words,
+                       splits, n_tiles, ws.recs, ws.runs, ws.passb);
+    RPT_LAUNCHED("slice_probe_kernel");
+    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(g_tiles), dim3(rpt::kTileThreads), 0, s, ws.pos, ws.passb, n,
+                       n_tiles, ws.bits, ws.seg_counts);
+    RPT_LAUNCHED("unpermute_kernel");
+  }
   return RPT_OK;
 }
 
@@ -708,11 +1063,11 @@ int rpt_bf_probe_phase2(const uint32_t* row_sel, uint64_t n, uint32_t* out_sel, 
     return RPT_OK;
   }
   if (!out_sel) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_sel");
-  const size_t need = rpt_probe_workspace_bytes(n);
+  const size_t need = workspace_layout(n, 0, false, nullptr, nullptr);
   if (!workspace || workspace_bytes < need)
     return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   ProbeWorkspace ws;
-  workspace_layout(n, workspace, &ws);
+  workspace_layout(n, 0, false, workspace, &ws);
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
   hipLaunchKernelGGL(rpt::group_sum_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,

@@ -6,6 +6,10 @@ OR-merge; the C++ host mirror of the DuckDB operators lives in include/rpt_host.
 """
 from ._lib import (  # noqa: F401
     LIB_PATH,
+    RPT_PROBE_AUTO,
+    RPT_PROBE_GATHER,
+    RPT_PROBE_LDS,
+    RPT_PROBE_PARTITIONED,
     RPT_KEY_HASH,
     RPT_KEY_I32,
     RPT_KEY_I64,

@@ -20,6 +20,11 @@ RPT_ERR_OUT_OF_MEMORY = 3
 RPT_ERR_WORKSPACE = 4
 RPT_ERR_SHAPE_MISMATCH = 5
 
+RPT_PROBE_AUTO = 0
+RPT_PROBE_GATHER = 1
+RPT_PROBE_LDS = 2
+RPT_PROBE_PARTITIONED = 3
+
 RPT_KEY_I64 = 0
 RPT_KEY_I32 = 1
 RPT_KEY_HASH = 2
@@ -63,7 +68,9 @@ SIGNATURES = {
     "rpt_last_error": (c_char_p, []),
     "rpt_bf_log_num_blocks_for_rows": (c_int, [c_uint64]),
     "rpt_bf_needs_resize": (c_int, [c_uint64, c_uint64]),
-    "rpt_probe_workspace_bytes": (c_size_t, [c_uint64]),
+    "rpt_probe_workspace_bytes": (c_size_t, [c_uint64, c_int]),
+    "rpt_bf_set_probe_strategy": (c_int, [c_void_p, c_int]),
+    "rpt_bf_probe_strategy": (c_int, [c_void_p]),
     "rpt_bf_create": (c_int, [c_int, c_uint64, POINTER(c_void_p)]),
     "rpt_bf_create_log_blocks": (c_int, [c_int, c_int, POINTER(c_void_p)]),
     "rpt_bf_destroy": (c_int, [c_void_p]),

@@ -86,8 +86,8 @@ class ProbeWorkspace:
         self.device = device
         self.buf: Optional[torch.Tensor] = None
 
-    def get(self, n: int) -> torch.Tensor:
-        need = int(load().rpt_probe_workspace_bytes(n))
+    def get(self, n: int, log_num_blocks: int) -> torch.Tensor:
+        need = int(load().rpt_probe_workspace_bytes(n, log_num_blocks))
         if self.buf is None or self.buf.numel() < need:
             self.buf = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         return self.buf
@@ -156,6 +156,21 @@ class BloomFilter:
     def finalized(self, v: bool) -> None:
         check(self._lib.rpt_bf_set_finalized(self._h, int(bool(v))))
 
+    @property
+    def probe_strategy(self) -> int:
+        """The strategy a probe runs now (RPT_PROBE_*; AUTO resolved by filter size)."""
+        v = self._lib.rpt_bf_probe_strategy(self._h)
+        if v < 0:
+            check(-v)
+        return v
+
+    @probe_strategy.setter
+    def probe_strategy(self, strategy: int) -> None:
+        check(self._lib.rpt_bf_set_probe_strategy(self._h, int(strategy)))
+
+    def workspace_bytes(self, n: int) -> int:
+        return int(self._lib.rpt_probe_workspace_bytes(n, self.log_num_blocks))
+
     def set_has_data(self, v: bool) -> None:
         check(self._lib.rpt_bf_set_has_data(self._h, int(bool(v))))
 
@@ -195,7 +210,7 @@ class BloomFilter:
             out_sel = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         if out_count is None:
             out_count = self._count
-        ws = workspace if workspace is not None else self._ws.get(n)
+        ws = workspace if workspace is not None else self._ws.get(n, self.log_num_blocks)
         check(self._lib.rpt_bf_probe(self._h, ctypes.byref(col), _ptr(row_sel), n, out_sel.data_ptr(),
                                      out_count.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(),
                                      _stream(self.device, stream)))

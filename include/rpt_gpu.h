@@ -38,7 +38,7 @@ typedef enum rpt_status {
   RPT_ERR_INVALID_ARGUMENT = 1, /* null handle/pointer, bad key type, n too large for uint32 sel */
   RPT_ERR_HIP = 2,              /* a HIP runtime call failed; rpt_last_error() has the text */
   RPT_ERR_OUT_OF_MEMORY = 3,    /* device allocation failed */
-  RPT_ERR_WORKSPACE = 4,        /* caller workspace smaller than rpt_probe_workspace_bytes(n) */
+  RPT_ERR_WORKSPACE = 4,        /* caller workspace smaller than rpt_probe_workspace_bytes() */
   RPT_ERR_SHAPE_MISMATCH = 5    /* merge of filters with different log_num_blocks / devices */
 } rpt_status;
 
@@ -47,6 +47,15 @@ typedef enum rpt_key_type {
   RPT_KEY_I32 = 1,  /* INTEGER / int32 keys (JOB join keys) */
   RPT_KEY_HASH = 2  /* pre-computed 64-bit hashes (HashColumns output); validity/NULLs not applied */
 } rpt_key_type;
+
+/* How a probe reaches the filter blocks (rpt_bf_set_probe_strategy). All give identical results. */
+typedef enum rpt_probe_strategy {
+  RPT_PROBE_AUTO = 0,       /* by filter size: LDS (<= 64 KiB), PARTITIONED (<= 16 MiB), else GATHER */
+  RPT_PROBE_GATHER = 1,     /* one random 8-byte gather per key from L2 / Infinity Cache / HBM */
+  RPT_PROBE_LDS = 2,        /* whole filter staged in each workgroup's LDS (filters <= 64 KiB) */
+  RPT_PROBE_PARTITIONED = 3 /* rows bucketed per 16 Ki-row tile by 64 KiB filter slice; each slice is
+                               probed from LDS, then row order is restored (filters 64 KiB..16 MiB) */
+} rpt_probe_strategy;
 
 /* A hipStream_t, passed opaquely so this header needs no HIP include. NULL = the null stream. */
 typedef void* rpt_stream_t;
@@ -86,8 +95,9 @@ int rpt_bf_log_num_blocks_for_rows(uint64_t n_rows);
 /* PhysicalCreateBF::Finalize resize rule, verbatim (physical_create_bf.cpp:394-398):
  * 1 iff actual_rows > 0 and actual_rows*8 > NextPow2(max(512, sized_for_rows*12)). */
 int rpt_bf_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows);
-/* Device workspace the probe needs for n rows (bytes, 256-aligned). */
-size_t rpt_probe_workspace_bytes(uint64_t n_rows);
+/* Device workspace a probe of n rows against a 2^log_num_blocks-block filter needs, for any
+ * strategy (bytes, 256-aligned). */
+size_t rpt_probe_workspace_bytes(uint64_t n_rows, int log_num_blocks);
 
 /* ---- lifecycle --------------------------------------------------------------------------- */
 /* PTBloomFilter::Initialize(context, est_num_rows) (bloom_filter.cpp:27-32): allocate and zero a
@@ -103,6 +113,10 @@ int rpt_bf_get_info(const rpt_bf* bf, rpt_bf_info* out);
 int rpt_bf_reinitialize(rpt_bf* bf, uint64_t actual_rows);
 /* PTBloomFilter::finalized_ = value (physical_create_bf.cpp:409-413). */
 int rpt_bf_set_finalized(rpt_bf* bf, int value);
+/* Select the probe strategy (rpt_probe_strategy); rpt_bf_probe_strategy returns the one a probe
+ * will run now (AUTO resolved), or a negative status. */
+int rpt_bf_set_probe_strategy(rpt_bf* bf, int strategy);
+int rpt_bf_probe_strategy(const rpt_bf* bf);
 /* Zero every block and clear has_data (stream-ordered). */
 int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
 
@@ -119,7 +133,7 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
  * *out_count_dev (device uint64). Rows are 0..n-1, or row_sel[0..n) when row_sel != NULL (the
  * already-sliced chunk of PhysicalUseBF's multi-filter loop, physical_use_bf.cpp:137-183); the
  * written ids are then the row_sel values. n must be < 2^32 (sel_t is uint32). out_sel capacity n.
- * workspace: device memory of rpt_probe_workspace_bytes(n) bytes, exclusively owned by this call
+ * workspace: device memory of rpt_probe_workspace_bytes(n, log_num_blocks) bytes, exclusively owned by this call
  * until it completes on `stream`. */
 int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
                  uint32_t* out_sel, uint64_t* out_count_dev, void* workspace, size_t workspace_bytes,

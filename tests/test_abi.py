@@ -66,10 +66,14 @@ def test_resize_rule_matches_oracle():
 def test_workspace_size_grows_with_rows():
     lib = _lib.load()
     prev = 0
-    for n in [1, 512, 513, 10**6, 10**9, 2**32 - 1]:
-        b = lib.rpt_probe_workspace_bytes(n)
-        assert b % 256 == 0 and b >= prev and b >= n // 8
-        prev = b
+    for L in [3, 13, 14, 21, 24]:
+        prev = 0
+        for n in [1, 512, 513, 10**6, 10**9, 2**32 - 1]:
+            b = lib.rpt_probe_workspace_bytes(n, L)
+            assert b % 256 == 0 and b >= prev and b >= n // 8
+            prev = b
+    # the partitioned strategy (64 KiB..16 MiB filters) needs records + row map + pass bytes
+    assert lib.rpt_probe_workspace_bytes(10**6, 21) >= 7 * 10**6 > lib.rpt_probe_workspace_bytes(10**6, 24)
 
 
 def test_argument_errors_are_reported():
@@ -81,4 +85,5 @@ def test_argument_errors_are_reported():
     out = ctypes.c_void_p()
     assert lib.rpt_bf_create_log_blocks(0, 41, ctypes.byref(out)) == _lib.RPT_ERR_INVALID_ARGUMENT
     assert lib.rpt_bf_destroy(None) == 0
+    assert lib.rpt_bf_set_probe_strategy(None, 1) == _lib.RPT_ERR_INVALID_ARGUMENT
     assert lib.rpt_synth_probe_keys(None, 1, 10, 0, 10, None) == _lib.RPT_ERR_INVALID_ARGUMENT

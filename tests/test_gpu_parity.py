@@ -8,6 +8,25 @@ import rpt_oracle as orc
 
 pytestmark = pytest.mark.gpu
 
+STRATEGIES = {"gather": 1, "lds": 2, "partitioned": 3}
+
+
+def supported(strategy: str, log_num_blocks: int) -> bool:
+    if strategy == "lds":
+        return log_num_blocks <= 13
+    if strategy == "partitioned":
+        return 13 <= log_num_blocks <= 21
+    return True
+
+
+def with_strategy(bf, strategy: str):
+    if not supported(strategy, bf.log_num_blocks):
+        pytest.skip(f"{strategy} does not apply to a 2^{bf.log_num_blocks}-block filter")
+    bf.probe_strategy = STRATEGIES[strategy]
+    assert bf.probe_strategy == STRATEGIES[strategy]
+    return bf
+
+
 KEY_CASES = ["kat16", "raw_hash_100k", "k64_n1", "k64_n100", "k64_n1000", "k64_n50000", "k64_n300000",
              "k32_n5000", "k64_n3000_nulls7", "k32_n3000_nulls5", "k64_n20000_over"]
 
@@ -36,11 +55,12 @@ def bits_of(words: torch.Tensor, n: int) -> np.ndarray:
     return np.unpackbits(w.view(np.uint8), bitorder="little")[:n].astype(bool)
 
 
+@pytest.mark.parametrize("strategy", list(STRATEGIES))
 @pytest.mark.parametrize("case", KEY_CASES)
-def test_golden_hash_path(rpt, golden, case):
+def test_golden_hash_path(rpt, golden, case, strategy):
     c = golden.cases[case]
     h, p, _ = golden.inputs(case)
-    bf = rpt.BloomFilter(log_num_blocks=c["log_num_blocks"])
+    bf = with_strategy(rpt.BloomFilter(log_num_blocks=c["log_num_blocks"]), strategy)
     bf.insert(dev(h), key_type=rpt.RPT_KEY_HASH)
     torch.cuda.synchronize()
     assert np.array_equal(bf.export_words(), golden.words(case))
@@ -51,11 +71,12 @@ def test_golden_hash_path(rpt, golden, case):
     assert np.array_equal(sel, np.flatnonzero(ref).astype(np.int32))
 
 
+@pytest.mark.parametrize("strategy", list(STRATEGIES))
 @pytest.mark.parametrize("case", [k for k in KEY_CASES if k.startswith("k") and k != "kat16"])
-def test_golden_key_path(rpt, golden, case):
+def test_golden_key_path(rpt, golden, case, strategy):
     c = golden.cases[case]
     _, _, kc = golden.inputs(case)
-    bf = rpt.BloomFilter(kc.size_rows)
+    bf = with_strategy(rpt.BloomFilter(kc.size_rows), strategy)
     assert bf.log_num_blocks == c["log_num_blocks"]
     v = dev(gu.validity_words(kc.valid)) if kc.valid is not None else None
     bf.insert(dev(kc.keys), validity=v)
@@ -97,7 +118,26 @@ def test_ragged_sizes_vs_oracle(rpt, dtype, n):
     assert np.array_equal(sel, orc.probe_keys(w, lnb, probe))
 
 
-def test_dictionary_validity_rowsel_vs_oracle(rpt):
+@pytest.mark.parametrize("strategy", list(STRATEGIES))
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+@pytest.mark.parametrize("n", [1, 16383, 16384, 16385, 3 * 16384 + 5, 200001])
+def test_partition_tile_edges_vs_oracle(rpt, strategy, dtype, n):
+    """Filters large enough for the partitioned path (2^17 blocks), ragged tile boundaries."""
+    rng = np.random.default_rng(n)
+    build = rng.integers(-2**40, 2**40, size=100000, dtype=np.int64).astype(dtype)
+    probe = np.concatenate([build[rng.integers(0, build.size, size=n // 3)],
+                            rng.integers(-2**40, 2**40, size=n - n // 3).astype(dtype)])
+    lnb = orc.log_num_blocks(build.size)
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, build)
+    bf = with_strategy(rpt.BloomFilter(build.size), strategy)
+    bf.insert(dev(build))
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, lnb, probe))
+
+
+@pytest.mark.parametrize("strategy", list(STRATEGIES))
+def test_dictionary_validity_rowsel_vs_oracle(rpt, strategy):
     rng = np.random.default_rng(7)
     dict_vals = rng.integers(-10**12, 10**12, size=3000, dtype=np.int64)
     n = 20000
@@ -108,6 +148,12 @@ def test_dictionary_validity_rowsel_vs_oracle(rpt):
     w = orc.new_words(lnb)
     orc.insert_keys(w, lnb, dict_vals, key_sel=key_sel[:5000], validity=vw)
     bf = rpt.BloomFilter(n)
+    if strategy == "lds":
+        bf = rpt.BloomFilter(log_num_blocks=13)
+        lnb = 13
+        w = orc.new_words(lnb)
+        orc.insert_keys(w, lnb, dict_vals, key_sel=key_sel[:5000], validity=vw)
+    with_strategy(bf, strategy)
     bf.insert(dev(dict_vals), key_sel=dev(key_sel[:5000]), validity=dev(vw))
     assert np.array_equal(bf.export_words(), w)
     # probe a dictionary vector through a row selection (an already-sliced chunk)
@@ -231,11 +277,13 @@ def _window_check(bf, w, lnb, probe_dev, sel, lo, hi):
     assert np.array_equal(sel[a:b], exp)
 
 
-@pytest.mark.parametrize("n_probe,n_build,p", [(10**8, 10**7, 100), (10**9, 10**7, 100)])
-def test_full_size_probe_properties(rpt, n_probe, n_build, p):
+@pytest.mark.parametrize("n_probe,n_build,p,strategy", [(10**8, 10**7, 100, "gather"),
+                                                         (10**8, 10**7, 1000, "partitioned"),
+                                                         (10**9, 10**7, 100, "partitioned")])
+def test_full_size_probe_properties(rpt, n_probe, n_build, p, strategy):
     """BASELINE sizes: sortedness, count == popcount(find bits), windows vs oracle, no false negatives."""
     build = rpt.synth_build_keys(n_build)
-    bf = rpt.BloomFilter(n_build)
+    bf = with_strategy(rpt.BloomFilter(n_build), strategy)
     bf.insert(build)
     lnb = bf.log_num_blocks
     w = bf.export_words()
@@ -256,6 +304,6 @@ def test_full_size_probe_properties(rpt, n_probe, n_build, p):
     for lo, hi in [(0, 10**6), (n_probe // 2 - 777, n_probe // 2 + 10**6), (n_probe - 10**6, n_probe)]:
         _window_check(bf, w, lnb, probe, sel_np, lo, hi)
     rate = count / n_probe
-    assert p / 1000 < rate < p / 1000 + 0.05
+    assert p / 1000 <= rate < p / 1000 + 0.05
     del probe, sel_t, bits, sel
     torch.cuda.empty_cache()
