@@ -47,6 +47,32 @@ def parse():
     return ap.parse_args()
 
 
+def algorithmic_bytes(kernel: str, n: int, survivors: int) -> int:
+    """SURVEY §8(d) per-unit bytes for the kernel's part of the probe: every kernel that streams the
+    key column is charged 8 B/key (the key read; its own intermediates are implementation traffic,
+    counted in `traffic`); the compaction is charged the 4 B/survivor selection vector it writes."""
+    if kernel.startswith("compact"):
+        return SEL_BYTES * survivors
+    if kernel.startswith(("slice_probe", "unpermute", "group_")):
+        return 0
+    return KEY_BYTES * n
+
+
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of `kernel` from the PMC summary tools/pmc_summary.py wrote for this build
+    (FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE, separate rocprofv3 --pmc passes)."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None
+    return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": f"profiles/pmc_latest.json ({d.get('round')})"}
+
+
 def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int) -> dict:
     """The C++ restatement of the reference CPU path, morsel-parallel in 2048-row vectors."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -101,6 +127,7 @@ def main():
         dist.init_process_group("nccl", device_id=device)
 
     import rpt_amd
+    from rpt_amd import _lib as rpt_lib
     from rpt_amd.distributed import allreduce_or_filter, shard_range
 
     n_probe = int(args.probe_rows)
@@ -150,6 +177,9 @@ def main():
         step()
     torch.cuda.synchronize()
     events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    # per-kernel HIP events on the launch stream (rpt_profiling_*) over the timed region
+    rpt_lib.profiling_reset()
+    rpt_lib.profiling(True)
     barrier()
     torch.cuda.synchronize()
     ts = time.perf_counter()
@@ -158,6 +188,8 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - ts
+    rpt_lib.profiling(False)
+    ktimes = rpt_lib.kernel_times()
 
     survivors = int(out_count.item())
     p1_ms = statistics.mean(e[0].elapsed_time(e[1]) for e in events)
@@ -171,9 +203,13 @@ def main():
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = world * n_probe * args.steps / elapsed
-        p1_bytes = KEY_BYTES * n_probe
-        achieved = p1_bytes / (p1_ms * 1e-3)
         probe_bytes = KEY_BYTES * n_probe + SEL_BYTES * survivors
+        # dominant kernel of the step (largest total device time)
+        dom_name, (dom_calls, dom_total) = max(ktimes.items(), key=lambda kv: kv[1][1])
+        dom_ms = dom_total / dom_calls
+        dom_bytes = algorithmic_bytes(dom_name, n_probe, survivors)
+        achieved = dom_bytes / (dom_ms * 1e-3)
+        traffic = pmc_traffic(dom_name)
         line = {
             "metric": "bloom probe keys/sec (whole node)",
             "value": value,
@@ -201,15 +237,18 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": f"probe phase 1 ({strategy_name} strategy)",
+                "kernel": dom_name,
                 "achieved": achieved / 1e9,
                 "peak": HBM_PEAK_BPS / 1e9,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_BPS,
-                "traffic": None,
-                "avg_launch_ms": p1_ms,
-                "algorithmic_bytes_per_launch": p1_bytes,
+                "traffic": traffic["bytes_per_launch"] if traffic else None,
+                "traffic_source": traffic["source"] if traffic else None,
+                "avg_launch_ms": dom_ms,
+                "algorithmic_bytes_per_launch": dom_bytes,
             },
+            "kernels_ms": {k: v[1] / v[0] for k, v in sorted(ktimes.items(), key=lambda kv: -kv[1][1])},
+            "phase1_ms": p1_ms,
             "probe_total": {
                 "avg_ms": probe_ms,
                 "algorithmic_bytes": probe_bytes,

@@ -34,16 +34,26 @@ constexpr int kBlockThreads = 256;
 constexpr int kWavesPerBlock = kBlockThreads / 64;
 constexpr uint64_t kSegRows = 512;                 // rows per wave segment (8 per lane)
 constexpr uint64_t kWordsPerSeg = kSegRows / 64;   // result-bit words per segment
-constexpr uint64_t kGroupSegs = 1024;              // segments per scan group
+constexpr uint64_t kGroupSegs = 256;               // segments per scan group (one compaction workgroup)
 constexpr int kBlocksPerCU = 8;
 
 // Partitioned ("routed") probe: the filter is cut into 64 KiB slices that fit in LDS; probe rows are
 // bucketed by slice per 16 Ki-row tile so that every filter access is an LDS read.
-constexpr int kSliceLog = 13;                          // 2^13 blocks = 64 KiB per slice
+#ifndef RPT_SLICE_LOG
+#define RPT_SLICE_LOG 14
+#endif
+constexpr int kSliceLog = RPT_SLICE_LOG;               // 2^13 blocks = 64 KiB (or 2^14 = 128 KiB) per slice
 constexpr uint64_t kSliceWords = 1ULL << kSliceLog;
-constexpr int kMaxSliceCount = 256;                    // P <= 256 slices (filters <= 16 MiB)
-constexpr uint64_t kTileRows = 16384;                  // rows per partition tile
-constexpr int kTileThreads = 1024;                     // 16 waves x 1024 rows
+constexpr int kMaxSliceCount = 256;                    // P <= 256 slices (filters <= 32 MiB at 128 KiB slices)
+#ifndef RPT_TILE_ROWS
+#define RPT_TILE_ROWS 16384
+#endif
+constexpr uint64_t kTileRows = RPT_TILE_ROWS;          // rows per partition tile (8 or 16 per thread)
+constexpr uint64_t kTileCap = kTileRows + 4 * kMaxSliceCount;  // record slots per tile (runs padded to 4)
+constexpr int kTileThreads = 1024;                     // 16 waves
+constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
+constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave in the partition kernel
+static_assert(kRowsPerThread == 8 || kRowsPerThread == 16, "tile = 8 Ki or 16 Ki rows");
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
 constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
 #ifndef RPT_PARTITION_MIN_WAVES
@@ -73,45 +83,51 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
                                             uint64_t (&h)[8], bool (&ok)[8]) {
   using Tr = KeyTraits<K>;
   using T = typename Tr::T;
-  const T* keys = static_cast<const T*>(a.keys);
+  // rows left from `base` (uniform), so per-row bounds checks are 32-bit and addresses are
+  // uniform-base + 32-bit lane offset
+  const uint32_t rem = n > base ? static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows) : 0u;
   if constexpr (DENSE) {
     constexpr int V = Tr::kVec;
+    const T* kb = static_cast<const T*>(a.keys) + base;
+    const uint64_t* vb = a.validity ? a.validity + (base >> 6) : nullptr;  // base is a multiple of 512
 #pragma unroll
     for (int c = 0; c < 8 / V; c++) {
-      const uint64_t row0 = base + static_cast<uint64_t>(c) * 64 * V + static_cast<uint64_t>(lane) * V;
+      const uint32_t off = static_cast<uint32_t>(c * 64 * V) + lane * V;
       T v[V];
-      if (row0 + V <= n) {
+      if (off + V <= rem) {
         if constexpr (V == 2) {
-          const u64x2 x = *reinterpret_cast<const u64x2*>(keys + row0);
+          const u64x2 x = *reinterpret_cast<const u64x2*>(kb + off);
           v[0] = static_cast<T>(x[0]);
           v[1] = static_cast<T>(x[1]);
         } else {
-          const u32x4 x = *reinterpret_cast<const u32x4*>(keys + row0);
+          const u32x4 x = *reinterpret_cast<const u32x4*>(kb + off);
 #pragma unroll
           for (int e = 0; e < V; e++) v[e] = static_cast<T>(x[e]);
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < V; e++) v[e] = (row0 + e < n) ? keys[row0 + e] : T(0);
+        for (int e = 0; e < V; e++) v[e] = (off + e < rem) ? kb[off + e] : T(0);
       }
-      uint64_t vw = 0;
-      if (K != kKeyHash && a.validity != nullptr) vw = a.validity[row0 >> 6];  // V | 64: one word
+      // validity bits of this lane's V rows, shifted down to bits 0..V-1 (V | 64: one word)
+      uint32_t vbits = (1u << V) - 1;
+      if (K != kKeyHash && vb != nullptr && off < rem) vbits = static_cast<uint32_t>(vb[off >> 6] >> (off & 63));
 #pragma unroll
       for (int e = 0; e < V; e++) {
-        const uint64_t row = row0 + e;
-        ok[c * V + e] = row < n;
+        ok[c * V + e] = off + e < rem;
         uint64_t hv = Tr::hash(v[e]);
-        if (K != kKeyHash && a.validity != nullptr && !((vw >> (row & 63)) & 1ULL)) hv = kNullHash;
+        if (K != kKeyHash && !((vbits >> e) & 1u)) hv = kNullHash;
         h[c * V + e] = hv;
       }
     }
   } else {
+    const T* keys = static_cast<const T*>(a.keys);
 #pragma unroll
     for (int c = 0; c < 8; c++) {
-      const uint64_t i = base + static_cast<uint64_t>(c) * 64 + lane;
-      ok[c] = i < n;
+      const uint32_t off = static_cast<uint32_t>(c * 64) + lane;
+      ok[c] = off < rem;
       uint64_t hv = 0;
       if (ok[c]) {
+        const uint64_t i = base + off;
         const uint64_t r = a.row_sel ? a.row_sel[i] : i;
         const uint64_t k = a.key_sel ? a.key_sel[r] : r;
         hv = Tr::hash(keys[k]);
@@ -119,6 +135,17 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
       }
       h[c] = hv;
     }
+  }
+}
+
+// Row offset inside a 512-row segment of the j-th hash load_hashes<K, DENSE> returns for `lane`.
+template <int K, bool DENSE>
+__device__ __forceinline__ uint32_t seg_row(int j, uint32_t lane) {
+  if constexpr (DENSE) {
+    constexpr int V = KeyTraits<K>::kVec;
+    return static_cast<uint32_t>((j / V) * 64 * V) + lane * V + static_cast<uint32_t>(j % V);
+  } else {
+    return static_cast<uint32_t>(j * 64) + lane;
   }
 }
 
@@ -195,65 +222,84 @@ __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_
 
 // ---- partitioned probe, A: bucket a 16 Ki-row tile by filter slice --------------------------------
 // Row r of the tile gets record rec = (uint32)hash (mask id, rotation and block-in-slice bits) stored
-// at position pos(r) of the tile's slice-sorted record array; pos(r) is written per row (u16) so the
-// unpermute step can restore row order; per (slice, tile) the run (start << 16 | count) is written
-// slice-major for the slice kernel.
+// at position pos(r) of the tile's slice-sorted record array (runs padded to 4 records); pos(r) is
+// written per row (u16) so the unpermute step can restore row order. Per tile the padded runs
+// (start << 16 | length) are written tile-major (one coalesced 4*P-byte row); runs_transpose_kernel
+// turns them slice-major for the slice kernel. Two passes over the rows held in registers: count per
+// slice (LDS atomics), scan, then claim positions with an LDS cursor per slice and scatter.
 template <int K, bool DENSE>
-__global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(KeyArgs a, uint64_t n, uint32_t slice_mask,
-                                                                uint64_t n_tiles, uint32_t* __restrict__ recs,
-                                                                uint16_t* __restrict__ pos_out,
-                                                                uint32_t* __restrict__ runs) {
-  __shared__ uint32_t s_rec[kTileRows];
+__global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(
+    KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
+    uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm) {
+  __shared__ uint32_t s_rec[kTileCap];
   __shared__ uint32_t s_cnt[kMaxSliceCount];
   __shared__ uint32_t s_base[kMaxSliceCount];
+  __shared__ uint32_t s_cur[kMaxSliceCount];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t n_slices = slice_mask + 1;
-  for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+  {  // one tile per workgroup (no persistent loop: keeps per-lane invariants out of registers)
+    const uint64_t tile = blockIdx.x;
     if (threadIdx.x < kMaxSliceCount) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t tile_base = tile * kTileRows;
-    // per row: rec = low 32 hash bits; key = slice << 16 | rank-in-slice (0xFFFFFFFF: row >= n)
-    uint32_t rec[16], key[16];
+    // pass 1: hash, stage the record at its row position in LDS, count rows per slice; only the 8-bit
+    // slice ids stay in registers (4 per word).
+    uint32_t sl4[kRowsPerThread / 4] = {};
 #pragma unroll
-    for (int sg = 0; sg < 2; sg++) {
+    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
+      const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
       uint64_t hh[8];
       bool oo[8];
-      load_hashes<K, DENSE>(a, tile_base + wave * 1024 + sg * kSegRows, n, lane, hh, oo);
+      load_hashes<K, DENSE>(a, tile_base + seg_local, n, lane, hh, oo);
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
-        rec[sg * 8 + j] = static_cast<uint32_t>(hh[j]);
-        key[sg * 8 + j] = oo[j] ? ((sl << 16) | atomicAdd(&s_cnt[sl], 1u)) : 0xFFFFFFFFu;
+        s_rec[seg_local + seg_row<K, DENSE>(j, lane)] = static_cast<uint32_t>(hh[j]);
+        sl4[(sg * 8 + j) >> 2] |= sl << (8 * (j & 3));
+        if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
       }
     }
     __syncthreads();
-    if (wave == 0) {  // exclusive scan of <= 256 slice counts: 4 per lane
+    if (wave == 0) {  // exclusive scan of <= 256 slice counts, each padded to 4 records: 4 per lane
       uint32_t c[4], t = 0;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         const uint32_t idx = lane * 4 + i;
-        c[i] = idx < n_slices ? s_cnt[idx] : 0u;
+        c[i] = idx < n_slices ? (s_cnt[idx] + 3u) & ~3u : 0u;
         t += c[i];
       }
       uint32_t off = wave_inclusive_sum(t) - t;
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         s_base[lane * 4 + i] = off;
+        s_cur[lane * 4 + i] = off;
         off += c[i];
       }
     }
-    __syncthreads();
+    // pass 2: pull this thread's records back out of the row-ordered staging ...
+    uint32_t rec[kRowsPerThread];
 #pragma unroll
-    for (int sg = 0; sg < 2; sg++) {
-      const uint64_t base = tile_base + wave * 1024 + sg * kSegRows;
+    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
+      const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+#pragma unroll
+      for (int j = 0; j < 8; j++) rec[sg * 8 + j] = s_rec[seg_local + seg_row<K, DENSE>(j, lane)];
+    }
+    __syncthreads();
+    // ... and scatter them to their slice-sorted positions
+#pragma unroll
+    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
+      const uint64_t base = tile_base + wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+      const uint32_t seg_rem = n > base ? static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows) : 0u;
       uint16_t pv[8];
 #pragma unroll
       for (int j = 0; j < 8; j++) {
-        const uint32_t kk = key[sg * 8 + j];
+        const int jj = sg * 8 + j;
+        const uint32_t sl = (sl4[jj >> 2] >> (8 * (jj & 3))) & 0xFFu;
+        const bool ok = seg_row<K, DENSE>(j, lane) < seg_rem;
         uint32_t p = 0;
-        if (kk != 0xFFFFFFFFu) {
-          p = s_base[kk >> 16] + (kk & 0xFFFFu);
-          s_rec[p] = rec[sg * 8 + j];
+        if (ok) {
+          p = atomicAdd(&s_cur[sl], 1u);
+          s_rec[p] = rec[jj];
         }
         pv[j] = static_cast<uint16_t>(p);
       }
@@ -278,13 +324,33 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
       }
     }
     __syncthreads();
-    const uint64_t tile_rows = (tile_base + kTileRows <= n) ? kTileRows : (n - tile_base);
-    u32x4* dst = reinterpret_cast<u32x4*>(recs + tile_base);
+    // records of the tile (pad slots hold stale values: probed, never read back)
+    const uint32_t used = s_base[slice_mask] + ((s_cnt[slice_mask] + 3u) & ~3u);
+    u32x4* dst = reinterpret_cast<u32x4*>(recs + tile * kTileCap);
     const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
-    for (uint32_t i = threadIdx.x; i < (tile_rows + 3) / 4; i += kTileThreads) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
     if (threadIdx.x < n_slices)
-      runs[static_cast<uint64_t>(threadIdx.x) * n_tiles + tile] = (s_base[threadIdx.x] << 16) | s_cnt[threadIdx.x];
+      runs_tm[tile * n_slices + threadIdx.x] = (s_base[threadIdx.x] << 16) | ((s_cnt[threadIdx.x] + 3u) & ~3u);
     __syncthreads();
+  }
+}
+
+// runs_sm[slice][tile] = runs_tm[tile][slice], through 64 x 64 LDS tiles (both sides coalesced).
+__global__ __launch_bounds__(kBlockThreads) void runs_transpose_kernel(const uint32_t* __restrict__ runs_tm,
+                                                                      uint32_t n_slices, uint64_t n_tiles,
+                                                                      uint32_t* __restrict__ runs_sm) {
+  __shared__ uint32_t s_t[64][65];
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * 64;
+  const uint32_t s0 = blockIdx.y * 64;
+  const uint32_t c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  for (uint32_t r = r0; r < 64; r += 4) {
+    const uint64_t t = t0 + r;
+    s_t[r][c] = (t < n_tiles && s0 + c < n_slices) ? runs_tm[t * n_slices + s0 + c] : 0u;
+  }
+  __syncthreads();
+  for (uint32_t r = r0; r < 64; r += 4) {
+    const uint64_t t = t0 + c;
+    if (t < n_tiles && s0 + r < n_slices) runs_sm[static_cast<uint64_t>(s0 + r) * n_tiles + t] = s_t[c][r];
   }
 }
 
@@ -296,15 +362,16 @@ __device__ __forceinline__ uint8_t probe_rec(const uint64_t* s_slice, const uint
 }
 
 // The runs of 64 consecutive tiles are walked as ONE flattened record stream per wave: record k of
-// the stream belongs to the tile whose inclusive run-length prefix first exceeds k. The (uniform)
-// tile cursor advances in scalar registers, so every load covers 64 consecutive records (coalesced
-// except at run boundaries) and kUnroll loads are in flight per wave.
+// the stream belongs to the tile whose inclusive run-length prefix first exceeds k. Runs are padded
+// to 4 records, so each lane owns 4 consecutive, 16-byte aligned records of one run: one 16-B load
+// and one 4-B store per lane, 256 records per wave step. The (uniform) tile cursor lives in scalar
+// registers; a step visits only the few tiles its 256 records overlap.
 __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64_t* __restrict__ words,
                                                                    uint32_t splits, uint64_t n_tiles,
                                                                    const uint32_t* __restrict__ recs,
                                                                    const uint32_t* __restrict__ runs,
                                                                    uint8_t* __restrict__ passb) {
-  constexpr int kUnroll = 8;
+  constexpr int kUnroll = 4;
   __shared__ uint64_t s_slice[kSliceWords];
   __shared__ uint64_t s_masks[kNumMasks];
   const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
@@ -321,23 +388,23 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   const uint32_t* my_runs = runs + static_cast<uint64_t>(slice) * n_tiles;
   for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
     const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
-    const uint32_t cnt = info & 0xFFFFu;
-    const uint64_t base = (tb + lane) * kTileRows + (info >> 16);
+    const uint32_t cnt = info & 0xFFFFu;  // padded run length (multiple of 4)
+    const uint64_t base = (tb + lane) * kTileCap + (info >> 16);
     const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
     const uint32_t incl = wave_inclusive_sum(cnt);
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-    uint32_t j = 0;  // uniform: first tile of the batch whose inclusive prefix exceeds the group start
-    for (uint32_t k0 = 0; k0 < total; k0 += 64 * kUnroll) {
+    uint32_t j = 0;  // uniform: first tile of the batch whose inclusive prefix exceeds the step start
+    for (uint32_t k0 = 0; k0 < total; k0 += 256 * kUnroll) {
       uint64_t addr[kUnroll];
-      uint32_t rec[kUnroll];
+      u32x4 rec[kUnroll];
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) {
-        const uint32_t kf = k0 + u * 64;
-        const uint32_t k = kf + lane;
+        const uint32_t kf = k0 + u * 256;
+        const uint32_t k = kf + lane * 4;
         addr[u] = ~0ULL;
         if (kf < total) {
           while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
-          const uint32_t kl = (kf + 63 < total) ? kf + 63 : total - 1;
+          const uint32_t kl = (kf + 255 < total) ? kf + 255 : total - 1;
           for (uint32_t jj = j;; jj++) {
             const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
             const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
@@ -348,84 +415,70 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
             if (inc > kl) break;
           }
         }
-        rec[u] = addr[u] != ~0ULL ? recs[addr[u]] : 0u;
+        rec[u] = addr[u] != ~0ULL ? *reinterpret_cast<const u32x4*>(recs + addr[u]) : u32x4{0, 0, 0, 0};
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) {
-        if (addr[u] != ~0ULL) passb[addr[u]] = probe_rec(s_slice, s_masks, rec[u]);
+        if (addr[u] != ~0ULL) {
+          const uint32_t pv = static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][0])) |
+                              (static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][1])) << 8) |
+                              (static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][2])) << 16) |
+                              (static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][3])) << 24);
+          *reinterpret_cast<uint32_t*>(passb + addr[u]) = pv;
+        }
       }
     }
   }
 }
 
 // ---- partitioned probe, C: restore row order -> result bits + per-segment counts (P1's format) -----
-// Double-buffered: the next tile's pass bytes are in flight (registers) while this tile's are read
-// from LDS; one barrier per tile.
-__global__ __launch_bounds__(kTileThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
-                                                                const uint8_t* __restrict__ passb, uint64_t n,
-                                                                uint64_t n_tiles, uint64_t* __restrict__ out_bits,
-                                                                uint32_t* __restrict__ seg_counts) {
-  __shared__ uint8_t s_pass[2][kTileRows];
+// One 256-thread workgroup per tile (8 per CU keep several tiles in flight): the tile's pass bytes
+// are staged in LDS, then each wave walks 8 segments with one row per lane per step, so a ballot is
+// directly the row-ordered result word.
+constexpr int kUnpermuteThreads = 256;
+__global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
+                                                                     const uint8_t* __restrict__ passb, uint64_t n,
+                                                                     uint64_t n_tiles, uint64_t* __restrict__ out_bits,
+                                                                     uint32_t* __restrict__ seg_counts) {
+  __shared__ uint8_t s_pass[kTileCap];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
-  uint64_t tile = blockIdx.x;
-  u32x4 pre = tile < n_tiles ? reinterpret_cast<const u32x4*>(passb + tile * kTileRows)[threadIdx.x] : u32x4{0, 0, 0, 0};
-  for (uint32_t buf = 0; tile < n_tiles; tile += gridDim.x, buf ^= 1) {
-    reinterpret_cast<u32x4*>(s_pass[buf])[threadIdx.x] = pre;  // 1024 x 16 B = one tile
-    const uint64_t next = tile + gridDim.x;
-    if (next < n_tiles) pre = reinterpret_cast<const u32x4*>(passb + next * kTileRows)[threadIdx.x];
-    uint32_t pp[2][4];
-#pragma unroll
-    for (int sg = 0; sg < 2; sg++) {
-      const uint64_t base = (tile * (kTileRows / kSegRows) + wave * 2 + sg) * kSegRows;
-#pragma unroll
-      for (int c = 0; c < 4; c++) pp[sg][c] = *reinterpret_cast<const uint32_t*>(pos + base + c * 128 + lane * 2);
+  constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / (kUnpermuteThreads / 64);
+  for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+    {
+      const u32x4* src = reinterpret_cast<const u32x4*>(passb + tile * kTileCap);
+      for (uint32_t i = threadIdx.x; i < kTileCap / 16; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
     }
     __syncthreads();
+    for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+      const uint64_t seg = tile * (kTileRows / kSegRows) + wave * kSegsPerWave + sg;
+      if (seg >= n_segs) break;
+      const uint64_t base = seg * kSegRows;
+      uint16_t pp[8];
 #pragma unroll
-    for (int sg = 0; sg < 2; sg++) {
-      const uint64_t seg = tile * (kTileRows / kSegRows) + wave * 2 + sg;
-      if (seg < n_segs) {
-        const uint64_t base = seg * kSegRows;
-        uint64_t b[8];
-        uint32_t cnt = 0;
+      for (int c = 0; c < 8; c++) pp[c] = pos[base + c * 64 + lane];
+      uint64_t mine = 0;
+      uint32_t cnt = 0;
 #pragma unroll
-        for (int c = 0; c < 4; c++) {
-          const uint64_t row0 = base + c * 128 + lane * 2;
-          const bool p0 = row0 < n && s_pass[buf][pp[sg][c] & 0xFFFFu];
-          const bool p1 = row0 + 1 < n && s_pass[buf][pp[sg][c] >> 16];
-          b[c * 2] = ballot64(p0);
-          b[c * 2 + 1] = ballot64(p1);
-          cnt += __popcll(b[c * 2]) + __popcll(b[c * 2 + 1]);
-        }
-        uint64_t mine = 0;
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-#pragma unroll
-          for (int q = 0; q < 2; q++) {
-            const uint64_t x = spread2(b[c * 2] >> (32 * q)) | (spread2(b[c * 2 + 1] >> (32 * q)) << 1);
-            mine = (lane == static_cast<uint32_t>(c * 2 + q)) ? x : mine;
-          }
-        }
-        if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
-        if (lane == 0) seg_counts[seg] = cnt;
+      for (int c = 0; c < 8; c++) {
+        const uint64_t w = ballot64(base + c * 64 + lane < n && s_pass[pp[c]]);
+        cnt += __popcll(w);
+        mine = (lane == static_cast<uint32_t>(c)) ? w : mine;
       }
+      if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
+      if (lane == 0) seg_counts[seg] = cnt;
     }
+    __syncthreads();
   }
 }
 
 // ---- P2a: survivor count per group of 1024 segments --------------------------------------------
 __global__ __launch_bounds__(kBlockThreads) void group_sum_kernel(const uint32_t* __restrict__ seg_counts,
                                                                  uint64_t n_segs, uint32_t* __restrict__ group_sums) {
+  static_assert(kGroupSegs == kBlockThreads, "one segment count per thread");
   __shared__ uint32_t s_part[kWavesPerBlock];
-  const uint64_t first = static_cast<uint64_t>(blockIdx.x) * kGroupSegs + threadIdx.x * 4;
-  uint32_t s = 0;
-  if (first + 4 <= n_segs) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(seg_counts + first);
-    s = v[0] + v[1] + v[2] + v[3];
-  } else {
-    for (uint64_t i = first; i < n_segs && i < first + 4; i++) s += seg_counts[i];
-  }
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kGroupSegs + threadIdx.x;
+  uint32_t s = i < n_segs ? seg_counts[i] : 0u;
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -469,23 +522,14 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
   __shared__ uint32_t s_wave[kWavesPerBlock];
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kGroupSegs;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t c[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint64_t s = g0 + threadIdx.x * 4 + i;
-    c[i] = s < n_segs ? seg_counts[s] : 0u;
-  }
-  const uint32_t tsum = c[0] + c[1] + c[2] + c[3];
-  const uint32_t incl = wave_inclusive_sum(tsum);
+  const uint64_t sidx = g0 + threadIdx.x;
+  const uint32_t c = sidx < n_segs ? seg_counts[sidx] : 0u;
+  const uint32_t incl = wave_inclusive_sum(c);
   if (lane == 63) s_wave[wave] = incl;
   __syncthreads();
-  uint32_t off = group_offs[blockIdx.x] + incl - tsum;
+  uint32_t off = group_offs[blockIdx.x] + incl - c;
   for (uint32_t w = 0; w < wave; w++) off += s_wave[w];
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    s_off[threadIdx.x * 4 + i] = off;
-    off += c[i];
-  }
+  s_off[threadIdx.x] = off;
   __syncthreads();
   const uint64_t n_words = n_segs * kWordsPerSeg;
   for (uint32_t b = wave; b < kGroupSegs / 8; b += kWavesPerBlock) {
@@ -664,6 +708,58 @@ struct DeviceGuard {
   if (guard_.err != hipSuccess)                                                                   \
     return fail(RPT_ERR_HIP, "hipSetDevice(%d) failed: %s", (dev), hipGetErrorString(guard_.err))
 
+
+// ---- kernel timing (rpt_profiling_*; mirrors rpt_profiling.hpp's counters at kernel granularity) ----
+struct ProfRecord {
+  const char* name;
+  hipEvent_t start, end;
+};
+struct ProfStat {
+  uint64_t launches = 0;
+  double total_ms = 0.0;
+};
+std::atomic<int> g_prof_enabled{0};
+std::mutex g_prof_mu;
+std::vector<ProfRecord> g_prof_pending;
+std::vector<hipEvent_t> g_prof_free;
+std::vector<std::pair<std::string, ProfStat>> g_prof_stats;
+
+hipEvent_t prof_event() {
+  if (!g_prof_free.empty()) {
+    hipEvent_t e = g_prof_free.back();
+    g_prof_free.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Brackets one kernel launch with events on its stream when profiling is enabled.
+struct ProfScope {
+  const char* name;
+  hipStream_t stream;
+  hipEvent_t start = nullptr;
+  ProfScope(const char* n, hipStream_t s) : name(n), stream(s) {
+    if (!g_prof_enabled.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    start = prof_event();
+    if (start && hipEventRecord(start, stream) != hipSuccess) start = nullptr;
+  }
+  void end() {
+    if (!start) return;
+    std::lock_guard<std::mutex> lk(g_prof_mu);
+    hipEvent_t e = prof_event();
+    if (e && hipEventRecord(e, stream) == hipSuccess) {
+      g_prof_pending.push_back({name, start, e});
+    } else {
+      g_prof_free.push_back(start);
+      if (e) g_prof_free.push_back(e);
+    }
+    start = nullptr;
+  }
+};
+
 int num_cus(int device) {
   static std::mutex mu;
   static std::vector<int> cache;
@@ -697,7 +793,8 @@ struct ProbeWorkspace {
   uint32_t* recs;
   uint16_t* pos;
   uint8_t* passb;
-  uint32_t* runs;
+  uint32_t* runs;     // slice-major [slice][tile]
+  uint32_t* runs_tm;  // tile-major [tile][slice] (partition kernel output)
 };
 
 uint32_t slice_count(int log_num_blocks) {
@@ -730,16 +827,17 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* 
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
   const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
   const uint64_t padded = n_tiles * rpt::kTileRows;
-  size_t sz[8] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
-                  align256(n_groups * 4), align256(n_groups * 4), 0, 0, 0, 0};
+  size_t sz[9] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
+                  align256(n_groups * 4), align256(n_groups * 4), 0, 0, 0, 0, 0};
   if (partitioned) {
-    sz[4] = align256(padded * 4);
+    sz[4] = align256(n_tiles * rpt::kTileCap * 4);
     sz[5] = align256(padded * 2);
-    sz[6] = align256(padded);
+    sz[6] = align256(n_tiles * rpt::kTileCap);
     sz[7] = align256(static_cast<uint64_t>(slice_count(log_num_blocks)) * n_tiles * 4);
+    sz[8] = sz[7];
   }
-  size_t off[8], total = 0;
-  for (int i = 0; i < 8; i++) {
+  size_t off[9], total = 0;
+  for (int i = 0; i < 9; i++) {
     off[i] = total;
     total += sz[i];
   }
@@ -753,6 +851,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* 
     ws->pos = partitioned ? reinterpret_cast<uint16_t*>(p + off[5]) : nullptr;
     ws->passb = partitioned ? reinterpret_cast<uint8_t*>(p + off[6]) : nullptr;
     ws->runs = partitioned ? reinterpret_cast<uint32_t*>(p + off[7]) : nullptr;
+    ws->runs_tm = partitioned ? reinterpret_cast<uint32_t*>(p + off[8]) : nullptr;
   }
   return total;
 }
@@ -878,6 +977,10 @@ size_t rpt_probe_workspace_bytes(uint64_t n_rows, int log_num_blocks) {
   return workspace_layout(n_rows, log_num_blocks, part, nullptr, nullptr);
 }
 
+int rpt_probe_strategy_supported(int strategy, int log_num_blocks) {
+  return strategy == RPT_PROBE_AUTO ? 1 : strategy_supported(strategy, log_num_blocks);
+}
+
 int rpt_bf_set_probe_strategy(rpt_bf* bf, int strategy) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
   if (strategy < RPT_PROBE_AUTO || strategy > RPT_PROBE_PARTITIONED)
@@ -978,7 +1081,9 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const unsigned grid = persistent_grid(bf->device, n_segs);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  ProfScope prof1_("insert_kernel", as_stream(stream));
   RPT_DISPATCH_KD(launch_insert_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n, n_segs);
+  prof1_.end();
   RPT_LAUNCHED("insert_kernel");
   return RPT_OK;
 }
@@ -993,8 +1098,10 @@ int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, ui
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const unsigned grid = persistent_grid(bf->device, n_segs);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  ProfScope prof2_("probe_bits_kernel", as_stream(stream));
   RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n,
                   n_segs, out_bits, static_cast<uint32_t*>(nullptr));
+  prof2_.end();
   RPT_LAUNCHED("probe_bits_kernel");
   return RPT_OK;
 }
@@ -1023,31 +1130,49 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
   const bool dense = dense_ok(col, row_sel);
   if (strategy == RPT_PROBE_GATHER) {
     const unsigned grid = persistent_grid(bf->device, n_segs);
+    ProfScope prof3_("probe_bits_kernel", s);
     RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
+    prof3_.end();
     RPT_LAUNCHED("probe_bits_kernel");
   } else if (strategy == RPT_PROBE_LDS) {
     const uint64_t lds = (8ULL << L) + 8ULL * rpt::kNumMasks;
     const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(rpt::kBlocksPerCU, (160ULL << 10) / lds));
     const unsigned grid = static_cast<unsigned>(
         std::max<uint64_t>(1, std::min(ceil_div(n_segs, rpt::kWavesPerBlock), num_cus(bf->device) * per_cu)));
+    ProfScope prof4_("probe_bits_kernel<lds>", s);
     RPT_DISPATCH_KD(launch_probe_bits_lds_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
+    prof4_.end();
     RPT_LAUNCHED("probe_bits_kernel<lds>");
   } else {
     const uint32_t slices = slice_count(L);
     const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
     const int cus = num_cus(bf->device);
-    const unsigned g_tiles = static_cast<unsigned>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) * 2));
+    const unsigned g_tiles = static_cast<unsigned>(n_tiles);  // one tile per workgroup
+    ProfScope prof5_("partition_kernel", s);
     RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense, g_tiles, s, a, n, slices - 1, n_tiles, ws.recs, ws.pos,
-                    ws.runs);
+                    ws.runs_tm);
+    prof5_.end();
     RPT_LAUNCHED("partition_kernel");
+    {
+      ProfScope prof_t("runs_transpose_kernel", s);
+      hipLaunchKernelGGL(rpt::runs_transpose_kernel, dim3(static_cast<unsigned>(ceil_div(n_tiles, 64)), ceil_div(slices, 64)),
+                         dim3(rpt::kBlockThreads), 0, s, ws.runs_tm, slices, n_tiles, ws.runs);
+      prof_t.end();
+      RPT_LAUNCHED("runs_transpose_kernel");
+    }
     // >= 2 workgroups per CU in total, but never more splits than tiles
     const uint32_t splits = static_cast<uint32_t>(std::max<uint64_t>(
         1, std::min<uint64_t>(n_tiles, ceil_div(static_cast<uint64_t>(cus) * 2, slices))));
+    ProfScope prof6_("slice_probe_kernel", s);
     hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words,
                        splits, n_tiles, ws.recs, ws.runs, ws.passb);
+    prof6_.end();
     RPT_LAUNCHED("slice_probe_kernel");
-    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(g_tiles), dim3(rpt::kTileThreads), 0, s, ws.pos, ws.passb, n,
+    const unsigned g_unperm = static_cast<unsigned>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) * 8));
+    ProfScope prof7_("unpermute_kernel", s);
+    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(g_unperm), dim3(rpt::kUnpermuteThreads), 0, s, ws.pos, ws.passb, n,
                        n_tiles, ws.bits, ws.seg_counts);
+    prof7_.end();
     RPT_LAUNCHED("unpermute_kernel");
   }
   return RPT_OK;
@@ -1070,14 +1195,20 @@ int rpt_bf_probe_phase2(const uint32_t* row_sel, uint64_t n, uint32_t* out_sel, 
   workspace_layout(n, 0, false, workspace, &ws);
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
+  ProfScope prof8_("group_sum_kernel", s);
   hipLaunchKernelGGL(rpt::group_sum_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,
                      ws.seg_counts, n_segs, ws.group_sums);
+  prof8_.end();
   RPT_LAUNCHED("group_sum_kernel");
+  ProfScope prof9_("group_scan_kernel", s);
   hipLaunchKernelGGL(rpt::group_scan_kernel, dim3(1), dim3(1024), 0, s, ws.group_sums,
                      static_cast<uint32_t>(n_groups), ws.group_offs, out_count_dev);
+  prof9_.end();
   RPT_LAUNCHED("group_scan_kernel");
+  ProfScope prof10_("compact_kernel", s);
   hipLaunchKernelGGL(rpt::compact_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,
                      ws.bits, ws.seg_counts, n_segs, ws.group_offs, row_sel, out_sel);
+  prof10_.end();
   RPT_LAUNCHED("compact_kernel");
   return RPT_OK;
 }
@@ -1102,11 +1233,13 @@ int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, r
   const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 4096));
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
   hipStream_t s = as_stream(stream);
+  ProfScope prof11_("hash_kernel", s);
   switch (col->key_type) {
     case RPT_KEY_I64: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyI64>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
     case RPT_KEY_I32: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyI32>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
     default: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyHash>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
   }
+  prof11_.end();
   RPT_LAUNCHED("hash_kernel");
   return RPT_OK;
 }
@@ -1115,8 +1248,10 @@ int rpt_words_or_slices(uint64_t* dst, const uint64_t* srcs, uint32_t k, uint64_
   if (!dst || (!srcs && k > 0)) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
   if (n_words == 0) return RPT_OK;
   const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n_words / 2, rpt::kBlockThreads), 8192)));
+  ProfScope prof12_("or_slices_kernel", as_stream(stream));
   hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), dst, srcs, k,
                      n_words, 0);
+  prof12_.end();
   RPT_LAUNCHED("or_slices_kernel");
   return RPT_OK;
 }
@@ -1125,8 +1260,10 @@ int rpt_words_or(uint64_t* dst, const uint64_t* src, uint64_t n_words, rpt_strea
   if (!dst || !src) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
   if (n_words == 0) return RPT_OK;
   const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n_words / 2, rpt::kBlockThreads), 8192)));
+  ProfScope prof13_("or_slices_kernel", as_stream(stream));
   hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), dst, src, 1u,
                      n_words, 1);
+  prof13_.end();
   RPT_LAUNCHED("or_slices_kernel");
   return RPT_OK;
 }
@@ -1180,8 +1317,10 @@ int rpt_bf_fold(rpt_bf* bf, int* out_new_log_num_blocks) {
     const uint64_t slice = nb >> folds;
     // target slice 0 accumulates slices 1 .. 2^folds-1 (they never overlap the target)
     const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(slice / 2, rpt::kBlockThreads), 8192)));
+    ProfScope prof14_("or_slices_kernel(fold)", nullptr);
     hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, nullptr, bf->words,
                        bf->words + slice, static_cast<uint32_t>((1u << folds) - 1), slice, 1);
+    prof14_.end();
     RPT_LAUNCHED("or_slices_kernel(fold)");
     RPT_HIP(hipDeviceSynchronize());
     bf->log_num_blocks -= folds;
@@ -1235,12 +1374,59 @@ int rpt_bf_copy_words_from(rpt_bf* bf, const uint64_t* src_dev, uint64_t n_words
   return RPT_OK;
 }
 
+
+int rpt_profiling_enable(int enable) {
+  g_prof_enabled.store(enable ? 1 : 0);
+  return RPT_OK;
+}
+
+int rpt_profiling_reset(void) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& r : g_prof_pending) {
+    (void)hipEventSynchronize(r.end);
+    g_prof_free.push_back(r.start);
+    g_prof_free.push_back(r.end);
+  }
+  g_prof_pending.clear();
+  g_prof_stats.clear();
+  return RPT_OK;
+}
+
+int rpt_profiling_read(rpt_kernel_stat* out, int capacity) {
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto& r : g_prof_pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.end) != hipSuccess || hipEventElapsedTime(&ms, r.start, r.end) != hipSuccess)
+      return -fail(RPT_ERR_HIP, "profiling: event query failed");
+    auto it = std::find_if(g_prof_stats.begin(), g_prof_stats.end(), [&](const auto& p) { return p.first == r.name; });
+    if (it == g_prof_stats.end()) {
+      g_prof_stats.push_back({std::string(r.name), ProfStat{}});
+      it = g_prof_stats.end() - 1;
+    }
+    it->second.launches++;
+    it->second.total_ms += ms;
+    g_prof_free.push_back(r.start);
+    g_prof_free.push_back(r.end);
+  }
+  g_prof_pending.clear();
+  const int n = static_cast<int>(g_prof_stats.size());
+  for (int i = 0; i < n && i < capacity && out; i++) {
+    memset(out[i].name, 0, sizeof out[i].name);
+    strncpy(out[i].name, g_prof_stats[i].first.c_str(), sizeof out[i].name - 1);
+    out[i].launches = g_prof_stats[i].second.launches;
+    out[i].total_ms = g_prof_stats[i].second.total_ms;
+  }
+  return n;
+}
+
 // ---- bench / test workload generators (include/rpt_gpu_synth.h) ---------------------------------
 int rpt_synth_build_keys(int64_t* out, uint64_t start, uint64_t n, rpt_stream_t stream) {
   if (!out) return fail(RPT_ERR_INVALID_ARGUMENT, "null out");
   if (n == 0) return RPT_OK;
   const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 8192));
+  ProfScope prof15_("synth_build_kernel", as_stream(stream));
   hipLaunchKernelGGL(rpt::synth_build_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), out, start, n);
+  prof15_.end();
   RPT_LAUNCHED("synth_build_kernel");
   return RPT_OK;
 }
@@ -1251,8 +1437,10 @@ int rpt_synth_probe_keys(int64_t* out, uint64_t n_build, uint32_t p_permille, ui
   if (p_permille > 1000) return fail(RPT_ERR_INVALID_ARGUMENT, "p_permille %u > 1000", p_permille);
   if (n == 0) return RPT_OK;
   const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 8192));
+  ProfScope prof16_("synth_probe_kernel", as_stream(stream));
   hipLaunchKernelGGL(rpt::synth_probe_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), out, n_build,
                      p_permille, start, n);
+  prof16_.end();
   RPT_LAUNCHED("synth_probe_kernel");
   return RPT_OK;
 }

@@ -61,6 +61,12 @@ class BfInfo(ctypes.Structure):
     ]
 
 
+class KernelStat(ctypes.Structure):
+    """rpt_kernel_stat (include/rpt_gpu.h)."""
+
+    _fields_ = [("name", ctypes.c_char * 48), ("launches", c_uint64), ("total_ms", ctypes.c_double)]
+
+
 # name -> (restype, argtypes); every symbol include/rpt_gpu.h and include/rpt_gpu_synth.h declare.
 SIGNATURES = {
     "rpt_abi_version": (c_int, []),
@@ -70,6 +76,7 @@ SIGNATURES = {
     "rpt_bf_needs_resize": (c_int, [c_uint64, c_uint64]),
     "rpt_probe_workspace_bytes": (c_size_t, [c_uint64, c_int]),
     "rpt_bf_set_probe_strategy": (c_int, [c_void_p, c_int]),
+    "rpt_probe_strategy_supported": (c_int, [c_int, c_int]),
     "rpt_bf_probe_strategy": (c_int, [c_void_p]),
     "rpt_bf_create": (c_int, [c_int, c_uint64, POINTER(c_void_p)]),
     "rpt_bf_create_log_blocks": (c_int, [c_int, c_int, POINTER(c_void_p)]),
@@ -99,6 +106,9 @@ SIGNATURES = {
     "rpt_bf_copy_words_to": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_bf_copy_words_from": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_bf_set_has_data": (c_int, [c_void_p, c_int]),
+    "rpt_profiling_enable": (c_int, [c_int]),
+    "rpt_profiling_reset": (c_int, []),
+    "rpt_profiling_read": (c_int, [POINTER(KernelStat), c_int]),
     "rpt_synth_build_keys": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
     "rpt_synth_probe_keys": (c_int, [c_void_p, c_uint64, c_uint32, c_uint64, c_uint64, c_void_p]),
 }
@@ -127,3 +137,22 @@ def check(status: int) -> None:
     if status != RPT_OK:
         lib = load()
         raise RptError(status, lib.rpt_last_error().decode(errors="replace"))
+
+
+def kernel_times() -> dict:
+    """{kernel name: (launches, total_ms)} recorded since the last reset (see rpt_profiling_*)."""
+    lib = load()
+    n = lib.rpt_profiling_read(None, 0)
+    if n < 0:
+        check(-n)
+    arr = (KernelStat * max(n, 1))()
+    n = lib.rpt_profiling_read(arr, n)
+    return {arr[i].name.decode(): (arr[i].launches, arr[i].total_ms) for i in range(n)}
+
+
+def profiling(enable: bool) -> None:
+    check(load().rpt_profiling_enable(int(enable)))
+
+
+def profiling_reset() -> None:
+    check(load().rpt_profiling_reset())

@@ -116,6 +116,8 @@ int rpt_bf_set_finalized(rpt_bf* bf, int value);
 /* Select the probe strategy (rpt_probe_strategy); rpt_bf_probe_strategy returns the one a probe
  * will run now (AUTO resolved), or a negative status. */
 int rpt_bf_set_probe_strategy(rpt_bf* bf, int strategy);
+/* 1 if `strategy` can probe a 2^log_num_blocks-block filter, else 0. */
+int rpt_probe_strategy_supported(int strategy, int log_num_blocks);
 int rpt_bf_probe_strategy(const rpt_bf* bf);
 /* Zero every block and clear has_data (stream-ordered). */
 int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
@@ -177,6 +179,20 @@ int rpt_bf_copy_words_to(const rpt_bf* bf, uint64_t* dst_dev, uint64_t n_words, 
 int rpt_bf_copy_words_from(rpt_bf* bf, const uint64_t* src_dev, uint64_t n_words, rpt_stream_t stream);
 /* Mark has_data after words were filled by a device-side exchange (multi-GPU merge). */
 int rpt_bf_set_has_data(rpt_bf* bf, int value);
+
+/* ---- kernel timing ----------------------------------------------------------------------- */
+/* The reference's per-operator profiling counters (src/include/rpt_profiling.hpp:16-217), at kernel
+ * granularity: while enabled, every kernel the library launches is bracketed by HIP events on its
+ * own stream. rpt_profiling_read resolves pending events (waits for them), fills up to `capacity`
+ * entries and returns the number of distinct kernels (negative status on error). */
+typedef struct rpt_kernel_stat {
+  char name[48];
+  uint64_t launches;
+  double total_ms;
+} rpt_kernel_stat;
+int rpt_profiling_enable(int enable);
+int rpt_profiling_reset(void);
+int rpt_profiling_read(rpt_kernel_stat* out, int capacity);
 
 #ifdef __cplusplus
 }

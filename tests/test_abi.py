@@ -86,4 +86,16 @@ def test_argument_errors_are_reported():
     assert lib.rpt_bf_create_log_blocks(0, 41, ctypes.byref(out)) == _lib.RPT_ERR_INVALID_ARGUMENT
     assert lib.rpt_bf_destroy(None) == 0
     assert lib.rpt_bf_set_probe_strategy(None, 1) == _lib.RPT_ERR_INVALID_ARGUMENT
+
+
+def test_strategy_support_rules():
+    lib = _lib.load()
+    for L in range(0, 30):
+        assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_GATHER, L) == 1
+        assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_AUTO, L) == 1
+        assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_LDS, L) == (L <= 13)
+    # partitioned: at least one full LDS slice, at most 256 slices
+    part = [L for L in range(0, 30) if lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_PARTITIONED, L)]
+    assert part == list(range(part[0], part[0] + 9)) and part[0] in (13, 14)
+    assert lib.rpt_probe_strategy_supported(99, 10) == 0
     assert lib.rpt_synth_probe_keys(None, 1, 10, 0, 10, None) == _lib.RPT_ERR_INVALID_ARGUMENT

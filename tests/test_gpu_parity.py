@@ -12,11 +12,9 @@ STRATEGIES = {"gather": 1, "lds": 2, "partitioned": 3}
 
 
 def supported(strategy: str, log_num_blocks: int) -> bool:
-    if strategy == "lds":
-        return log_num_blocks <= 13
-    if strategy == "partitioned":
-        return 13 <= log_num_blocks <= 21
-    return True
+    from rpt_amd import _lib
+
+    return bool(_lib.load().rpt_probe_strategy_supported(STRATEGIES[strategy], log_num_blocks))
 
 
 def with_strategy(bf, strategy: str):
@@ -149,8 +147,8 @@ def test_dictionary_validity_rowsel_vs_oracle(rpt, strategy):
     orc.insert_keys(w, lnb, dict_vals, key_sel=key_sel[:5000], validity=vw)
     bf = rpt.BloomFilter(n)
     if strategy == "lds":
-        bf = rpt.BloomFilter(log_num_blocks=13)
         lnb = 13
+        bf = rpt.BloomFilter(log_num_blocks=lnb)
         w = orc.new_words(lnb)
         orc.insert_keys(w, lnb, dict_vals, key_sel=key_sel[:5000], validity=vw)
     with_strategy(bf, strategy)
