@@ -1,0 +1,393 @@
+// rpt_host.cpp — C++ host mirror of PTBloomFilter / PhysicalCreateBF / PhysicalUseBF over the
+// C-ABI (include/rpt_host.hpp). Host-side only: every device operation goes through rpt_gpu.h.
+#include "rpt_host.hpp"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstring>
+#include <utility>
+
+namespace rpt {
+
+namespace {
+
+void check(int status) {
+  if (status != RPT_OK) throw GpuError(status, std::string("librpt_gpu: ") + rpt_last_error());
+}
+
+void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw GpuError(RPT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DeviceScope {
+  int prev = -1, dev;
+  explicit DeviceScope(int d) : dev(d) {
+    check_hip(hipGetDevice(&prev), "hipGetDevice");
+    if (prev != d) check_hip(hipSetDevice(d), "hipSetDevice");
+  }
+  ~DeviceScope() {
+    if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+  }
+};
+
+size_t key_size(KeyType t) { return t == KeyType::I32 ? 4 : 8; }
+
+bool valid_bit(const uint64_t* validity, uint64_t idx) {
+  return validity == nullptr || ((validity[idx >> 6] >> (idx & 63)) & 1ULL);
+}
+
+// Flatten one column of `chunk` (FLAT / CONSTANT / DICTIONARY) into `keys` (element size of the
+// column) and row validity bits appended at row offset `row0` of `valid_words`.
+// Returns true if any row was NULL.
+bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* valid_words, uint64_t row0) {
+  const size_t es = key_size(v.key_type);
+  bool any_null = false;
+  auto put_valid = [&](uint64_t r, bool ok) {
+    const uint64_t g = row0 + r;
+    if (ok) valid_words[g >> 6] |= 1ULL << (g & 63);
+    else any_null = true;
+  };
+  switch (v.type) {
+    case VectorType::FLAT:
+      std::memcpy(keys, v.data, count * es);
+      for (uint64_t r = 0; r < count; r++) put_valid(r, valid_bit(v.validity, r));
+      break;
+    case VectorType::CONSTANT: {
+      const bool ok = valid_bit(v.validity, 0);
+      for (uint64_t r = 0; r < count; r++) {
+        std::memcpy(keys + r * es, v.data, es);
+        put_valid(r, ok);
+      }
+      break;
+    }
+    case VectorType::DICTIONARY: {
+      const uint8_t* src = static_cast<const uint8_t*>(v.data);
+      for (uint64_t r = 0; r < count; r++) {
+        const uint32_t k = v.sel[r];
+        if (k >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
+        std::memcpy(keys + r * es, src + static_cast<uint64_t>(k) * es, es);
+        put_valid(r, valid_bit(v.validity, k));
+      }
+      break;
+    }
+  }
+  return any_null;
+}
+
+// Stage column `col` of `chunks` to the device as one flat key column (slots 0/1 of the context).
+rpt_key_column stage(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col, uint64_t total) {
+  if (chunks.empty()) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "no chunks");
+  const Vector& v0 = chunks[0]->data.at(col);
+  const size_t es = key_size(v0.key_type);
+  const uint64_t nwords = (total + 63) / 64;
+  auto* hkeys = static_cast<uint8_t*>(ctx.host(0, std::max<size_t>(total * es, 16)));
+  auto* hvalid = static_cast<uint64_t*>(ctx.host(1, std::max<size_t>(nwords * 8, 8)));
+  std::memset(hvalid, 0, nwords * 8);
+  bool any_null = false;
+  uint64_t row = 0;
+  for (const DataChunk* c : chunks) {
+    const Vector& v = c->data.at(col);
+    if (v.key_type != v0.key_type) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "mixed key types in one column");
+    any_null |= flatten_column(v, c->count, hkeys + row * es, hvalid, row);
+    row += c->count;
+  }
+  void* dkeys = ctx.dev(0, std::max<size_t>(total * es, 16));
+  void* dvalid = ctx.dev(1, std::max<size_t>(nwords * 8, 8));
+  auto s = static_cast<hipStream_t>(ctx.stream());
+  check_hip(hipMemcpyAsync(dkeys, hkeys, total * es, hipMemcpyHostToDevice, s), "stage keys");
+  if (any_null) check_hip(hipMemcpyAsync(dvalid, hvalid, nwords * 8, hipMemcpyHostToDevice, s), "stage validity");
+  rpt_key_column kc;
+  kc.key_type = static_cast<int32_t>(v0.key_type);
+  kc.keys = dkeys;
+  kc.key_sel = nullptr;
+  kc.validity = any_null ? static_cast<const uint64_t*>(dvalid) : nullptr;
+  return kc;
+}
+
+uint64_t total_rows(const std::vector<const DataChunk*>& chunks) {
+  uint64_t t = 0;
+  for (const DataChunk* c : chunks) t += c->count;
+  return t;
+}
+
+void require_single_column(const std::vector<uint64_t>& cols) {
+  // The hot path always hashes exactly one column (physical_create_bf.cpp:225,403,
+  // physical_use_bf.cpp:163); composite keys (CombineHash) are SURVEY §8f row 4.
+  if (cols.size() != 1) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "exactly one key column per filter is supported");
+}
+
+}  // namespace
+
+// ---- DeviceContext -----------------------------------------------------------------------------
+DeviceContext::DeviceContext(int device) : device_(device) {
+  DeviceScope ds(device_);
+  hipStream_t s;
+  check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  stream_ = s;
+}
+
+DeviceContext::~DeviceContext() {
+  DeviceScope ds(device_);
+  if (stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
+  for (auto& b : host_)
+    if (b.p) (void)hipHostFree(b.p);
+  for (auto& b : dev_)
+    if (b.p) (void)hipFree(b.p);
+  if (stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
+}
+
+void DeviceContext::synchronize() {
+  DeviceScope ds(device_);
+  check_hip(hipStreamSynchronize(static_cast<hipStream_t>(stream_)), "hipStreamSynchronize");
+}
+
+void* DeviceContext::host(int slot, size_t bytes) {
+  Buf& b = host_[slot];
+  if (b.cap < bytes) {
+    synchronize();
+    if (b.p) check_hip(hipHostFree(b.p), "hipHostFree");
+    b.p = nullptr;
+    const size_t cap = std::max(bytes, 2 * b.cap);
+    check_hip(hipHostMalloc(&b.p, cap, hipHostMallocDefault), "hipHostMalloc");
+    b.cap = cap;
+  }
+  return b.p;
+}
+
+void* DeviceContext::dev(int slot, size_t bytes) {
+  Buf& b = dev_[slot];
+  if (b.cap < bytes) {
+    synchronize();
+    DeviceScope ds(device_);
+    if (b.p) check_hip(hipFree(b.p), "hipFree");
+    b.p = nullptr;
+    const size_t cap = std::max(bytes, 2 * b.cap);
+    check_hip(hipMalloc(&b.p, cap), "hipMalloc");
+    b.cap = cap;
+  }
+  return b.p;
+}
+
+// ---- PTBloomFilter -------------------------------------------------------------------------------
+PTBloomFilter::~PTBloomFilter() {
+  if (bf_) rpt_bf_destroy(bf_);
+}
+
+void PTBloomFilter::Initialize(int device, uint32_t est_num_rows) {
+  if (bf_) {
+    rpt_bf_destroy(bf_);
+    bf_ = nullptr;
+  }
+  check(rpt_bf_create(device, est_num_rows, &bf_));
+}
+
+void PTBloomFilter::Insert(DeviceContext& ctx, const DataChunk& chunk, const std::vector<uint64_t>& cols) {
+  InsertBatch(ctx, {&chunk}, cols);
+}
+
+void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                                const std::vector<uint64_t>& cols) {
+  require_single_column(cols);
+  const uint64_t total = total_rows(chunks);
+  if (total == 0) return;  // bloom_filter.cpp:72-74
+  rpt_key_column kc = stage(ctx, chunks, cols[0], total);
+  check(rpt_bf_insert(bf_, &kc, total, ctx.stream()));
+  ctx.synchronize();  // the staging buffers are reused by the next call
+}
+
+uint64_t PTBloomFilter::LookupSel(DeviceContext& ctx, const DataChunk& chunk, SelectionVector& sel,
+                                  const std::vector<uint64_t>& cols) const {
+  std::vector<SelectionVector> sels;
+  LookupSelBatch(ctx, {&chunk}, sels, cols);
+  sel.swap(sels[0]);
+  return sel.size();
+}
+
+void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                                   std::vector<SelectionVector>& sels, const std::vector<uint64_t>& cols) const {
+  require_single_column(cols);
+  sels.assign(chunks.size(), SelectionVector());
+  const uint64_t total = total_rows(chunks);
+  if (total == 0) return;  // bloom_filter.cpp:63-65
+  rpt_key_column kc = stage(ctx, chunks, cols[0], total);
+  rpt_bf_info info;
+  check(rpt_bf_get_info(bf_, &info));
+  const size_t ws_bytes = rpt_probe_workspace_bytes(total, info.log_num_blocks);
+  void* ws = ctx.dev(2, ws_bytes);
+  auto* d_sel = static_cast<uint32_t*>(ctx.dev(3, total * 4));
+  auto* d_cnt = static_cast<uint64_t*>(ctx.dev(4, 8));
+  check(rpt_bf_probe(bf_, &kc, nullptr, total, d_sel, d_cnt, ws, ws_bytes, ctx.stream()));
+  auto* h_cnt = static_cast<uint64_t*>(ctx.host(2, 8));
+  auto s = static_cast<hipStream_t>(ctx.stream());
+  check_hip(hipMemcpyAsync(h_cnt, d_cnt, 8, hipMemcpyDeviceToHost, s), "copy count");
+  ctx.synchronize();
+  const uint64_t cnt = *h_cnt;
+  auto* h_sel = static_cast<uint32_t*>(ctx.host(3, std::max<uint64_t>(cnt, 1) * 4));
+  if (cnt) check_hip(hipMemcpyAsync(h_sel, d_sel, cnt * 4, hipMemcpyDeviceToHost, s), "copy sel");
+  ctx.synchronize();
+  // split the batch-wide ascending sel into per-chunk sels
+  uint64_t k = 0, start = 0;
+  for (size_t i = 0; i < chunks.size(); i++) {
+    const uint64_t end = start + chunks[i]->count;
+    SelectionVector& out = sels[i];
+    while (k < cnt && h_sel[k] < end) out.push_back(static_cast<uint32_t>(h_sel[k++] - start));
+    start = end;
+  }
+}
+
+void PTBloomFilter::ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const std::vector<DataChunk>& data,
+                                          const std::vector<uint64_t>& cols) {
+  check(rpt_bf_reinitialize(bf_, actual_rows));
+  std::vector<const DataChunk*> ptrs;
+  for (const DataChunk& c : data)
+    if (c.count) ptrs.push_back(&c);
+  if (!ptrs.empty()) InsertBatch(ctx, ptrs, cols);
+}
+
+uint64_t PTBloomFilter::SizedForRows() const {
+  rpt_bf_info i;
+  check(rpt_bf_get_info(bf_, &i));
+  return i.sized_for_rows;
+}
+
+bool PTBloomFilter::IsEmpty() const {
+  rpt_bf_info i;
+  check(rpt_bf_get_info(bf_, &i));
+  return !i.has_data;
+}
+
+int PTBloomFilter::LogNumBlocks() const {
+  rpt_bf_info i;
+  check(rpt_bf_get_info(bf_, &i));
+  return i.log_num_blocks;
+}
+
+std::vector<uint64_t> PTBloomFilter::ExportWords() const {
+  rpt_bf_info i;
+  check(rpt_bf_get_info(bf_, &i));
+  std::vector<uint64_t> w(i.num_blocks);
+  check(rpt_bf_export_words(bf_, w.data(), w.size()));
+  return w;
+}
+
+// ---- CreateBF ------------------------------------------------------------------------------------
+CreateBF::CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices)
+    : device_(device), estimated_cardinality_(estimated_cardinality), cols_(std::move(bound_column_indices)) {
+  for (size_t i = 0; i < cols_.size(); i++) {
+    auto bf = std::make_shared<PTBloomFilter>();
+    // CreateBFGlobalSinkState: Initialize(context, op.estimated_cardinality) -> uint32 (cpp:179-186)
+    bf->Initialize(device_, static_cast<uint32_t>(estimated_cardinality_));
+    filters_.push_back(std::move(bf));
+    resized_.push_back(false);
+  }
+}
+
+void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
+  // materialize the key columns (flattened, owned) for a possible rehash in Finalize
+  DataChunk m;
+  m.count = chunk.count;
+  m.data.resize(chunk.data.size());
+  for (uint64_t col : cols_) {
+    const Vector& v = chunk.data.at(col);
+    const size_t es = key_size(v.key_type);
+    std::vector<uint64_t> keys((chunk.count * es + 7) / 8 + 1, 0);
+    std::vector<uint64_t> valid((chunk.count + 63) / 64 + 1, 0);
+    const bool any_null = flatten_column(v, chunk.count, reinterpret_cast<uint8_t*>(keys.data()), valid.data(), 0);
+    Vector f;
+    f.type = VectorType::FLAT;
+    f.key_type = v.key_type;
+    f.data = keys.data();  // heap buffers keep their address when the vectors are moved
+    f.validity = any_null ? valid.data() : nullptr;
+    local.storage.push_back(std::move(keys));
+    local.storage.push_back(std::move(valid));
+    m.data[col] = f;
+  }
+  local.chunks.push_back(std::move(m));
+  // insert into one filter per build column (physical_create_bf.cpp:221-227)
+  for (size_t i = 0; i < cols_.size(); i++) filters_[i]->Insert(local.ctx, chunk, {cols_[i]});
+}
+
+void CreateBF::Combine(LocalState& local) {
+  std::lock_guard<std::mutex> lk(lock_);
+  for (auto& c : local.chunks) {
+    total_rows_ += c.count;
+    all_chunks_.push_back(std::move(c));
+  }
+  for (auto& s : local.storage) all_storage_.push_back(std::move(s));
+  local.chunks.clear();
+  local.storage.clear();
+}
+
+void CreateBF::Finalize() {
+  const uint64_t actual_rows = total_rows_;
+  if (actual_rows > 0) {
+    DeviceContext ctx(device_);
+    for (size_t i = 0; i < filters_.size(); i++) {
+      auto& bf = *filters_[i];
+      // physical_create_bf.cpp:394-398: resize iff actual*8 > NextPow2(max(512, sized_for*12))
+      if (rpt_bf_needs_resize(bf.SizedForRows(), actual_rows)) {
+        bf.ReinitializeAndRehash(ctx, actual_rows, all_chunks_, {cols_[i]});
+        resized_[i] = true;
+      }
+    }
+  }
+  for (auto& bf : filters_) bf->finalized_ = true;  // physical_create_bf.cpp:409-413
+}
+
+// ---- UseBF ---------------------------------------------------------------------------------------
+UseBF::UseBF(std::vector<std::shared_ptr<PTBloomFilter>> filters, std::vector<uint64_t> bound_column_indices,
+             bool passthrough)
+    : filters_(std::move(filters)), cols_(std::move(bound_column_indices)), passthrough_(passthrough) {
+  if (filters_.size() != cols_.size()) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "one bound column per filter");
+}
+
+uint64_t UseBF::Execute(DeviceContext& ctx, const DataChunk& input, SelectionVector& out) const {
+  const uint64_t n = input.count;
+  out.resize(n);
+  for (uint64_t r = 0; r < n; r++) out[r] = static_cast<uint32_t>(r);
+  if (passthrough_) return n;  // physical_use_bf.cpp:62-66
+  rows_in_ += n;
+  if (filters_.empty() || n == 0) {  // cpp:113-121
+    rows_out_ += n;
+    return n;
+  }
+  for (size_t i = 0; i < filters_.size(); i++) {
+    const auto& bf = filters_[i];
+    if (!bf || !bf->finalized_) continue;  // cpp:139-142
+    if (bf->IsEmpty()) {                   // cpp:145-155
+      out.clear();
+      return 0;
+    }
+    // LookupSel over the current slice of the input (physical_use_bf.cpp:163,176-179)
+    DataChunk sliced;
+    sliced.count = out.size();
+    sliced.data.resize(input.data.size());
+    const Vector& v = input.data.at(cols_[i]);
+    Vector sv = v;
+    std::vector<uint32_t> composed;
+    if (v.type == VectorType::FLAT) {
+      sv.type = VectorType::DICTIONARY;
+      sv.sel = out.data();
+      sv.dict_size = n;
+    } else if (v.type == VectorType::DICTIONARY) {
+      composed.resize(out.size());
+      for (size_t r = 0; r < out.size(); r++) composed[r] = v.sel[out[r]];
+      sv.sel = composed.data();
+    }
+    sliced.data[cols_[i]] = sv;
+    SelectionVector sel;
+    const uint64_t cnt = bf->LookupSel(ctx, sliced, sel, {cols_[i]});
+    if (cnt == 0) {  // cpp:166-173
+      out.clear();
+      return 0;
+    }
+    SelectionVector next(cnt);
+    for (uint64_t r = 0; r < cnt; r++) next[r] = out[sel[r]];
+    out.swap(next);
+  }
+  rows_out_ += out.size();
+  return out.size();
+}
+
+}  // namespace rpt

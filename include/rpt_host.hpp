@@ -1,0 +1,172 @@
+// rpt_host.hpp — C++ host mirror of the predicate-transfer hot path over librpt_gpu.so.
+//
+// What a DuckDB-side shim links against (C++17, no DuckDB types): the reference's PTBloomFilter
+// (src/include/bloom_filter.hpp:22-57) and the hot-path logic of PhysicalCreateBF
+// (src/operators/physical_create_bf.cpp:201-419) and PhysicalUseBF::ExecuteInternal
+// (src/operators/physical_use_bf.cpp:60-198), operating on DuckDB-shaped key vectors. Errors are
+// C++ exceptions (GpuError), as in the reference (DuckDB exceptions); nothing throws across the
+// C-ABI underneath.
+//
+// Vectors are HOST-resident (DuckDB DataChunks live in host memory). Each call stages its rows
+// to the device through pinned buffers on the caller's HIP stream; callers that own device-resident
+// columns should use the C-ABI (rpt_gpu.h) directly. The *Batch entry points concatenate many
+// 2048-row chunks into one device call, which is how the shim amortises PCIe latency.
+#pragma once
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "rpt_gpu.h"
+
+namespace rpt {
+
+class GpuError : public std::runtime_error {
+ public:
+  GpuError(int status, const std::string& what) : std::runtime_error(what), status_(status) {}
+  int status() const { return status_; }
+
+ private:
+  int status_;
+};
+
+// DuckDB VectorType subset the hot path sees (HashColumns flattens CONSTANT, bloom_filter.cpp:19-21).
+enum class VectorType { FLAT, CONSTANT, DICTIONARY };
+enum class KeyType { I32 = RPT_KEY_I32, I64 = RPT_KEY_I64 };
+
+// One key column of a DataChunk.
+//   FLAT:       data[row], validity indexed by row
+//   CONSTANT:   data[0] for every row, validity bit 0 for every row
+//   DICTIONARY: data[sel[row]] (dictionary of dict_size entries), validity indexed by sel[row]
+struct Vector {
+  VectorType type = VectorType::FLAT;
+  KeyType key_type = KeyType::I64;
+  const void* data = nullptr;
+  const uint32_t* sel = nullptr;       // DICTIONARY only
+  uint64_t dict_size = 0;              // DICTIONARY only
+  const uint64_t* validity = nullptr;  // DuckDB ValidityMask words; nullptr = all valid
+};
+
+struct DataChunk {
+  std::vector<Vector> data;
+  uint64_t count = 0;  // <= 2048 in DuckDB; any size here
+};
+
+using SelectionVector = std::vector<uint32_t>;  // sel_t
+
+// Device stream + pinned/device staging owned by one host thread (DuckDB thread-local state).
+class DeviceContext {
+ public:
+  explicit DeviceContext(int device);
+  ~DeviceContext();
+  DeviceContext(const DeviceContext&) = delete;
+  DeviceContext& operator=(const DeviceContext&) = delete;
+  int device() const { return device_; }
+  void* stream() const { return stream_; }
+  void synchronize();
+
+  // internal: grow-on-demand buffers
+  void* host(int slot, size_t bytes);
+  void* dev(int slot, size_t bytes);
+
+ private:
+  int device_;
+  void* stream_ = nullptr;
+  struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+  };
+  Buf host_[8], dev_[8];
+};
+
+// PTBloomFilter (bloom_filter.hpp:22-57) with the filter on the device.
+class PTBloomFilter {
+ public:
+  PTBloomFilter() = default;
+  ~PTBloomFilter();
+  PTBloomFilter(const PTBloomFilter&) = delete;
+  PTBloomFilter& operator=(const PTBloomFilter&) = delete;
+
+  // bloom_filter.cpp:27-32 (est_num_rows is uint32 as in physical_create_bf.cpp:187)
+  void Initialize(int device, uint32_t est_num_rows);
+  // bloom_filter.cpp:70-78: thread-safe (device atomic OR); no-op on an empty chunk
+  void Insert(DeviceContext& ctx, const DataChunk& chunk, const std::vector<uint64_t>& cols);
+  void InsertBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, const std::vector<uint64_t>& cols);
+  // bloom_filter.cpp:60-68: ascending surviving row ids; returns the count
+  uint64_t LookupSel(DeviceContext& ctx, const DataChunk& chunk, SelectionVector& sel,
+                     const std::vector<uint64_t>& cols) const;
+  // many chunks in one device call; sels[i] holds chunk i's survivors (ids relative to chunk i)
+  void LookupSelBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                      std::vector<SelectionVector>& sels, const std::vector<uint64_t>& cols) const;
+  // bloom_filter.cpp:34-58: reallocate for actual_rows and re-insert the materialized chunks
+  void ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const std::vector<DataChunk>& data,
+                             const std::vector<uint64_t>& cols);
+
+  uint64_t SizedForRows() const;
+  bool IsEmpty() const;
+  int LogNumBlocks() const;
+  std::vector<uint64_t> ExportWords() const;
+  rpt_bf* native() const { return bf_; }
+
+  bool finalized_ = false;
+
+ private:
+  rpt_bf* bf_ = nullptr;
+};
+
+// The hot-path part of PhysicalCreateBF: parallel Sink (materialize + insert), Combine, Finalize
+// (resize rule + rehash, finalized_), one filter per build column (bloom_filter_map,
+// physical_create_bf.hpp:73). Materialization keeps the build chunks' key columns (the reference
+// keeps full rows in a ColumnDataCollection, physical_create_bf.cpp:211-218).
+class CreateBF {
+ public:
+  struct LocalState {
+    explicit LocalState(int device) : ctx(device) {}
+    DeviceContext ctx;
+    std::vector<DataChunk> chunks;               // materialized key columns (views of owned storage)
+    std::vector<std::vector<uint64_t>> storage;  // owned copies backing `chunks`
+  };
+
+  CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices);
+  std::unique_ptr<LocalState> MakeLocalState() const { return std::make_unique<LocalState>(device_); }
+  void Sink(LocalState& local, const DataChunk& chunk) const;  // physical_create_bf.cpp:201-242
+  void Combine(LocalState& local);                             // physical_create_bf.cpp:244-275
+  void Finalize();                                             // physical_create_bf.cpp:352-419
+  std::shared_ptr<PTBloomFilter> GetBloomFilter(size_t build_column) const { return filters_.at(build_column); }
+  uint64_t MaterializedRows() const { return total_rows_; }
+  bool Resized(size_t build_column) const { return resized_.at(build_column); }
+
+ private:
+  int device_;
+  uint64_t estimated_cardinality_;
+  std::vector<uint64_t> cols_;
+  std::vector<std::shared_ptr<PTBloomFilter>> filters_;
+  std::vector<bool> resized_;
+  std::mutex lock_;
+  std::vector<DataChunk> all_chunks_;
+  std::vector<std::vector<uint64_t>> all_storage_;
+  uint64_t total_rows_ = 0;
+};
+
+// PhysicalUseBF::ExecuteInternal (physical_use_bf.cpp:60-198): AND of the filters over the chunk,
+// in filter order, with its early exits (empty filter -> 0 rows, 0 survivors -> stop) and skips
+// (filter not finalized). Returns the surviving row ids of the input chunk (ascending).
+class UseBF {
+ public:
+  UseBF(std::vector<std::shared_ptr<PTBloomFilter>> filters, std::vector<uint64_t> bound_column_indices,
+        bool passthrough = false);
+  uint64_t Execute(DeviceContext& ctx, const DataChunk& input, SelectionVector& out) const;
+  uint64_t rows_in() const { return rows_in_; }
+  uint64_t rows_out() const { return rows_out_; }
+
+ private:
+  std::vector<std::shared_ptr<PTBloomFilter>> filters_;
+  std::vector<uint64_t> cols_;
+  bool passthrough_;
+  mutable uint64_t rows_in_ = 0, rows_out_ = 0;  // UseBFStats (rpt_profiling.hpp) counters
+};
+
+}  // namespace rpt

@@ -1,0 +1,274 @@
+// test_host_mirror.cpp — the C++ host mirror (include/rpt_host.hpp) end to end on the GPU, checked
+// against the CPU restatement (oracle/librpt_oracle.so, test infrastructure).
+//
+// CREATE_BF: 4 sink threads, 2048-row chunks (last one ragged), FLAT/CONSTANT/DICTIONARY vectors with
+// NULLs, an under-estimated cardinality so Finalize must ReinitializeAndRehash; then USE_BF with two
+// filters (chain = AND), the empty-build early exit, the not-finalized skip and passthrough.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "rpt_host.hpp"
+
+extern "C" {
+int rpt_oracle_log_num_blocks(uint64_t n_rows);
+void rpt_oracle_insert_i64(uint64_t* words, int log_nb, const int64_t* keys, const uint32_t* key_sel,
+                           const uint64_t* validity, uint64_t n);
+void rpt_oracle_insert_i32(uint64_t* words, int log_nb, const int32_t* keys, const uint32_t* key_sel,
+                           const uint64_t* validity, uint64_t n);
+uint64_t rpt_oracle_probe_i64(const uint64_t* words, int log_nb, const int64_t* keys, const uint32_t* key_sel,
+                              const uint64_t* validity, uint64_t n, uint32_t* sel);
+uint64_t rpt_oracle_probe_i32(const uint64_t* words, int log_nb, const int32_t* keys, const uint32_t* key_sel,
+                              const uint64_t* validity, uint64_t n, uint32_t* sel);
+}
+
+static int g_fail = 0;
+#define EXPECT(cond, ...)                        \
+  do {                                           \
+    if (!(cond)) {                               \
+      fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      fprintf(stderr, __VA_ARGS__);              \
+      fprintf(stderr, "\n");                     \
+      g_fail++;                                  \
+    }                                            \
+  } while (0)
+
+// A host-side "table" of two key columns, with per-chunk vector shapes.
+struct Table {
+  std::vector<int64_t> c0;   // BIGINT keys
+  std::vector<bool> v0;      // validity of c0
+  std::vector<int32_t> c1;   // INTEGER keys
+  std::vector<bool> v1;
+};
+
+static std::vector<uint64_t> pack(const std::vector<bool>& v, size_t lo, size_t n) {
+  std::vector<uint64_t> w((n + 63) / 64 + 1, 0);
+  for (size_t i = 0; i < n; i++)
+    if (v[lo + i]) w[i / 64] |= 1ULL << (i % 64);
+  return w;
+}
+
+// Chunk storage: keeps the buffers each rpt::Vector points into alive.
+struct ChunkStore {
+  std::vector<std::vector<int64_t>> i64;
+  std::vector<std::vector<int32_t>> i32;
+  std::vector<std::vector<uint32_t>> sel;
+  std::vector<std::vector<uint64_t>> valid;
+  std::vector<rpt::DataChunk> chunks;
+};
+
+// Cut rows [0, n) into 2048-row chunks; chunk k uses shape k % 3 for column 0 (FLAT, DICTIONARY, and
+// CONSTANT when the chunk's c0 values are all equal) and DICTIONARY for column 1 on odd chunks.
+static void make_chunks(const Table& t, size_t n, ChunkStore& st, bool allow_constant) {
+  for (size_t lo = 0, k = 0; lo < n; lo += 2048, k++) {
+    const size_t cnt = std::min<size_t>(2048, n - lo);
+    rpt::DataChunk ch;
+    ch.count = cnt;
+    ch.data.resize(3);
+    // column 0
+    rpt::Vector a;
+    a.key_type = rpt::KeyType::I64;
+    bool all_same = true;
+    for (size_t i = 1; i < cnt; i++) all_same &= (t.c0[lo + i] == t.c0[lo] && t.v0[lo + i] == t.v0[lo]);
+    if (allow_constant && all_same) {
+      st.i64.push_back({t.c0[lo]});
+      st.valid.push_back({t.v0[lo] ? 1ULL : 0ULL});
+      a.type = rpt::VectorType::CONSTANT;
+      a.data = st.i64.back().data();
+      a.validity = st.valid.back().data();
+    } else if (k % 3 == 1) {
+      // dictionary: reversed distinct copy + selection
+      std::vector<int64_t> dict(cnt);
+      std::vector<uint32_t> sel(cnt);
+      std::vector<bool> dv(cnt);
+      for (size_t i = 0; i < cnt; i++) {
+        dict[cnt - 1 - i] = t.c0[lo + i];
+        dv[cnt - 1 - i] = t.v0[lo + i];
+        sel[i] = static_cast<uint32_t>(cnt - 1 - i);
+      }
+      std::vector<uint64_t> w((cnt + 63) / 64 + 1, 0);
+      for (size_t i = 0; i < cnt; i++)
+        if (dv[i]) w[i / 64] |= 1ULL << (i % 64);
+      st.i64.push_back(std::move(dict));
+      st.sel.push_back(std::move(sel));
+      st.valid.push_back(std::move(w));
+      a.type = rpt::VectorType::DICTIONARY;
+      a.data = st.i64.back().data();
+      a.sel = st.sel.back().data();
+      a.dict_size = cnt;
+      a.validity = st.valid.back().data();
+    } else {
+      st.i64.push_back(std::vector<int64_t>(t.c0.begin() + lo, t.c0.begin() + lo + cnt));
+      st.valid.push_back(pack(t.v0, lo, cnt));
+      a.type = rpt::VectorType::FLAT;
+      a.data = st.i64.back().data();
+      a.validity = st.valid.back().data();
+    }
+    ch.data[0] = a;
+    // column 1 (INTEGER)
+    rpt::Vector b;
+    b.key_type = rpt::KeyType::I32;
+    if (k % 2) {
+      std::vector<int32_t> dict(cnt);
+      std::vector<uint32_t> sel(cnt);
+      for (size_t i = 0; i < cnt; i++) {
+        dict[i] = t.c1[lo + i];
+        sel[i] = static_cast<uint32_t>(i);
+      }
+      st.i32.push_back(std::move(dict));
+      st.sel.push_back(std::move(sel));
+      st.valid.push_back(pack(t.v1, lo, cnt));
+      b.type = rpt::VectorType::DICTIONARY;
+      b.data = st.i32.back().data();
+      b.sel = st.sel.back().data();
+      b.dict_size = cnt;
+      b.validity = st.valid.back().data();
+    } else {
+      st.i32.push_back(std::vector<int32_t>(t.c1.begin() + lo, t.c1.begin() + lo + cnt));
+      st.valid.push_back(pack(t.v1, lo, cnt));
+      b.type = rpt::VectorType::FLAT;
+      b.data = st.i32.back().data();
+      b.validity = st.valid.back().data();
+    }
+    ch.data[1] = b;
+    ch.data[2] = rpt::Vector();  // an unrelated payload column the operators never touch
+    st.chunks.push_back(std::move(ch));
+  }
+}
+
+static Table make_table(size_t n, uint64_t seed, int null_every, size_t const_run) {
+  std::mt19937_64 rng(seed);
+  Table t;
+  t.c0.resize(n);
+  t.v0.resize(n);
+  t.c1.resize(n);
+  t.v1.resize(n);
+  for (size_t i = 0; i < n; i++) {
+    t.c0[i] = static_cast<int64_t>(rng() % 200000) - 100000;
+    t.v0[i] = null_every == 0 || (i % null_every) != 0;
+    t.c1[i] = static_cast<int32_t>(rng() % 300000) - 7;
+    t.v1[i] = null_every == 0 || (i % (null_every + 2)) != 1;
+  }
+  // a constant chunk (chunk 3) for the CONSTANT vector path
+  for (size_t i = 3 * 2048; i < std::min(n, 3 * 2048 + const_run); i++) {
+    t.c0[i] = 4242;
+    t.v0[i] = true;
+  }
+  return t;
+}
+
+int main() {
+  try {
+    const int dev = 0;
+    // ---------------- build -------------------------------------------------------------------
+    const size_t nb = 50001;
+    Table bt = make_table(nb, 1, 97, 2048);
+    ChunkStore bst;
+    make_chunks(bt, nb, bst, true);
+    rpt::CreateBF create(dev, /*estimated_cardinality=*/1000, {0, 1});
+    std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> locals;
+    for (int t = 0; t < 4; t++) locals.push_back(create.MakeLocalState());
+    std::vector<std::thread> ths;
+    for (int t = 0; t < 4; t++) {
+      ths.emplace_back([&, t] {
+        for (size_t k = t; k < bst.chunks.size(); k += 4) create.Sink(*locals[t], bst.chunks[k]);
+      });
+    }
+    for (auto& th : ths) th.join();
+    for (auto& l : locals) create.Combine(*l);
+    create.Finalize();
+    EXPECT(create.MaterializedRows() == nb, "materialized %llu", (unsigned long long)create.MaterializedRows());
+    EXPECT(create.Resized(0) && create.Resized(1), "under-estimated filters must be resized");
+    const int lnb = rpt_oracle_log_num_blocks(nb);
+    std::vector<uint64_t> w0(1ULL << lnb, 0), w1(1ULL << lnb, 0);
+    {
+      std::vector<uint64_t> va = pack(bt.v0, 0, nb), vb = pack(bt.v1, 0, nb);
+      rpt_oracle_insert_i64(w0.data(), lnb, bt.c0.data(), nullptr, va.data(), nb);
+      rpt_oracle_insert_i32(w1.data(), lnb, bt.c1.data(), nullptr, vb.data(), nb);
+    }
+    auto f0 = create.GetBloomFilter(0), f1 = create.GetBloomFilter(1);
+    EXPECT(f0->LogNumBlocks() == lnb && f0->SizedForRows() == nb, "resized filter sizing");
+    EXPECT(f0->ExportWords() == w0, "filter 0 words differ from the oracle");
+    EXPECT(f1->ExportWords() == w1, "filter 1 words differ from the oracle");
+    EXPECT(f0->finalized_ && f1->finalized_ && !f0->IsEmpty(), "finalized / has data");
+
+    // ---------------- probe -------------------------------------------------------------------
+    const size_t np = 20000;
+    Table pt = make_table(np, 2, 31, 2048);
+    for (size_t i = 0; i < np; i += 3) {  // a third of the probe rows hit the build side
+      pt.c0[i] = bt.c0[(i * 7) % nb];
+      pt.c1[i] = bt.c1[(i * 7) % nb];
+    }
+    ChunkStore pst;
+    make_chunks(pt, np, pst, true);
+    rpt::DeviceContext ctx(dev);
+    rpt::UseBF use({f0, f1}, {0, 1});
+    std::vector<uint32_t> tmp0(np), tmp1(np);
+    size_t base = 0, total = 0;
+    for (const auto& ch : pst.chunks) {
+      rpt::SelectionVector out;
+      use.Execute(ctx, ch, out);
+      // oracle: AND of the two filters over this chunk's rows
+      std::vector<uint64_t> va = pack(pt.v0, base, ch.count), vb = pack(pt.v1, base, ch.count);
+      const uint64_t n0 = rpt_oracle_probe_i64(w0.data(), lnb, pt.c0.data() + base, nullptr, va.data(), ch.count, tmp0.data());
+      const uint64_t n1 = rpt_oracle_probe_i32(w1.data(), lnb, pt.c1.data() + base, nullptr, vb.data(), ch.count, tmp1.data());
+      std::vector<uint32_t> exp;
+      for (uint64_t i = 0, j = 0; i < n0; i++) {
+        while (j < n1 && tmp1[j] < tmp0[i]) j++;
+        if (j < n1 && tmp1[j] == tmp0[i]) exp.push_back(tmp0[i]);
+      }
+      EXPECT(out == exp, "USE_BF chunk at row %zu: %zu survivors, oracle %zu", base, out.size(), exp.size());
+      total += out.size();
+      base += ch.count;
+    }
+    EXPECT(use.rows_in() == np && use.rows_out() == total, "USE_BF counters");
+    // batch lookup == per-chunk lookup
+    {
+      std::vector<const rpt::DataChunk*> ptrs;
+      for (const auto& ch : pst.chunks) ptrs.push_back(&ch);
+      std::vector<rpt::SelectionVector> sels;
+      f0->LookupSelBatch(ctx, ptrs, sels, {0});
+      for (size_t k = 0; k < ptrs.size(); k++) {
+        rpt::SelectionVector one;
+        f0->LookupSel(ctx, *ptrs[k], one, {0});
+        EXPECT(sels[k] == one, "batch lookup differs at chunk %zu", k);
+      }
+    }
+    // ---------------- early exits / skips ---------------------------------------------------
+    {
+      rpt::CreateBF empty(dev, 100, {0});
+      empty.Finalize();
+      auto fe = empty.GetBloomFilter(0);
+      EXPECT(fe->IsEmpty() && fe->finalized_, "empty build");
+      rpt::UseBF u({fe}, {0});
+      rpt::SelectionVector out;
+      EXPECT(u.Execute(ctx, pst.chunks[0], out) == 0 && out.empty(), "empty filter -> no rows");
+      auto nf = std::make_shared<rpt::PTBloomFilter>();
+      nf->Initialize(dev, 10);  // never finalized: skipped, all rows pass
+      rpt::UseBF u2({nf}, {0});
+      EXPECT(u2.Execute(ctx, pst.chunks[0], out) == pst.chunks[0].count, "not-finalized filter is skipped");
+      rpt::UseBF u3({f0}, {0}, /*passthrough=*/true);
+      EXPECT(u3.Execute(ctx, pst.chunks[0], out) == pst.chunks[0].count, "passthrough");
+      bool threw = false;
+      try {
+        rpt::SelectionVector s2;
+        f0->LookupSel(ctx, pst.chunks[0], s2, {0, 1});
+      } catch (const rpt::GpuError& e) {
+        threw = e.status() == RPT_ERR_INVALID_ARGUMENT;
+      }
+      EXPECT(threw, "multi-column keys are rejected with INVALID_ARGUMENT");
+    }
+  } catch (const std::exception& e) {
+    fprintf(stderr, "exception: %s\n", e.what());
+    return 2;
+  }
+  if (g_fail) {
+    fprintf(stderr, "%d check(s) failed\n", g_fail);
+    return 1;
+  }
+  printf("ALL OK\n");
+  return 0;
+}
