@@ -56,6 +56,9 @@ constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per w
 static_assert(kRowsPerThread == 8 || kRowsPerThread == 16, "tile = 8 Ki or 16 Ki rows");
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
 constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
+#ifndef RPT_SLICE_UNROLL
+#define RPT_SLICE_UNROLL 8                             // 256-record groups in flight per wave
+#endif
 #ifndef RPT_PARTITION_MIN_WAVES
 #define RPT_PARTITION_MIN_WAVES 8                      // 2 partition workgroups per CU (64 VGPRs)
 #endif
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
                                                                    const uint32_t* __restrict__ recs,
                                                                    const uint32_t* __restrict__ runs,
                                                                    uint8_t* __restrict__ passb) {
-  constexpr int kUnroll = 4;
+  constexpr int kUnroll = RPT_SLICE_UNROLL;
   __shared__ uint64_t s_slice[kSliceWords];
   __shared__ uint64_t s_masks[kNumMasks];
   const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
@@ -520,6 +523,7 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
                                                                uint32_t* __restrict__ out_sel) {
   __shared__ uint32_t s_off[kGroupSegs];
   __shared__ uint32_t s_wave[kWavesPerBlock];
+  __shared__ uint16_t s_stage[kWavesPerBlock][8 * kSegRows];  // one 4096-row step per wave (row offsets)
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kGroupSegs;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t sidx = g0 + threadIdx.x;
@@ -532,20 +536,31 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
   s_off[threadIdx.x] = off;
   __syncthreads();
   const uint64_t n_words = n_segs * kWordsPerSeg;
+  // Each wave expands 8 segments (64 words = 4096 rows) per step: survivors are first written to the
+  // wave's LDS buffer in row order, then streamed out with coalesced stores.
+  uint16_t* buf = s_stage[wave];
   for (uint32_t b = wave; b < kGroupSegs / 8; b += kWavesPerBlock) {
     const uint64_t seg0 = g0 + b * 8;
     if (seg0 >= n_segs) break;
     const uint64_t wi = seg0 * kWordsPerSeg + lane;
     uint64_t word = wi < n_words ? bits[wi] : 0ULL;
     const uint32_t pc = __popcll(word);
-    uint32_t pos = s_off[b * 8] + wave_inclusive_sum(pc) - pc;
-    const uint64_t row_base = wi * 64;
+    const uint32_t incl = wave_inclusive_sum(pc);
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    uint32_t p = incl - pc;
     while (word) {
-      const uint32_t j = __builtin_ctzll(word);
-      const uint64_t row = row_base + j;
-      out_sel[pos++] = row_sel ? row_sel[row] : static_cast<uint32_t>(row);
+      buf[p++] = static_cast<uint16_t>(lane * 64 + __builtin_ctzll(word));
       word &= word - 1;
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    uint32_t* dst = out_sel + s_off[b * 8];
+    const uint32_t step_row = static_cast<uint32_t>(seg0 * kSegRows);
+    for (uint32_t i = lane; i < total; i += 64) {
+      const uint32_t row = step_row + buf[i];
+      dst[i] = row_sel ? row_sel[row] : row;
+    }
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -827,8 +842,8 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* 
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
   const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
   const uint64_t padded = n_tiles * rpt::kTileRows;
-  size_t sz[9] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
-                  align256(n_groups * 4), align256(n_groups * 4), 0, 0, 0, 0, 0};
+  size_t sz[10] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
+                   align256(n_groups * 4), align256(n_groups * 4), 0, 0, 0, 0, 0, 0};
   if (partitioned) {
     sz[4] = align256(n_tiles * rpt::kTileCap * 4);
     sz[5] = align256(padded * 2);
@@ -836,8 +851,8 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* 
     sz[7] = align256(static_cast<uint64_t>(slice_count(log_num_blocks)) * n_tiles * 4);
     sz[8] = sz[7];
   }
-  size_t off[9], total = 0;
-  for (int i = 0; i < 9; i++) {
+  size_t off[10], total = 0;
+  for (int i = 0; i < 10; i++) {
     off[i] = total;
     total += sz[i];
   }
@@ -1178,21 +1193,24 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
   return RPT_OK;
 }
 
-int rpt_bf_probe_phase2(const uint32_t* row_sel, uint64_t n, uint32_t* out_sel, uint64_t* out_count_dev,
-                        void* workspace, size_t workspace_bytes, rpt_stream_t stream) {
-  if (!out_count_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_count");
+int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, uint32_t* out_sel,
+                        uint64_t* out_count_dev, void* workspace, size_t workspace_bytes, rpt_stream_t stream) {
+  if (!bf || !out_count_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
   if (n >= (1ULL << 32)) return fail(RPT_ERR_INVALID_ARGUMENT, "n=%llu rows exceeds uint32 sel_t", (unsigned long long)n);
+  RPT_ON_DEVICE(bf->device);
   hipStream_t s = as_stream(stream);
   if (n == 0) {  // bloom_filter.cpp:63-65
     RPT_HIP(hipMemsetAsync(out_count_dev, 0, sizeof(uint64_t), s));
     return RPT_OK;
   }
   if (!out_sel) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_sel");
-  const size_t need = workspace_layout(n, 0, false, nullptr, nullptr);
+  const int L = bf->log_num_blocks;
+  const bool part = resolve_strategy(bf->probe_strategy.load(), L) == RPT_PROBE_PARTITIONED;
+  const size_t need = workspace_layout(n, L, part, nullptr, nullptr);
   if (!workspace || workspace_bytes < need)
     return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   ProbeWorkspace ws;
-  workspace_layout(n, 0, false, workspace, &ws);
+  workspace_layout(n, L, part, workspace, &ws);
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
   ProfScope prof8_("group_sum_kernel", s);
@@ -1220,7 +1238,7 @@ int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* ro
   RPT_ON_DEVICE(bf->device);
   int st = rpt_bf_probe_phase1(bf, col, row_sel, n, workspace, workspace_bytes, stream);
   if (st != RPT_OK) return st;
-  return rpt_bf_probe_phase2(row_sel, n, out_sel, out_count_dev, workspace, workspace_bytes, stream);
+  return rpt_bf_probe_phase2(bf, row_sel, n, out_sel, out_count_dev, workspace, workspace_bytes, stream);
 }
 
 int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, rpt_stream_t stream) {

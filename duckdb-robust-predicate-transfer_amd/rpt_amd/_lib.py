@@ -93,7 +93,9 @@ SIGNATURES = {
     "rpt_bf_probe_phase1": (
         c_int, [c_void_p, POINTER(KeyColumn), c_void_p, c_uint64, c_void_p, c_size_t, c_void_p]
     ),
-    "rpt_bf_probe_phase2": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rpt_bf_probe_phase2": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    ),
     "rpt_bf_find_bits": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_hash_keys": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_bf_merge_or": (c_int, [c_void_p, c_void_p, c_void_p]),

@@ -228,8 +228,8 @@ class BloomFilter:
 
     def probe_phase2(self, n: int, out_sel: torch.Tensor, out_count: torch.Tensor, workspace: torch.Tensor, *,
                      row_sel=None, stream=None) -> None:
-        """Count scan + selection-vector expansion (rpt_bf_probe_phase2)."""
-        check(self._lib.rpt_bf_probe_phase2(_ptr(row_sel), n, out_sel.data_ptr(), out_count.data_ptr(),
+        """Selection-vector expansion (rpt_bf_probe_phase2)."""
+        check(self._lib.rpt_bf_probe_phase2(self._h, _ptr(row_sel), n, out_sel.data_ptr(), out_count.data_ptr(),
                                             workspace.data_ptr(), workspace.numel() * workspace.element_size(),
                                             _stream(self.device, stream)))
 

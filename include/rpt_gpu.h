@@ -140,13 +140,14 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
 int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
                  uint32_t* out_sel, uint64_t* out_count_dev, void* workspace, size_t workspace_bytes,
                  rpt_stream_t stream);
-/* rpt_bf_probe in its two stream-ordered phases (same workspace, same stream), for callers that
- * time or overlap them: phase 1 = hash + gather + result bits + per-segment counts (the
- * HBM-streaming kernel); phase 2 = scan of the counts + expansion into out_sel / *out_count_dev. */
+/* rpt_bf_probe in its two stream-ordered phases (same filter, workspace and stream), for callers that
+ * time or overlap them. GATHER / LDS: phase 1 = hash + gather + result bits + per-segment counts,
+ * phase 2 = scan + expansion into out_sel. PARTITIONED: phase 1 = partition rows by filter slice +
+ * probe each slice from LDS + restore row order into the result bits, phase 2 = as above. */
 int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
                         void* workspace, size_t workspace_bytes, rpt_stream_t stream);
-int rpt_bf_probe_phase2(const uint32_t* row_sel, uint64_t n, uint32_t* out_sel, uint64_t* out_count_dev,
-                        void* workspace, size_t workspace_bytes, rpt_stream_t stream);
+int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, uint32_t* out_sel,
+                        uint64_t* out_count_dev, void* workspace, size_t workspace_bytes, rpt_stream_t stream);
 /* Arrow BlockedBloomFilter::Find(…, result_bit_vector) shape: bit i (LSB-first in uint64 words) of
  * out_bits = row i passes. out_bits must hold ceil(n/512)*8 words. */
 int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, uint64_t* out_bits,
