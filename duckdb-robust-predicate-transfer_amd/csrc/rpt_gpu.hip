@@ -1175,9 +1175,12 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
       prof_t.end();
       RPT_LAUNCHED("runs_transpose_kernel");
     }
-    // >= 2 workgroups per CU in total, but never more splits than tiles
+    // exactly one resident round of slice workgroups (LDS decides how many fit per CU), never more
+    // splits than tiles
+    const uint64_t slice_lds = rpt::kSliceWords * 8 + 8ULL * rpt::kNumMasks;
+    const uint64_t per_cu = std::max<uint64_t>(1, (160ULL << 10) / slice_lds);
     const uint32_t splits = static_cast<uint32_t>(std::max<uint64_t>(
-        1, std::min<uint64_t>(n_tiles, ceil_div(static_cast<uint64_t>(cus) * 2, slices))));
+        1, std::min<uint64_t>(n_tiles, (static_cast<uint64_t>(cus) * per_cu) / slices)));
     ProfScope prof6_("slice_probe_kernel", s);
     hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words,
                        splits, n_tiles, ws.recs, ws.runs, ws.passb);
