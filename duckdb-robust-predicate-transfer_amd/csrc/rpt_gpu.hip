@@ -44,12 +44,13 @@ constexpr int kBlocksPerCU = 8;
 #endif
 constexpr int kSliceLog = RPT_SLICE_LOG;               // 2^13 blocks = 64 KiB (or 2^14 = 128 KiB) per slice
 constexpr uint64_t kSliceWords = 1ULL << kSliceLog;
-constexpr int kMaxSliceCount = 256;                    // P <= 256 slices (filters <= 32 MiB at 128 KiB slices)
+constexpr int kMaxSliceCount = 1024;                   // P <= 1024 slices (filters <= 128 MiB at 128 KiB slices)
 #ifndef RPT_TILE_ROWS
 #define RPT_TILE_ROWS 16384
 #endif
 constexpr uint64_t kTileRows = RPT_TILE_ROWS;          // rows per partition tile (8 or 16 per thread)
-constexpr uint64_t kTileCap = kTileRows + 4 * kMaxSliceCount;  // record slots per tile (runs padded to 4)
+// record slots per tile: every slice run is padded to 4 records
+__host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices) { return (kTileRows + 4ULL * n_slices + 15) & ~15ULL; }
 constexpr int kTileThreads = 1024;                     // 16 waves
 constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
 constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave in the partition kernel
@@ -230,24 +231,27 @@ __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_
 // (start << 16 | length) are written tile-major (one coalesced 4*P-byte row); runs_transpose_kernel
 // turns them slice-major for the slice kernel. Two passes over the rows held in registers: count per
 // slice (LDS atomics), scan, then claim positions with an LDS cursor per slice and scatter.
+// Dynamic LDS: tile_cap record slots, then the per-slice count and cursor arrays.
 template <int K, bool DENSE>
 __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(
     KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
     uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm) {
-  __shared__ uint32_t s_rec[kTileCap];
-  __shared__ uint32_t s_cnt[kMaxSliceCount];
-  __shared__ uint32_t s_base[kMaxSliceCount];
-  __shared__ uint32_t s_cur[kMaxSliceCount];
+  extern __shared__ uint32_t s_dyn[];
+  const uint64_t tile_cap = tile_cap_for(slice_mask + 1);
+  uint32_t* s_rec = s_dyn;
+  uint32_t* s_cnt = s_dyn + tile_cap;                  // rows per slice in this tile
+  uint32_t* s_cur = s_dyn + tile_cap + slice_mask + 1;  // run start, then scatter cursor (start + count)
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t n_slices = slice_mask + 1;
   {  // one tile per workgroup (no persistent loop: keeps per-lane invariants out of registers)
     const uint64_t tile = blockIdx.x;
-    if (threadIdx.x < kMaxSliceCount) s_cnt[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads) s_cnt[i] = 0;
     __syncthreads();
     const uint64_t tile_base = tile * kTileRows;
-    // pass 1: hash, stage the record at its row position in LDS, count rows per slice; only the 8-bit
-    // slice ids stay in registers (4 per word).
-    uint32_t sl4[kRowsPerThread / 4] = {};
+    // pass 1: hash, stage the record at its row position in LDS, count rows per slice; only the 16-bit
+    // slice ids stay in registers (2 per word).
+    static_assert(kMaxSliceCount <= 65536, "slice ids are packed as 16 bits");
+    uint32_t sl2[kRowsPerThread / 2] = {};
 #pragma unroll
     for (int sg = 0; sg < kSegsPerWaveA; sg++) {
       const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
@@ -258,24 +262,24 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
       for (int j = 0; j < 8; j++) {
         const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
         s_rec[seg_local + seg_row<K, DENSE>(j, lane)] = static_cast<uint32_t>(hh[j]);
-        sl4[(sg * 8 + j) >> 2] |= sl << (8 * (j & 3));
+        sl2[(sg * 8 + j) >> 1] |= sl << (16 * (j & 1));
         if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
       }
     }
     __syncthreads();
-    if (wave == 0) {  // exclusive scan of <= 256 slice counts, each padded to 4 records: 4 per lane
-      uint32_t c[4], t = 0;
+    if (wave == 0) {  // exclusive scan of the slice counts, each padded to 4 records: kMaxSliceCount/64 per lane
+      constexpr int kPer = kMaxSliceCount / 64;
+      uint32_t c[kPer], t = 0;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t idx = lane * 4 + i;
+      for (int i = 0; i < kPer; i++) {
+        const uint32_t idx = lane * kPer + i;
         c[i] = idx < n_slices ? (s_cnt[idx] + 3u) & ~3u : 0u;
         t += c[i];
       }
       uint32_t off = wave_inclusive_sum(t) - t;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        s_base[lane * 4 + i] = off;
-        s_cur[lane * 4 + i] = off;
+      for (int i = 0; i < kPer; i++) {
+        if (lane * kPer + i < n_slices) s_cur[lane * kPer + i] = off;
         off += c[i];
       }
     }
@@ -297,7 +301,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const int jj = sg * 8 + j;
-        const uint32_t sl = (sl4[jj >> 2] >> (8 * (jj & 3))) & 0xFFu;
+        const uint32_t sl = (sl2[jj >> 1] >> (16 * (jj & 1))) & 0xFFFFu;
         const bool ok = seg_row<K, DENSE>(j, lane) < seg_rem;
         uint32_t p = 0;
         if (ok) {
@@ -327,13 +331,14 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
       }
     }
     __syncthreads();
-    // records of the tile (pad slots hold stale values: probed, never read back)
-    const uint32_t used = s_base[slice_mask] + ((s_cnt[slice_mask] + 3u) & ~3u);
-    u32x4* dst = reinterpret_cast<u32x4*>(recs + tile * kTileCap);
+    // records of the tile (pad slots hold stale values: probed, never read back); the scatter left
+    // s_cur[i] = start_i + count_i
+    const uint32_t used = s_cur[slice_mask] - s_cnt[slice_mask] + ((s_cnt[slice_mask] + 3u) & ~3u);
+    u32x4* dst = reinterpret_cast<u32x4*>(recs + tile * tile_cap);
     const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
     for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
-    if (threadIdx.x < n_slices)
-      runs_tm[tile * n_slices + threadIdx.x] = (s_base[threadIdx.x] << 16) | ((s_cnt[threadIdx.x] + 3u) & ~3u);
+    for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
+      runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i]) << 16) | ((s_cnt[i] + 3u) & ~3u);
     __syncthreads();
   }
 }
@@ -389,10 +394,11 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(slice) * n_tiles;
+  const uint64_t tile_cap = tile_cap_for(gridDim.x / splits);
   for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
     const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
     const uint32_t cnt = info & 0xFFFFu;  // padded run length (multiple of 4)
-    const uint64_t base = (tb + lane) * kTileCap + (info >> 16);
+    const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
     const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
     const uint32_t incl = wave_inclusive_sum(cnt);
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
@@ -441,16 +447,17 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 constexpr int kUnpermuteThreads = 256;
 __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
                                                                      const uint8_t* __restrict__ passb, uint64_t n,
-                                                                     uint64_t n_tiles, uint64_t* __restrict__ out_bits,
+                                                                     uint64_t n_tiles, uint64_t tile_cap,
+                                                                     uint64_t* __restrict__ out_bits,
                                                                      uint32_t* __restrict__ seg_counts) {
-  __shared__ uint8_t s_pass[kTileCap];
+  extern __shared__ uint8_t s_pass[];  // tile_cap bytes
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
   constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / (kUnpermuteThreads / 64);
   for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     {
-      const u32x4* src = reinterpret_cast<const u32x4*>(passb + tile * kTileCap);
-      for (uint32_t i = threadIdx.x; i < kTileCap / 16; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
+      const u32x4* src = reinterpret_cast<const u32x4*>(passb + tile * tile_cap);
+      for (uint32_t i = threadIdx.x; i < tile_cap / 16; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
     }
     __syncthreads();
     for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
@@ -845,9 +852,10 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* 
   size_t sz[10] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
                    align256(n_groups * 4), align256(n_groups * 4), 0, 0, 0, 0, 0, 0};
   if (partitioned) {
-    sz[4] = align256(n_tiles * rpt::kTileCap * 4);
+    const uint64_t cap = rpt::tile_cap_for(slice_count(log_num_blocks));
+    sz[4] = align256(n_tiles * cap * 4);
     sz[5] = align256(padded * 2);
-    sz[6] = align256(n_tiles * rpt::kTileCap);
+    sz[6] = align256(n_tiles * cap);
     sz[7] = align256(static_cast<uint64_t>(slice_count(log_num_blocks)) * n_tiles * 4);
     sz[8] = sz[7];
   }
@@ -908,7 +916,14 @@ void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, con
 template <int K, bool D>
 void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
                         uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs) {
-  hipLaunchKernelGGL((rpt::partition_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n, slice_mask,
+  const uint32_t slices = slice_mask + 1;
+  const size_t lds = rpt::tile_cap_for(slices) * 4 + 2ULL * slices * 4;
+  static std::once_flag once;  // per instantiation; > 64 KiB of dynamic LDS must be opted into
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  hipLaunchKernelGGL((rpt::partition_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, slice_mask,
                      n_tiles, recs, pos, runs);
 }
 
@@ -1188,8 +1203,9 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     RPT_LAUNCHED("slice_probe_kernel");
     const unsigned g_unperm = static_cast<unsigned>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) * 8));
     ProfScope prof7_("unpermute_kernel", s);
-    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(g_unperm), dim3(rpt::kUnpermuteThreads), 0, s, ws.pos, ws.passb, n,
-                       n_tiles, ws.bits, ws.seg_counts);
+    const uint64_t cap = rpt::tile_cap_for(slices);
+    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(g_unperm), dim3(rpt::kUnpermuteThreads), cap, s, ws.pos, ws.passb, n,
+                       n_tiles, cap, ws.bits, ws.seg_counts);
     prof7_.end();
     RPT_LAUNCHED("unpermute_kernel");
   }

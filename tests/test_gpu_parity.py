@@ -134,6 +134,21 @@ def test_partition_tile_edges_vs_oracle(rpt, strategy, dtype, n):
     assert np.array_equal(sel, orc.probe_keys(w, lnb, probe))
 
 
+@pytest.mark.parametrize("strategy", ["gather", "partitioned"])
+@pytest.mark.parametrize("log_nb", [21, 22, 24])
+def test_large_filters_vs_oracle(rpt, strategy, log_nb):
+    """16 MiB .. 128 MiB filters (256 .. 1024 LDS slices; BASELINE C3 uses 2^24 blocks)."""
+    build = orc.synth_build_keys(300000)
+    probe = orc.synth_probe_keys(1_000_003, 300000, 300)
+    bf = with_strategy(rpt.BloomFilter(log_num_blocks=log_nb), strategy)
+    bf.insert(dev(build))
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, build)
+    assert np.array_equal(bf.export_words(), w)
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
+
+
 @pytest.mark.parametrize("strategy", list(STRATEGIES))
 def test_dictionary_validity_rowsel_vs_oracle(rpt, strategy):
     rng = np.random.default_rng(7)
