@@ -310,8 +310,9 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
         }
         pv[j] = static_cast<uint16_t>(p);
       }
-      // pos is padded to whole tiles: rows >= n get don't-care values.
-      if constexpr (DENSE) {
+      // pos is padded to whole tiles: rows >= n get don't-care values. (nullptr: build, no row map)
+      if (pos_out == nullptr) {
+      } else if constexpr (DENSE) {
         constexpr int V = KeyTraits<K>::kVec;
 #pragma unroll
         for (int c = 0; c < 8 / V; c++) {
@@ -338,7 +339,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
     const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
     for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
     for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
-      runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i]) << 16) | ((s_cnt[i] + 3u) & ~3u);
+      runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i]) << 16) | s_cnt[i];  // start | true count
     __syncthreads();
   }
 }
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   const uint64_t tile_cap = tile_cap_for(gridDim.x / splits);
   for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
     const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
-    const uint32_t cnt = info & 0xFFFFu;  // padded run length (multiple of 4)
+    const uint32_t cnt = ((info & 0xFFFFu) + 3u) & ~3u;  // padded run length (multiple of 4)
     const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
     const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
     const uint32_t incl = wave_inclusive_sum(cnt);
@@ -437,6 +438,76 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
         }
       }
     }
+  }
+}
+
+// ---- partitioned build: OR each slice's records into an LDS copy, then merge into the filter ----
+// Same flattened run walk as slice_probe_kernel. The slice starts from zero in LDS (ds_or_b64 per
+// record) and is merged into the filter with coalesced 64-bit device-scope atomic ORs of its non-zero
+// words, so concurrent inserts and several workgroups per slice compose (OR is idempotent).
+__global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* __restrict__ words, uint32_t splits,
+                                                                    uint64_t n_tiles,
+                                                                    const uint32_t* __restrict__ recs,
+                                                                    const uint32_t* __restrict__ runs) {
+  __shared__ uint64_t s_slice[kSliceWords];
+  __shared__ uint64_t s_masks[kNumMasks];
+  const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
+  const uint64_t t_lo = n_tiles * part / splits, t_hi = n_tiles * (part + 1) / splits;
+  for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) s_slice[i] = 0;
+  fill_mask_table(s_masks);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr uint32_t kWaves = kSliceThreads / 64;
+  const uint32_t* my_runs = runs + static_cast<uint64_t>(slice) * n_tiles;
+  const uint64_t tile_cap = tile_cap_for(gridDim.x / splits);
+  for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
+    const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
+    const uint32_t real = info & 0xFFFFu;      // records of the run
+    const uint32_t cnt = (real + 3u) & ~3u;    // padded length (k-space)
+    const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
+    const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
+    const uint32_t incl = wave_inclusive_sum(cnt);
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    uint32_t j = 0;
+    for (uint32_t kf = 0; kf < total; kf += 256) {
+      const uint32_t k = kf + lane * 4;
+      while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
+      const uint32_t kl = (kf + 255 < total) ? kf + 255 : total - 1;
+      uint64_t addr = ~0ULL;
+      uint32_t nreal = 0;  // how many of this lane's 4 slots are real records (pad slots are stale)
+      for (uint32_t jj = j;; jj++) {
+        const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
+        const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
+        const uint32_t rl = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(real), jj));
+        const uint64_t b =
+            static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_lo), jj))) |
+            (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_hi), jj))) << 32);
+        if (k >= inc - c && k < inc) {
+          const uint32_t off = k - (inc - c);
+          addr = b + off;
+          nreal = rl > off ? (rl - off < 4 ? rl - off : 4) : 0;
+        }
+        if (inc > kl) break;
+      }
+      if (addr != ~0ULL) {
+        const u32x4 r = *reinterpret_cast<const u32x4*>(recs + addr);
+#pragma unroll
+        for (uint32_t e = 0; e < 4; e++) {
+          if (e < nreal) {
+            const uint32_t rec = r[e];
+            const uint64_t m = rotl64(s_masks[rec & (kNumMasks - 1)], (rec >> kLogNumMasks) & 63u);
+            atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[(rec >> (kLogNumMasks + 6)) & (kSliceWords - 1)]),
+                     static_cast<unsigned long long>(m));
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
+  for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
+    const uint64_t v = s_slice[i];
+    if (v) __hip_atomic_fetch_or(dst + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -684,6 +755,7 @@ struct rpt_bf {
   std::atomic<int> has_data{0};
   std::atomic<int> finalized{0};
   std::atomic<int> probe_strategy{RPT_PROBE_AUTO};
+  std::atomic<int> insert_strategy{RPT_INSERT_AUTO};
 };
 
 namespace {
@@ -877,6 +949,36 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* 
     ws->runs_tm = partitioned ? reinterpret_cast<uint32_t*>(p + off[8]) : nullptr;
   }
   return total;
+}
+
+// Build workspace (partitioned insert): records | runs (slice-major) | runs (tile-major).
+struct InsertWorkspace {
+  uint32_t* recs;
+  uint32_t* runs;
+  uint32_t* runs_tm;
+};
+
+size_t insert_workspace_layout(uint64_t n, int log_num_blocks, void* base, InsertWorkspace* ws) {
+  const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
+  const uint32_t slices = slice_count(log_num_blocks);
+  const size_t b0 = align256(n_tiles * rpt::tile_cap_for(slices) * 4);
+  const size_t b1 = align256(static_cast<uint64_t>(slices) * n_tiles * 4);
+  if (ws) {
+    char* p = static_cast<char*>(base);
+    ws->recs = reinterpret_cast<uint32_t*>(p);
+    ws->runs = reinterpret_cast<uint32_t*>(p + b0);
+    ws->runs_tm = reinterpret_cast<uint32_t*>(p + b0 + b1);
+  }
+  return b0 + 2 * b1;
+}
+
+constexpr uint64_t kPartitionedInsertMinRows = 1ULL << 20;
+
+int resolve_insert_strategy(int requested, int log_num_blocks, uint64_t n) {
+  const bool part_ok = strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks);
+  if (requested == RPT_INSERT_AUTO)
+    return (part_ok && n >= kPartitionedInsertMinRows) ? RPT_INSERT_PARTITIONED : RPT_INSERT_ATOMIC;
+  return requested;
 }
 
 int check_col(const rpt_key_column* col) {
@@ -1115,6 +1217,62 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
   RPT_DISPATCH_KD(launch_insert_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n, n_segs);
   prof1_.end();
   RPT_LAUNCHED("insert_kernel");
+  return RPT_OK;
+}
+
+size_t rpt_insert_workspace_bytes(uint64_t n_rows, int log_num_blocks) {
+  return strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks) ? insert_workspace_layout(n_rows, log_num_blocks, nullptr, nullptr)
+                                                                    : 0;
+}
+
+int rpt_bf_set_insert_strategy(rpt_bf* bf, int strategy) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  if (strategy < RPT_INSERT_AUTO || strategy > RPT_INSERT_PARTITIONED)
+    return fail(RPT_ERR_INVALID_ARGUMENT, "unknown insert strategy %d", strategy);
+  bf->insert_strategy.store(strategy);
+  return RPT_OK;
+}
+
+int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* workspace, size_t workspace_bytes,
+                     rpt_stream_t stream) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  if (n == 0) return RPT_OK;  // bloom_filter.cpp:72-74
+  const int L = bf->log_num_blocks;
+  const int strategy = resolve_insert_strategy(bf->insert_strategy.load(), L, n);
+  if (strategy == RPT_INSERT_ATOMIC) return rpt_bf_insert(bf, col, n, stream);
+  if (!strategy_supported(RPT_PROBE_PARTITIONED, L))
+    return fail(RPT_ERR_INVALID_ARGUMENT, "partitioned insert unsupported for a 2^%d-block filter", L);
+  int st = check_col(col);
+  if (st != RPT_OK) return st;
+  const size_t need = insert_workspace_layout(n, L, nullptr, nullptr);
+  if (!workspace || workspace_bytes < need)
+    return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
+  RPT_ON_DEVICE(bf->device);
+  bf->has_data.store(1);  // bloom_filter.cpp:75
+  InsertWorkspace ws;
+  insert_workspace_layout(n, L, workspace, &ws);
+  hipStream_t s = as_stream(stream);
+  const uint32_t slices = slice_count(L);
+  const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
+  const int cus = num_cus(bf->device);
+  const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  ProfScope prof_p("partition_kernel", s);
+  RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense_ok(col, nullptr), static_cast<unsigned>(n_tiles), s, a, n,
+                  slices - 1, n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm);
+  prof_p.end();
+  RPT_LAUNCHED("partition_kernel");
+  ProfScope prof_t("runs_transpose_kernel", s);
+  hipLaunchKernelGGL(rpt::runs_transpose_kernel, dim3(static_cast<unsigned>(ceil_div(n_tiles, 64)), ceil_div(slices, 64)),
+                     dim3(rpt::kBlockThreads), 0, s, ws.runs_tm, slices, n_tiles, ws.runs);
+  prof_t.end();
+  RPT_LAUNCHED("runs_transpose_kernel");
+  const uint32_t splits = static_cast<uint32_t>(
+      std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) / slices)));
+  ProfScope prof_i("slice_insert_kernel", s);
+  hipLaunchKernelGGL(rpt::slice_insert_kernel, dim3(slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words, splits,
+                     n_tiles, ws.recs, ws.runs);
+  prof_i.end();
+  RPT_LAUNCHED("slice_insert_kernel");
   return RPT_OK;
 }
 

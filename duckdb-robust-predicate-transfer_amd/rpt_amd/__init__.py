@@ -6,6 +6,9 @@ OR-merge; the C++ host mirror of the DuckDB operators lives in include/rpt_host.
 """
 from ._lib import (  # noqa: F401
     LIB_PATH,
+    RPT_INSERT_ATOMIC,
+    RPT_INSERT_AUTO,
+    RPT_INSERT_PARTITIONED,
     RPT_PROBE_AUTO,
     RPT_PROBE_GATHER,
     RPT_PROBE_LDS,

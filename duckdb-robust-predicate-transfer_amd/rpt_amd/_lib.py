@@ -25,6 +25,10 @@ RPT_PROBE_GATHER = 1
 RPT_PROBE_LDS = 2
 RPT_PROBE_PARTITIONED = 3
 
+RPT_INSERT_AUTO = 0
+RPT_INSERT_ATOMIC = 1
+RPT_INSERT_PARTITIONED = 2
+
 RPT_KEY_I64 = 0
 RPT_KEY_I32 = 1
 RPT_KEY_HASH = 2
@@ -86,6 +90,9 @@ SIGNATURES = {
     "rpt_bf_set_finalized": (c_int, [c_void_p, c_int]),
     "rpt_bf_clear": (c_int, [c_void_p, c_void_p]),
     "rpt_bf_insert": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p]),
+    "rpt_insert_workspace_bytes": (c_size_t, [c_uint64, c_int]),
+    "rpt_bf_insert_ws": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p, c_size_t, c_void_p]),
+    "rpt_bf_set_insert_strategy": (c_int, [c_void_p, c_int]),
     "rpt_bf_probe": (
         c_int,
         [c_void_p, POINTER(KeyColumn), c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],

@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from ._lib import (
+    RPT_INSERT_PARTITIONED,
     RPT_KEY_HASH,
     RPT_KEY_I32,
     RPT_KEY_I64,
@@ -176,10 +177,20 @@ class BloomFilter:
 
     # ---- build -----------------------------------------------------------------------------
     def insert(self, keys: torch.Tensor, *, key_type: Optional[int] = None, key_sel=None, validity=None,
-               n: Optional[int] = None, stream=None) -> None:
+               n: Optional[int] = None, stream=None, strategy: Optional[int] = None) -> None:
+        """PTBloomFilter::Insert. Large batches use the partitioned insert (workspace allocated here)
+        unless strategy=RPT_INSERT_ATOMIC; results are identical."""
         n = keys.numel() if (n is None and key_sel is None) else (key_sel.numel() if n is None else n)
         col = make_column(keys, key_type, key_sel, validity)
-        check(self._lib.rpt_bf_insert(self._h, ctypes.byref(col), n, _stream(self.device, stream)))
+        if strategy is not None:
+            check(self._lib.rpt_bf_set_insert_strategy(self._h, int(strategy)))
+        ws_bytes = int(self._lib.rpt_insert_workspace_bytes(n, self.log_num_blocks))
+        if ws_bytes and (strategy == RPT_INSERT_PARTITIONED or (strategy in (None, 0) and n >= (1 << 20))):
+            ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device)
+            check(self._lib.rpt_bf_insert_ws(self._h, ctypes.byref(col), n, ws.data_ptr(), ws_bytes,
+                                             _stream(self.device, stream)))
+        else:
+            check(self._lib.rpt_bf_insert(self._h, ctypes.byref(col), n, _stream(self.device, stream)))
 
     def reinitialize(self, actual_rows: int) -> None:
         check(self._lib.rpt_bf_reinitialize(self._h, int(actual_rows)))

@@ -57,6 +57,14 @@ typedef enum rpt_probe_strategy {
                                probed from LDS, then row order is restored (filters 64 KiB..16 MiB) */
 } rpt_probe_strategy;
 
+/* How an insert reaches the filter (rpt_bf_set_insert_strategy). All give identical filters. */
+typedef enum rpt_insert_strategy {
+  RPT_INSERT_AUTO = 0,       /* PARTITIONED for >= 2^20 rows when the filter supports it, else ATOMIC */
+  RPT_INSERT_ATOMIC = 1,     /* one device-scope 64-bit atomic OR per key */
+  RPT_INSERT_PARTITIONED = 2 /* rows bucketed by 128 KiB filter slice; each slice ORed in LDS, then
+                                merged with coalesced atomic ORs (filters 128 KiB..128 MiB) */
+} rpt_insert_strategy;
+
 /* A hipStream_t, passed opaquely so this header needs no HIP include. NULL = the null stream. */
 typedef void* rpt_stream_t;
 
@@ -128,6 +136,14 @@ int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
  * insert into one filter concurrently (parallel Sink, physical_create_bf.hpp:43-45). n == 0 is a
  * no-op; otherwise has_data becomes 1. */
 int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_t stream);
+
+/* rpt_bf_insert with a caller workspace, which enables the partitioned insert for large batches
+ * (same result, same thread-safety). workspace: rpt_insert_workspace_bytes(n, log_num_blocks)
+ * bytes of device memory (0 when the filter only supports atomic inserts). */
+size_t rpt_insert_workspace_bytes(uint64_t n_rows, int log_num_blocks);
+int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* workspace, size_t workspace_bytes,
+                     rpt_stream_t stream);
+int rpt_bf_set_insert_strategy(rpt_bf* bf, int strategy);
 
 /* ---- probe ------------------------------------------------------------------------------- */
 /* PTBloomFilter::LookupSel (bloom_filter.cpp:60-68) for a batch of rows: writes the ids of rows

@@ -231,6 +231,26 @@ def test_merge_of_partials_equals_single_build(rpt):
     assert np.array_equal(dst.cpu().numpy().view(np.uint64), ref)
 
 
+@pytest.mark.parametrize("log_nb", [14, 17, 21, 24])
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+def test_partitioned_insert_vs_oracle(rpt, log_nb, dtype):
+    """Partitioned build (slice-local LDS OR + atomic merge) == atomic build == oracle, incl. NULLs,
+    ragged tiles and a second batch into the same filter."""
+    rng = np.random.default_rng(log_nb)
+    keys = rng.integers(-2**40, 2**40, size=3 * 16384 + 77, dtype=np.int64).astype(dtype)
+    valid = rng.random(keys.size) > 0.01
+    vw = gu.validity_words(valid)
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, keys, validity=vw)
+    more = rng.integers(-2**40, 2**40, size=20001, dtype=np.int64).astype(dtype)
+    orc.insert_keys(w, log_nb, more)
+    for strategy in (rpt.RPT_INSERT_PARTITIONED, rpt.RPT_INSERT_ATOMIC):
+        bf = rpt.BloomFilter(log_num_blocks=log_nb)
+        bf.insert(dev(keys), validity=dev(vw), strategy=strategy)
+        bf.insert(dev(more), strategy=strategy)
+        assert np.array_equal(bf.export_words(), w), strategy
+
+
 def test_concurrent_inserts_on_two_streams(rpt):
     keys = orc.synth_build_keys(400000)
     bf = rpt.BloomFilter(keys.size)
