@@ -121,10 +121,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # RPT_BENCH_BACKEND=gloo is a rehearsal mode for boxes with fewer GPUs than ranks: ranks share
+    # devices and the OR-merge collectives run over gloo through host memory. Default: RCCL.
+    backend = os.environ.get("RPT_BENCH_BACKEND", "nccl")
+    dev_index = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     import rpt_amd
     from rpt_amd import _lib as rpt_lib
@@ -136,7 +143,7 @@ def main():
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[local])
+            dist.barrier(device_ids=[dev_index]) if backend == "nccl" else dist.barrier()
 
     # ---- CREATE_BF: sharded build + OR merge (reported, not the headline) -------------------------
     lo, hi = shard_range(n_build, rank, world)
@@ -152,6 +159,22 @@ def main():
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     bf.finalized = True
+    merge_check = None
+    if world > 1:
+        # untimed: the OR-merged filter must be bit-identical to a single-GPU build of all rows
+        ref = rpt_amd.BloomFilter(n_build, device=device)
+        ref.insert(rpt_amd.synth_build_keys(n_build, device=device))
+        a = torch.empty(bf.num_blocks, dtype=torch.int64, device=device)
+        b = torch.empty_like(a)
+        bf.copy_words_to(a)
+        ref.copy_words_to(b)
+        ok = torch.tensor([1 if torch.equal(a, b) else 0], dtype=torch.int64,
+                          device=device if backend == "nccl" else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        merge_check = "bit-identical to a single-GPU build on every rank" if ok.item() else "MISMATCH"
+        del ref, a, b
+        if not ok.item():
+            raise SystemExit("OR-merged filter differs from the single-GPU build")
     bf.probe_strategy = {"auto": 0, "gather": 1, "lds": 2, "partitioned": 3}[args.strategy]
     strategy_name = {1: "gather", 2: "lds", 3: "partitioned"}[bf.probe_strategy]
     del build_keys
@@ -195,7 +218,8 @@ def main():
     p1_ms = statistics.mean(e[0].elapsed_time(e[1]) for e in events)
     probe_ms = statistics.mean(e[0].elapsed_time(e[2]) for e in events)
 
-    t = torch.tensor([elapsed, t1 - t0, t2 - t1], dtype=torch.float64, device=device)
+    t = torch.tensor([elapsed, t1 - t0, t2 - t1], dtype=torch.float64,
+                     device=device if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, insert_s, merge_s = t.tolist()
@@ -231,7 +255,8 @@ def main():
                 "build_rows": n_build,
                 "filter_bytes": bf.num_blocks * 8,
                 "pass_fraction": survivors / n_probe,
-                "parallelism": f"row-range shards over {world} GPU(s), filter replicated (RCCL OR-merge)",
+                "parallelism": f"row-range shards over {world} GPU(s), filter replicated "
+                               f"({'RCCL' if backend == 'nccl' else backend + ' rehearsal'} OR-merge)",
                 "probe_strategy": strategy_name,
                 "job_geomean": "not measured: needs DuckDB v1.4.4 + job.duckdb (SURVEY §8f row 1)",
             },
@@ -260,6 +285,7 @@ def main():
                 "insert_ms": insert_s * 1e3,
                 "insert_keys_per_s": (n_build / world) / insert_s if insert_s > 0 else None,
                 "or_merge_ms": merge_s * 1e3,
+                "merge_check": merge_check,
             },
         }
         if not args.no_cpu_baseline and world == 1:
@@ -267,7 +293,7 @@ def main():
         print(json.dumps(line), flush=True)
 
     if world > 1:
-        dist.barrier(device_ids=[local])
+        barrier()
         dist.destroy_process_group()
 
 

@@ -63,14 +63,23 @@ def or_allreduce_words(full: torch.Tensor, group=None, or_slices: Optional[OrSli
 
 
 def allreduce_or_filter(bf, group=None) -> None:
-    """OR-merge a BloomFilter across all ranks (all ranks must hold the same log_num_blocks)."""
+    """OR-merge a BloomFilter across all ranks (all ranks must hold the same log_num_blocks).
+
+    With RCCL the words stay on the device. A gloo group (CPU collectives; used to rehearse the
+    multi-rank path on a box with fewer GPUs than ranks) stages the words through host memory."""
     world = dist.get_world_size(group)
     nw = bf.num_blocks
     buf = torch.zeros(padded_words(nw, world), dtype=torch.int64, device=bf.device)
     bf.copy_words_to(buf)
-    or_allreduce_words(buf, group)
+    on_device = dist.get_backend(group) != "gloo"
+    if on_device:
+        or_allreduce_words(buf, group)
+    else:
+        host = buf.cpu()
+        or_allreduce_words(host, group, or_slices=cpu_or_slices)
+        buf.copy_(host)
     bf.copy_words_from(buf)
-    flag = torch.tensor([0 if bf.is_empty() else 1], dtype=torch.int64, device=bf.device)
+    flag = torch.tensor([0 if bf.is_empty() else 1], dtype=torch.int64, device=bf.device if on_device else "cpu")
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     bf.set_has_data(bool(flag.item()))
 

@@ -1,7 +1,3 @@
 mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 500 python -m pytest tests -m gpu -q -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
-[ $rc -le 1 ] || exit 1
-for args in "" "--build-rows 1e8"; do
-timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline $args > gpurun_out/bench.log 2>&1 || exit 1
-python3 -c "import json;d=json.loads([l for l in open('gpurun_out/bench.log') if l.startswith('{')][-1]);print('$args', round(d['value']/1e9,1), 'Gkeys/s', 'build', d['build'])"
-done
+RPT_BENCH_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 1 --probe-rows 2e8 > gpurun_out/bench_n2.log 2>&1; echo "n2 rc=$?"; grep '^{' gpurun_out/bench_n2.log | tail -c 1200
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" 2>&1 | tail -2
