@@ -50,7 +50,14 @@ constexpr int kMaxSliceCount = 1024;                   // P <= 1024 slices (filt
 #endif
 constexpr uint64_t kTileRows = RPT_TILE_ROWS;          // rows per partition tile (8 or 16 per thread)
 // record slots per tile: every slice run is padded to 4 records
-__host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices) { return (kTileRows + 4ULL * n_slices + 15) & ~15ULL; }
+// Runs are padded to kRunPad records so a lane owns kRunPad aligned records of one run and its pass
+// results form one byte of bits. Tile capacity is a multiple of 128 so the tile's pass bits are
+// whole 16-byte vectors.
+constexpr uint32_t kRunPad = 8;
+__host__ __device__ constexpr uint32_t pad_run(uint32_t c) { return (c + kRunPad - 1) & ~(kRunPad - 1); }
+__host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices) {
+  return (kTileRows + static_cast<uint64_t>(kRunPad) * n_slices + 127) & ~127ULL;
+}
 constexpr int kTileThreads = 1024;                     // 16 waves
 constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
 constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave in the partition kernel
@@ -273,7 +280,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
 #pragma unroll
       for (int i = 0; i < kPer; i++) {
         const uint32_t idx = lane * kPer + i;
-        c[i] = idx < n_slices ? (s_cnt[idx] + 3u) & ~3u : 0u;
+        c[i] = idx < n_slices ? pad_run(s_cnt[idx]) : 0u;
         t += c[i];
       }
       uint32_t off = wave_inclusive_sum(t) - t;
@@ -334,7 +341,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
     __syncthreads();
     // records of the tile (pad slots hold stale values: probed, never read back); the scatter left
     // s_cur[i] = start_i + count_i
-    const uint32_t used = s_cur[slice_mask] - s_cnt[slice_mask] + ((s_cnt[slice_mask] + 3u) & ~3u);
+    const uint32_t used = s_cur[slice_mask] - s_cnt[slice_mask] + pad_run(s_cnt[slice_mask]);
     u32x4* dst = reinterpret_cast<u32x4*>(recs + tile * tile_cap);
     const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
     for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
@@ -379,7 +386,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
                                                                    uint32_t splits, uint64_t n_tiles,
                                                                    const uint32_t* __restrict__ recs,
                                                                    const uint32_t* __restrict__ runs,
-                                                                   uint8_t* __restrict__ passb) {
+                                                                   uint8_t* __restrict__ passbits) {
   constexpr int kUnroll = RPT_SLICE_UNROLL;
   __shared__ uint64_t s_slice[kSliceWords];
   __shared__ uint64_t s_masks[kNumMasks];
@@ -398,23 +405,24 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   const uint64_t tile_cap = tile_cap_for(gridDim.x / splits);
   for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
     const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
-    const uint32_t cnt = ((info & 0xFFFFu) + 3u) & ~3u;  // padded run length (multiple of 4)
+    const uint32_t cnt = pad_run(info & 0xFFFFu);  // padded run length (multiple of kRunPad)
     const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
     const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
     const uint32_t incl = wave_inclusive_sum(cnt);
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
     uint32_t j = 0;  // uniform: first tile of the batch whose inclusive prefix exceeds the step start
-    for (uint32_t k0 = 0; k0 < total; k0 += 256 * kUnroll) {
+    constexpr uint32_t kStep = 64 * kRunPad;  // records per wave step
+    for (uint32_t k0 = 0; k0 < total; k0 += kStep * kUnroll) {
       uint64_t addr[kUnroll];
-      u32x4 rec[kUnroll];
+      u32x4 rec[kUnroll][2];
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) {
-        const uint32_t kf = k0 + u * 256;
-        const uint32_t k = kf + lane * 4;
+        const uint32_t kf = k0 + u * kStep;
+        const uint32_t k = kf + lane * kRunPad;
         addr[u] = ~0ULL;
         if (kf < total) {
           while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
-          const uint32_t kl = (kf + 255 < total) ? kf + 255 : total - 1;
+          const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
           for (uint32_t jj = j;; jj++) {
             const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
             const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
@@ -425,16 +433,20 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
             if (inc > kl) break;
           }
         }
-        rec[u] = addr[u] != ~0ULL ? *reinterpret_cast<const u32x4*>(recs + addr[u]) : u32x4{0, 0, 0, 0};
+        if (addr[u] != ~0ULL) {
+          rec[u][0] = *reinterpret_cast<const u32x4*>(recs + addr[u]);
+          rec[u][1] = *reinterpret_cast<const u32x4*>(recs + addr[u] + 4);
+        } else {
+          rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
+        }
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) {
         if (addr[u] != ~0ULL) {
-          const uint32_t pv = static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][0])) |
-                              (static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][1])) << 8) |
-                              (static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][2])) << 16) |
-                              (static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][3])) << 24);
-          *reinterpret_cast<uint32_t*>(passb + addr[u]) = pv;
+          uint32_t bits = 0;
+#pragma unroll
+          for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][e >> 2][e & 3])) << e;
+          passbits[addr[u] / kRunPad] = static_cast<uint8_t>(bits);
         }
       }
     }
@@ -463,18 +475,19 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
     const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
     const uint32_t real = info & 0xFFFFu;      // records of the run
-    const uint32_t cnt = (real + 3u) & ~3u;    // padded length (k-space)
+    const uint32_t cnt = pad_run(real);          // padded length (k-space)
     const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
     const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
     const uint32_t incl = wave_inclusive_sum(cnt);
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
     uint32_t j = 0;
-    for (uint32_t kf = 0; kf < total; kf += 256) {
-      const uint32_t k = kf + lane * 4;
+    constexpr uint32_t kStep = 64 * kRunPad;
+    for (uint32_t kf = 0; kf < total; kf += kStep) {
+      const uint32_t k = kf + lane * kRunPad;
       while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
-      const uint32_t kl = (kf + 255 < total) ? kf + 255 : total - 1;
+      const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
       uint64_t addr = ~0ULL;
-      uint32_t nreal = 0;  // how many of this lane's 4 slots are real records (pad slots are stale)
+      uint32_t nreal = 0;  // how many of this lane's kRunPad slots are real records (pad slots are stale)
       for (uint32_t jj = j;; jj++) {
         const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
         const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
@@ -485,16 +498,17 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
         if (k >= inc - c && k < inc) {
           const uint32_t off = k - (inc - c);
           addr = b + off;
-          nreal = rl > off ? (rl - off < 4 ? rl - off : 4) : 0;
+          nreal = rl > off ? (rl - off < kRunPad ? rl - off : kRunPad) : 0;
         }
         if (inc > kl) break;
       }
       if (addr != ~0ULL) {
-        const u32x4 r = *reinterpret_cast<const u32x4*>(recs + addr);
+        const u32x4 r0 = *reinterpret_cast<const u32x4*>(recs + addr);
+        const u32x4 r1 = *reinterpret_cast<const u32x4*>(recs + addr + 4);
 #pragma unroll
-        for (uint32_t e = 0; e < 4; e++) {
+        for (uint32_t e = 0; e < kRunPad; e++) {
           if (e < nreal) {
-            const uint32_t rec = r[e];
+            const uint32_t rec = e < 4 ? r0[e] : r1[e - 4];
             const uint64_t m = rotl64(s_masks[rec & (kNumMasks - 1)], (rec >> kLogNumMasks) & 63u);
             atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[(rec >> (kLogNumMasks + 6)) & (kSliceWords - 1)]),
                      static_cast<unsigned long long>(m));
@@ -517,18 +531,18 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
 // directly the row-ordered result word.
 constexpr int kUnpermuteThreads = 256;
 __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
-                                                                     const uint8_t* __restrict__ passb, uint64_t n,
+                                                                     const uint8_t* __restrict__ passbits, uint64_t n,
                                                                      uint64_t n_tiles, uint64_t tile_cap,
                                                                      uint64_t* __restrict__ out_bits,
                                                                      uint32_t* __restrict__ seg_counts) {
-  extern __shared__ uint8_t s_pass[];  // tile_cap bytes
+  extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
   constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / (kUnpermuteThreads / 64);
   for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
     {
-      const u32x4* src = reinterpret_cast<const u32x4*>(passb + tile * tile_cap);
-      for (uint32_t i = threadIdx.x; i < tile_cap / 16; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
+      const u32x4* src = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / 8));
+      for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
     }
     __syncthreads();
     for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
@@ -542,7 +556,7 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint
       uint32_t cnt = 0;
 #pragma unroll
       for (int c = 0; c < 8; c++) {
-        const uint64_t w = ballot64(base + c * 64 + lane < n && s_pass[pp[c]]);
+        const uint64_t w = ballot64(base + c * 64 + lane < n && ((s_pass[pp[c] >> 3] >> (pp[c] & 7)) & 1));
         cnt += __popcll(w);
         mine = (lane == static_cast<uint32_t>(c)) ? w : mine;
       }
@@ -927,7 +941,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* 
     const uint64_t cap = rpt::tile_cap_for(slice_count(log_num_blocks));
     sz[4] = align256(n_tiles * cap * 4);
     sz[5] = align256(padded * 2);
-    sz[6] = align256(n_tiles * cap);
+    sz[6] = align256(n_tiles * cap / 8);
     sz[7] = align256(static_cast<uint64_t>(slice_count(log_num_blocks)) * n_tiles * 4);
     sz[8] = sz[7];
   }
@@ -1362,7 +1376,7 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     const unsigned g_unperm = static_cast<unsigned>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) * 8));
     ProfScope prof7_("unpermute_kernel", s);
     const uint64_t cap = rpt::tile_cap_for(slices);
-    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(g_unperm), dim3(rpt::kUnpermuteThreads), cap, s, ws.pos, ws.passb, n,
+    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(g_unperm), dim3(rpt::kUnpermuteThreads), cap / 8, s, ws.pos, ws.passb, n,
                        n_tiles, cap, ws.bits, ws.seg_counts);
     prof7_.end();
     RPT_LAUNCHED("unpermute_kernel");
