@@ -19,6 +19,7 @@
 #include <atomic>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -231,9 +232,46 @@ __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_
   }
 }
 
+// ---- slice records -------------------------------------------------------------------------------
+// A record carries the 30 hash bits a filter slice needs, laid out for the slice kernels' 32-bit ALU:
+//   [0..4]   rotation & 31  (v_alignbit reads the low 5 bits of its shift operand: no extract)
+//   [5..15]  index into the 2048-entry rotated-mask table: mask id (h & 1023) | rotation bit 5 << 10
+//   [16..29] block within the slice ([30..31]: slice bits, masked off)
+// Table entry (id, r5) = ROTL64(mask(id), 32 * r5). With r = 32 * r5 + t:
+//   (w & ROTL(mask, r)) == ROTL(mask, r)  <=>  (ROTR(w, t) & entry) == entry
+// and ROTR(w, t) for t < 32 is two v_alignbit_b32 — no 64-bit shifts, no rotation of the mask.
+__device__ __forceinline__ uint32_t slice_record(uint64_t h) {
+  const uint32_t x = static_cast<uint32_t>(h);
+  return ((x >> kLogNumMasks) & 31u) | ((x & (kNumMasks - 1)) << 5) | (x & 0xFFFF8000u);
+}
+constexpr uint32_t kRotMasks = 2 * kNumMasks;
+__device__ __forceinline__ void fill_rot_mask_table(uint64_t* s_rmasks) {
+  for (int i = threadIdx.x; i < static_cast<int>(kRotMasks); i += blockDim.x) {
+    const int id = i & (kNumMasks - 1), w = id >> 6, s = id & 63;
+    const uint64_t lo = kMaskBits[w], hi = kMaskBits[w + 1];
+    const uint64_t m = ((lo >> s) | ((hi << 1) << (63 - s))) & kFullMask;
+    s_rmasks[i] = (i >> kLogNumMasks) ? rotl64(m, 32) : m;
+  }
+}
+__device__ __forceinline__ uint64_t rot_entry(const uint64_t* s_rmasks, uint32_t rec) {
+  return s_rmasks[(rec >> 5) & (kRotMasks - 1)];
+}
+__device__ __forceinline__ uint32_t rec_word(uint32_t rec) { return (rec >> 16) & (kSliceWords - 1); }
+// the filter mask of a record: ROTL(entry, t)
+__device__ __forceinline__ uint64_t rec_mask(const uint64_t* s_rmasks, uint32_t rec) {
+  return rotl64(rot_entry(s_rmasks, rec), rec & 31u);
+}
+__device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_t* s_rmasks, uint32_t rec) {
+  const uint64_t e = rot_entry(s_rmasks, rec);
+  const uint64_t w = s_slice[rec_word(rec)];
+  const uint32_t wl = static_cast<uint32_t>(w), wh = static_cast<uint32_t>(w >> 32);
+  const uint32_t xl = __builtin_amdgcn_alignbit(wh, wl, rec), xh = __builtin_amdgcn_alignbit(wl, wh, rec);
+  return ((~xl & static_cast<uint32_t>(e)) | (~xh & static_cast<uint32_t>(e >> 32))) == 0u;
+}
+
 // ---- partitioned probe, A: bucket a 16 Ki-row tile by filter slice --------------------------------
-// Row r of the tile gets record rec = (uint32)hash (mask id, rotation and block-in-slice bits) stored
-// at position pos(r) of the tile's slice-sorted record array (runs padded to 4 records); pos(r) is
+// Row r of the tile gets record slice_record(hash) stored at position pos(r) of the tile's
+// slice-sorted record array (runs padded to kRunPad records); pos(r) is
 // written per row (u16) so the unpermute step can restore row order. Per tile the padded runs
 // (start << 16 | length) are written tile-major (one coalesced 4*P-byte row); runs_transpose_kernel
 // turns them slice-major for the slice kernel. Two passes over the rows held in registers: count per
@@ -268,7 +306,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
-        s_rec[seg_local + seg_row<K, DENSE>(j, lane)] = static_cast<uint32_t>(hh[j]);
+        s_rec[seg_local + seg_row<K, DENSE>(j, lane)] = slice_record(hh[j]);
         sl2[(sg * 8 + j) >> 1] |= sl << (16 * (j & 1));
         if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
       }
@@ -371,25 +409,23 @@ __global__ __launch_bounds__(kBlockThreads) void runs_transpose_kernel(const uin
 }
 
 // ---- partitioned probe, B: one workgroup per (slice, tile range) probes its records from LDS -------
-__device__ __forceinline__ uint8_t probe_rec(const uint64_t* s_slice, const uint64_t* s_masks, uint32_t rec) {
-  const uint64_t m = rotl64(s_masks[rec & (kNumMasks - 1)], (rec >> kLogNumMasks) & 63u);
-  const uint64_t w = s_slice[(rec >> (kLogNumMasks + 6)) & (kSliceWords - 1)];
-  return (w & m) == m ? 1 : 0;
-}
 
 // The runs of 64 consecutive tiles are walked as ONE flattened record stream per wave: record k of
 // the stream belongs to the tile whose inclusive run-length prefix first exceeds k. Runs are padded
-// to 4 records, so each lane owns 4 consecutive, 16-byte aligned records of one run: one 16-B load
-// and one 4-B store per lane, 256 records per wave step. The (uniform) tile cursor lives in scalar
-// registers; a step visits only the few tiles its 256 records overlap.
+// to kRunPad = 8 records, so each lane owns 8 consecutive, 32-byte aligned records of one run: two
+// 16-B loads and one byte of pass bits per lane, 512 records per wave step. The (uniform) tile cursor
+// lives in scalar registers; a step visits only the few tiles its 512 records overlap. Record offsets
+// are 32-bit relative to the batch's first tile (a uniform base pointer).
 __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64_t* __restrict__ words,
                                                                    uint32_t splits, uint64_t n_tiles,
                                                                    const uint32_t* __restrict__ recs,
                                                                    const uint32_t* __restrict__ runs,
                                                                    uint8_t* __restrict__ passbits) {
   constexpr int kUnroll = RPT_SLICE_UNROLL;
-  __shared__ uint64_t s_slice[kSliceWords];
-  __shared__ uint64_t s_masks[kNumMasks];
+  // one LDS array, table first: the slice's base offset folds into the ds_read immediate
+  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
+  uint64_t* const s_rmasks = s_lds;
+  uint64_t* const s_slice = s_lds + kRotMasks;
   const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
   const uint64_t t_lo = n_tiles * part / splits, t_hi = n_tiles * (part + 1) / splits;
   {
@@ -397,57 +433,55 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
     u64x2* dst = reinterpret_cast<u64x2*>(s_slice);
     for (uint32_t i = threadIdx.x; i < kSliceWords / 2; i += kSliceThreads) dst[i] = src[i];
   }
-  fill_mask_table(s_masks);
+  fill_rot_mask_table(s_rmasks);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(slice) * n_tiles;
-  const uint64_t tile_cap = tile_cap_for(gridDim.x / splits);
+  const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(gridDim.x / splits));
+  uint32_t info_next = (t_lo + wave * 64 + lane < t_hi) ? my_runs[t_lo + wave * 64 + lane] : 0u;
   for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
-    const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
+    const uint32_t info = info_next;  // the next batch's runs are fetched while this one is probed
+    info_next = (tb + kWaves * 64 + lane < t_hi) ? my_runs[tb + kWaves * 64 + lane] : 0u;
     const uint32_t cnt = pad_run(info & 0xFFFFu);  // padded run length (multiple of kRunPad)
-    const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
-    const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
+    const uint32_t start = lane * tile_cap + (info >> 16);
+    const uint32_t* brecs = recs + tb * tile_cap;  // uniform
+    uint8_t* bpass = passbits + tb * (tile_cap / kRunPad);
     const uint32_t incl = wave_inclusive_sum(cnt);
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
     uint32_t j = 0;  // uniform: first tile of the batch whose inclusive prefix exceeds the step start
     constexpr uint32_t kStep = 64 * kRunPad;  // records per wave step
     for (uint32_t k0 = 0; k0 < total; k0 += kStep * kUnroll) {
-      uint64_t addr[kUnroll];
+      uint32_t off[kUnroll];
       u32x4 rec[kUnroll][2];
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) {
         const uint32_t kf = k0 + u * kStep;
         const uint32_t k = kf + lane * kRunPad;
-        addr[u] = ~0ULL;
+        off[u] = ~0u;
         if (kf < total) {
           while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
           const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
           for (uint32_t jj = j;; jj++) {
             const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
             const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
-            const uint64_t b =
-                static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_lo), jj))) |
-                (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_hi), jj))) << 32);
-            if (k >= inc - c && k < inc) addr[u] = b + (k - (inc - c));
+            const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(start), jj));
+            if (k >= inc - c && k < inc) off[u] = b + (k - (inc - c));
             if (inc > kl) break;
           }
         }
-        if (addr[u] != ~0ULL) {
-          rec[u][0] = *reinterpret_cast<const u32x4*>(recs + addr[u]);
-          rec[u][1] = *reinterpret_cast<const u32x4*>(recs + addr[u] + 4);
-        } else {
-          rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
+        rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
+        if (off[u] != ~0u) {
+          rec[u][0] = *reinterpret_cast<const u32x4*>(brecs + off[u]);
+          rec[u][1] = *reinterpret_cast<const u32x4*>(brecs + off[u] + 4);
         }
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) {
-        if (addr[u] != ~0ULL) {
-          uint32_t bits = 0;
+        uint32_t bits = 0;
 #pragma unroll
-          for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_masks, rec[u][e >> 2][e & 3])) << e;
-          passbits[addr[u] / kRunPad] = static_cast<uint8_t>(bits);
-        }
+        for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
+        if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
       }
     }
   }
@@ -461,12 +495,14 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
                                                                     uint64_t n_tiles,
                                                                     const uint32_t* __restrict__ recs,
                                                                     const uint32_t* __restrict__ runs) {
-  __shared__ uint64_t s_slice[kSliceWords];
-  __shared__ uint64_t s_masks[kNumMasks];
+  // one LDS array, table first: the slice's base offset folds into the ds_read immediate
+  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
+  uint64_t* const s_rmasks = s_lds;
+  uint64_t* const s_slice = s_lds + kRotMasks;
   const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
   const uint64_t t_lo = n_tiles * part / splits, t_hi = n_tiles * (part + 1) / splits;
   for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) s_slice[i] = 0;
-  fill_mask_table(s_masks);
+  fill_rot_mask_table(s_rmasks);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
@@ -509,9 +545,8 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
         for (uint32_t e = 0; e < kRunPad; e++) {
           if (e < nreal) {
             const uint32_t rec = e < 4 ? r0[e] : r1[e - 4];
-            const uint64_t m = rotl64(s_masks[rec & (kNumMasks - 1)], (rec >> kLogNumMasks) & 63u);
-            atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[(rec >> (kLogNumMasks + 6)) & (kSliceWords - 1)]),
-                     static_cast<unsigned long long>(m));
+            atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[rec_word(rec)]),
+                     static_cast<unsigned long long>(rec_mask(s_rmasks, rec)));
           }
         }
       }
@@ -526,44 +561,48 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
 }
 
 // ---- partitioned probe, C: restore row order -> result bits + per-segment counts (P1's format) -----
-// One 256-thread workgroup per tile (8 per CU keep several tiles in flight): the tile's pass bytes
-// are staged in LDS, then each wave walks 8 segments with one row per lane per step, so a ballot is
-// directly the row-ordered result word.
+// One 256-thread workgroup per tile: the tile's pass bits (tile_cap / 8 bytes) are staged in LDS while
+// each wave's row positions are already in flight; a lane owns 8 consecutive rows of a segment (one
+// 16-B load of positions) and produces byte `lane` of the segment's 512-bit row-ordered result.
 constexpr int kUnpermuteThreads = 256;
 __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
                                                                      const uint8_t* __restrict__ passbits, uint64_t n,
-                                                                     uint64_t n_tiles, uint64_t tile_cap,
+                                                                     uint64_t tile_cap,
                                                                      uint64_t* __restrict__ out_bits,
                                                                      uint32_t* __restrict__ seg_counts) {
   extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
   constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / (kUnpermuteThreads / 64);
-  for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
-    {
-      const u32x4* src = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / 8));
-      for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
-    }
-    __syncthreads();
-    for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
-      const uint64_t seg = tile * (kTileRows / kSegRows) + wave * kSegsPerWave + sg;
-      if (seg >= n_segs) break;
-      const uint64_t base = seg * kSegRows;
-      uint16_t pp[8];
+  const uint64_t tile = blockIdx.x;
+  const uint64_t seg0 = tile * (kTileRows / kSegRows) + wave * kSegsPerWave;
+  u32x4 pv[kSegsPerWave];  // 8 row positions (u16) per lane per segment
 #pragma unroll
-      for (int c = 0; c < 8; c++) pp[c] = pos[base + c * 64 + lane];
-      uint64_t mine = 0;
-      uint32_t cnt = 0;
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    pv[sg] = u32x4{0, 0, 0, 0};
+    if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos + (seg0 + sg) * kSegRows + lane * 8);
+  }
+  {
+    const u32x4* src = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / 8));
+    for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
+  }
+  __syncthreads();
+  uint8_t* out_bytes = reinterpret_cast<uint8_t*>(out_bits);
 #pragma unroll
-      for (int c = 0; c < 8; c++) {
-        const uint64_t w = ballot64(base + c * 64 + lane < n && ((s_pass[pp[c] >> 3] >> (pp[c] & 7)) & 1));
-        cnt += __popcll(w);
-        mine = (lane == static_cast<uint32_t>(c)) ? w : mine;
-      }
-      if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
-      if (lane == 0) seg_counts[seg] = cnt;
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    const uint64_t seg = seg0 + sg;
+    if (seg >= n_segs) break;
+    uint32_t byte = 0;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+      byte |= ((static_cast<uint32_t>(s_pass[p >> 3]) >> (p & 7)) & 1u) << e;
     }
-    __syncthreads();
+    const uint64_t row0 = seg * kSegRows + lane * 8;  // rows >= n (last segment) carry don't-care positions
+    if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
+    out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);
+    const uint32_t cnt = wave_sum(__popc(byte));
+    if (lane == 0) seg_counts[seg] = cnt;
   }
 }
 
@@ -631,11 +670,19 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
   // Each wave expands 8 segments (64 words = 4096 rows) per step: survivors are first written to the
   // wave's LDS buffer in row order, then streamed out with coalesced stores.
   uint16_t* buf = s_stage[wave];
-  for (uint32_t b = wave; b < kGroupSegs / 8; b += kWavesPerBlock) {
+  constexpr uint32_t kSteps = kGroupSegs / 8 / kWavesPerBlock;
+  uint64_t words[kSteps];  // all of this wave's result words in flight at once
+#pragma unroll
+  for (uint32_t i = 0; i < kSteps; i++) {
+    const uint64_t wi = (g0 + (wave + i * kWavesPerBlock) * 8) * kWordsPerSeg + lane;
+    words[i] = wi < n_words ? bits[wi] : 0ULL;
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kSteps; i++) {
+    const uint32_t b = wave + i * kWavesPerBlock;
     const uint64_t seg0 = g0 + b * 8;
     if (seg0 >= n_segs) break;
-    const uint64_t wi = seg0 * kWordsPerSeg + lane;
-    uint64_t word = wi < n_words ? bits[wi] : 0ULL;
+    uint64_t word = words[i];
     const uint32_t pc = __popcll(word);
     const uint32_t incl = wave_inclusive_sum(pc);
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
@@ -648,9 +695,9 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     uint32_t* dst = out_sel + s_off[b * 8];
     const uint32_t step_row = static_cast<uint32_t>(seg0 * kSegRows);
-    for (uint32_t i = lane; i < total; i += 64) {
-      const uint32_t row = step_row + buf[i];
-      dst[i] = row_sel ? row_sel[row] : row;
+    for (uint32_t q = lane; q < total; q += 64) {
+      const uint32_t row = step_row + buf[q];
+      dst[q] = row_sel ? row_sel[row] : row;
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -1364,7 +1411,7 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     }
     // exactly one resident round of slice workgroups (LDS decides how many fit per CU), never more
     // splits than tiles
-    const uint64_t slice_lds = rpt::kSliceWords * 8 + 8ULL * rpt::kNumMasks;
+    const uint64_t slice_lds = rpt::kSliceWords * 8 + 8ULL * rpt::kRotMasks;
     const uint64_t per_cu = std::max<uint64_t>(1, (160ULL << 10) / slice_lds);
     const uint32_t splits = static_cast<uint32_t>(std::max<uint64_t>(
         1, std::min<uint64_t>(n_tiles, (static_cast<uint64_t>(cus) * per_cu) / slices)));
@@ -1373,11 +1420,10 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
                        splits, n_tiles, ws.recs, ws.runs, ws.passb);
     prof6_.end();
     RPT_LAUNCHED("slice_probe_kernel");
-    const unsigned g_unperm = static_cast<unsigned>(std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) * 8));
     ProfScope prof7_("unpermute_kernel", s);
     const uint64_t cap = rpt::tile_cap_for(slices);
-    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(g_unperm), dim3(rpt::kUnpermuteThreads), cap / 8, s, ws.pos, ws.passb, n,
-                       n_tiles, cap, ws.bits, ws.seg_counts);
+    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8, s,
+                       ws.pos, ws.passb, n, cap, ws.bits, ws.seg_counts);
     prof7_.end();
     RPT_LAUNCHED("unpermute_kernel");
   }
