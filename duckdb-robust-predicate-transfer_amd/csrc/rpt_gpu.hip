@@ -38,7 +38,7 @@ constexpr uint64_t kWordsPerSeg = kSegRows / 64;   // result-bit words per segme
 constexpr uint64_t kGroupSegs = 256;               // segments per scan group (one compaction workgroup)
 constexpr int kBlocksPerCU = 8;
 
-// Partitioned ("routed") probe: the filter is cut into 64 KiB slices that fit in LDS; probe rows are
+// Partitioned ("routed") probe: the filter is cut into 128 KiB slices that fit in LDS; probe rows are
 // bucketed by slice per 16 Ki-row tile so that every filter access is an LDS read.
 #ifndef RPT_SLICE_LOG
 #define RPT_SLICE_LOG 14
@@ -50,7 +50,6 @@ constexpr int kMaxSliceCount = 1024;                   // P <= 1024 slices (filt
 #define RPT_TILE_ROWS 16384
 #endif
 constexpr uint64_t kTileRows = RPT_TILE_ROWS;          // rows per partition tile (8 or 16 per thread)
-// record slots per tile: every slice run is padded to 4 records
 // Runs are padded to kRunPad records so a lane owns kRunPad aligned records of one run and its pass
 // results form one byte of bits. Tile capacity is a multiple of 128 so the tile's pass bits are
 // whole 16-byte vectors.
@@ -62,7 +61,7 @@ __host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices) {
 constexpr int kTileThreads = 1024;                     // 16 waves
 constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
 constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave in the partition kernel
-static_assert(kRowsPerThread == 8 || kRowsPerThread == 16, "tile = 8 Ki or 16 Ki rows");
+static_assert(kRowsPerThread == 8 || kRowsPerThread == 16 || kRowsPerThread == 32, "tile = 8, 16 or 32 Ki rows");
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
 constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
 #ifndef RPT_SLICE_UNROLL
@@ -90,9 +89,11 @@ __device__ __forceinline__ bool valid_at(const uint64_t* validity, uint64_t idx)
 //  DENSE   (flat column, no selections, 16-B aligned): row(c, e) = base + c*64*V + lane*V + e,
 //          one 16-byte load per (c): fully coalesced 1 KiB per wave instruction.
 //  GENERAL (dictionary key_sel and/or row_sel):        row(c) = base + c*64 + lane.
-template <int K, bool DENSE>
+// MM: also fold the valid (non-NULL, in-range) key values into mm[0] = min, mm[1] = max (the build's
+// min/max dynamic filter, physical_create_bf.cpp:82-119, fused into the key read).
+template <int K, bool DENSE, bool MM = false>
 __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uint64_t n, uint32_t lane,
-                                            uint64_t (&h)[8], bool (&ok)[8]) {
+                                            uint64_t (&h)[8], bool (&ok)[8], int64_t* mm = nullptr) {
   using Tr = KeyTraits<K>;
   using T = typename Tr::T;
   // rows left from `base` (uniform), so per-row bounds checks are 32-bit and addresses are
@@ -129,6 +130,12 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
         uint64_t hv = Tr::hash(v[e]);
         if (K != kKeyHash && !((vbits >> e) & 1u)) hv = kNullHash;
         h[c * V + e] = hv;
+        if constexpr (MM && K != kKeyHash) {
+          if (off + e < rem && ((vbits >> e) & 1u)) {
+            mm[0] = min(mm[0], static_cast<int64_t>(v[e]));
+            mm[1] = max(mm[1], static_cast<int64_t>(v[e]));
+          }
+        }
       }
     }
   } else {
@@ -142,8 +149,16 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
         const uint64_t i = base + off;
         const uint64_t r = a.row_sel ? a.row_sel[i] : i;
         const uint64_t k = a.key_sel ? a.key_sel[r] : r;
-        hv = Tr::hash(keys[k]);
-        if (K != kKeyHash && !valid_at(a.validity, k)) hv = kNullHash;
+        const T kv = keys[k];
+        hv = Tr::hash(kv);
+        const bool valid = valid_at(a.validity, k);
+        if (K != kKeyHash && !valid) hv = kNullHash;
+        if constexpr (MM && K != kKeyHash) {
+          if (valid) {
+            mm[0] = min(mm[0], static_cast<int64_t>(kv));
+            mm[1] = max(mm[1], static_cast<int64_t>(kv));
+          }
+        }
       }
       h[c] = hv;
     }
@@ -160,6 +175,34 @@ __device__ __forceinline__ uint32_t seg_row(int j, uint32_t lane) {
     return static_cast<uint32_t>(j * 64) + lane;
   }
 }
+
+// Wave-wide (min, max) of per-lane values, returned wave-uniform (scalar registers).
+__device__ __forceinline__ void wave_minmax(int64_t& mn, int64_t& mx) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    mn = min(mn, static_cast<int64_t>(__shfl_xor(static_cast<long long>(mn), d, 64)));
+    mx = max(mx, static_cast<int64_t>(__shfl_xor(static_cast<long long>(mx), d, 64)));
+  }
+  auto uniform = [](int64_t v) {
+    const uint64_t u = static_cast<uint64_t>(v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u >> 32));
+    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  mn = uniform(mn);
+  mx = uniform(mx);
+}
+// Fold a wave's uniform (min, max) into stats[0..1] (int64, device). A wave whose values cannot lower
+// the min or raise the max — the common case once a few waves have reported — skips the atomics.
+__device__ __forceinline__ void publish_minmax(int64_t mn, int64_t mx, int64_t* stats) {
+  if ((threadIdx.x & 63) == 0) {
+    if (mn < __hip_atomic_load(stats, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      __hip_atomic_fetch_min(stats, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mx > __hip_atomic_load(stats + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      __hip_atomic_fetch_max(stats + 1, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+constexpr int64_t kMinInit = INT64_MAX, kMaxInit = INT64_MIN;  // "no value yet"
 
 // ---- P1: probe -> result bits + per-segment survivor counts ------------------------------------
 // FILTER_IN_LDS: the whole filter (<= 64 KiB) is staged in LDS and every gather is an LDS read.
@@ -277,10 +320,10 @@ __device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_
 // turns them slice-major for the slice kernel. Two passes over the rows held in registers: count per
 // slice (LDS atomics), scan, then claim positions with an LDS cursor per slice and scatter.
 // Dynamic LDS: tile_cap record slots, then the per-slice count and cursor arrays.
-template <int K, bool DENSE>
+template <int K, bool DENSE, bool MM>
 __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(
     KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
-    uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm) {
+    uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm, int64_t* __restrict__ stats) {
   extern __shared__ uint32_t s_dyn[];
   const uint64_t tile_cap = tile_cap_for(slice_mask + 1);
   uint32_t* s_rec = s_dyn;
@@ -297,12 +340,19 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
     // slice ids stay in registers (2 per word).
     static_assert(kMaxSliceCount <= 65536, "slice ids are packed as 16 bits");
     uint32_t sl2[kRowsPerThread / 2] = {};
+    int64_t wmn = kMinInit, wmx = kMaxInit;  // wave-uniform: the key min/max stays out of VGPRs
 #pragma unroll
     for (int sg = 0; sg < kSegsPerWaveA; sg++) {
       const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
       uint64_t hh[8];
       bool oo[8];
-      load_hashes<K, DENSE>(a, tile_base + seg_local, n, lane, hh, oo);
+      int64_t mm[2] = {kMinInit, kMaxInit};
+      load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
+      if constexpr (MM && K != kKeyHash) {
+        wave_minmax(mm[0], mm[1]);
+        wmn = min(wmn, mm[0]);
+        wmx = max(wmx, mm[1]);
+      }
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
@@ -311,6 +361,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
         if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
       }
     }
+    if constexpr (MM && K != kKeyHash) publish_minmax(wmn, wmx, stats);
     __syncthreads();
     if (wave == 0) {  // exclusive scan of the slice counts, each padded to 4 records: kMaxSliceCount/64 per lane
       constexpr int kPer = kMaxSliceCount / 64;
@@ -706,17 +757,20 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
 // ---- k2: insert ----------------------------------------------------------------------------------
 template <int K, bool DENSE>
 __global__ __launch_bounds__(kBlockThreads) void insert_kernel(uint64_t* __restrict__ words, uint64_t block_mask,
-                                                              KeyArgs a, uint64_t n, uint64_t n_segs) {
+                                                              KeyArgs a, uint64_t n, uint64_t n_segs,
+                                                              int64_t* __restrict__ stats) {
+  constexpr bool MM = K != kKeyHash;
   __shared__ uint64_t s_masks[kNumMasks];
   fill_mask_table(s_masks);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  int64_t mm[2] = {kMinInit, kMaxInit};
   for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6); seg < n_segs;
        seg += total_waves) {
     uint64_t h[8];
     bool ok[8];
-    load_hashes<K, DENSE>(a, seg * kSegRows, n, lane, h, ok);
+    load_hashes<K, DENSE, MM>(a, seg * kSegRows, n, lane, h, ok, mm);
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       if (ok[j]) {
@@ -725,10 +779,14 @@ __global__ __launch_bounds__(kBlockThreads) void insert_kernel(uint64_t* __restr
       }
     }
   }
+  if constexpr (MM) {
+    wave_minmax(mm[0], mm[1]);
+    publish_minmax(mm[0], mm[1], stats);
+  }
 }
 
 // ---- hashing only (parity / debugging) ---------------------------------------------------------
-template <int K>
+template <int K, bool COMBINE>
 __global__ __launch_bounds__(kBlockThreads) void hash_kernel(KeyArgs a, uint64_t n, uint64_t* __restrict__ out) {
   using Tr = KeyTraits<K>;
   const typename Tr::T* keys = static_cast<const typename Tr::T*>(a.keys);
@@ -737,7 +795,7 @@ __global__ __launch_bounds__(kBlockThreads) void hash_kernel(KeyArgs a, uint64_t
     const uint64_t k = a.key_sel ? a.key_sel[i] : i;
     uint64_t hv = Tr::hash(keys[k]);
     if (K != kKeyHash && !valid_at(a.validity, k)) hv = kNullHash;
-    out[i] = hv;
+    out[i] = COMBINE ? combine_hash(out[i], hv) : hv;
   }
 }
 
@@ -812,6 +870,7 @@ struct rpt_bf {
   int log_num_blocks = 0;
   uint64_t* words = nullptr;
   uint64_t alloc_words = 0;
+  int64_t* stats = nullptr;  // device {min, max} of the inserted I32/I64 keys (min/max dynamic filter)
   uint64_t sized_for_rows = 0;
   std::atomic<int> has_data{0};
   std::atomic<int> finalized{0};
@@ -1076,24 +1135,34 @@ void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, con
                      (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
 }
 
-template <int K, bool D>
-void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
-                        uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs) {
+template <int K, bool D, bool MM>
+void launch_partition_mm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
+                         uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats) {
   const uint32_t slices = slice_mask + 1;
   const size_t lds = rpt::tile_cap_for(slices) * 4 + 2ULL * slices * 4;
   static std::once_flag once;  // per instantiation; > 64 KiB of dynamic LDS must be opted into
   std::call_once(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   });
-  hipLaunchKernelGGL((rpt::partition_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, slice_mask,
-                     n_tiles, recs, pos, runs);
+  hipLaunchKernelGGL((rpt::partition_kernel<K, D, MM>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, slice_mask,
+                     n_tiles, recs, pos, runs, stats);
+}
+
+// stats == nullptr: probe (no min/max); otherwise the build's key min/max is folded into stats.
+template <int K, bool D>
+void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
+                        uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats) {
+  if (K != rpt::kKeyHash && stats != nullptr)
+    launch_partition_mm<K, D, true>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats);
+  else
+    launch_partition_mm<K, D, false>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, nullptr);
 }
 
 template <int K, bool D>
 void launch_insert_t(unsigned grid, hipStream_t s, rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n, uint64_t n_segs) {
   hipLaunchKernelGGL((rpt::insert_kernel<K, D>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
-                     (1ULL << bf->log_num_blocks) - 1, a, n, n_segs);
+                     (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bf->stats);
 }
 
 #define RPT_DISPATCH_KD(fn, kt, dense, ...)                  \
@@ -1134,6 +1203,53 @@ int alloc_words(rpt_bf* bf, int log_nb) {
   return RPT_OK;
 }
 
+const int64_t kStatsInit[2] = {INT64_MAX, INT64_MIN};
+
+int alloc_stats(rpt_bf* bf) {
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, sizeof kStatsInit);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(RPT_ERR_OUT_OF_MEMORY, "hipMalloc(stats) failed: %s", hipGetErrorString(e));
+  }
+  bf->stats = static_cast<int64_t*>(p);
+  e = hipMemcpy(bf->stats, kStatsInit, sizeof kStatsInit, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return fail(RPT_ERR_HIP, "stats init failed: %s", hipGetErrorString(e));
+  return RPT_OK;
+}
+
+// {min, max} reset on the stream (after the caller's earlier work on it)
+__global__ void stats_reset_kernel(int64_t* stats) {
+  stats[0] = INT64_MAX;
+  stats[1] = INT64_MIN;
+}
+__global__ void stats_merge_kernel(int64_t* dst, const int64_t* src) {
+  if (src[0] < dst[0]) dst[0] = src[0];
+  if (src[1] > dst[1]) dst[1] = src[1];
+}
+
+}  // namespace
+
+namespace {
+template <bool COMBINE>
+int launch_hash(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, rpt_stream_t stream) {
+  if (!out_hashes) return fail(RPT_ERR_INVALID_ARGUMENT, "null out");
+  if (n == 0) return RPT_OK;
+  int st = check_col(col);
+  if (st != RPT_OK) return st;
+  const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 4096));
+  const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  hipStream_t s = as_stream(stream);
+  ProfScope prof_("hash_kernel", s);
+  switch (col->key_type) {
+    case RPT_KEY_I64: hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyI64, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
+    case RPT_KEY_I32: hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyI32, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
+    default: hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyHash, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
+  }
+  prof_.end();
+  RPT_LAUNCHED("hash_kernel");
+  return RPT_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1195,7 +1311,9 @@ int rpt_bf_create_log_blocks(int device, int log_num_blocks, rpt_bf** out) {
   rpt_bf* bf = new rpt_bf();
   bf->device = device;
   int st = alloc_words(bf, log_num_blocks);
+  if (st == RPT_OK) st = alloc_stats(bf);
   if (st != RPT_OK) {
+    if (bf->words) (void)hipFree(bf->words);
     delete bf;
     return st;
   }
@@ -1214,6 +1332,7 @@ int rpt_bf_destroy(rpt_bf* bf) {
   {
     DeviceGuard g(bf->device);
     if (bf->words) (void)hipFree(bf->words);
+    if (bf->stats) (void)hipFree(bf->stats);
   }
   delete bf;
   return RPT_OK;
@@ -1241,6 +1360,7 @@ int rpt_bf_reinitialize(rpt_bf* bf, uint64_t actual_rows) {
   if (st != RPT_OK) return st;
   bf->sized_for_rows = actual_rows;
   bf->has_data.store(0);
+  RPT_HIP(hipMemcpy(bf->stats, kStatsInit, sizeof kStatsInit, hipMemcpyHostToDevice));
   return RPT_OK;
 }
 
@@ -1260,7 +1380,33 @@ int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
   RPT_ON_DEVICE(bf->device);
   RPT_HIP(hipMemsetAsync(bf->words, 0, (1ULL << bf->log_num_blocks) * 8, as_stream(stream)));
+  hipLaunchKernelGGL(stats_reset_kernel, dim3(1), dim3(1), 0, as_stream(stream), bf->stats);
+  RPT_LAUNCHED("stats_reset_kernel");
   bf->has_data.store(0);
+  return RPT_OK;
+}
+
+int rpt_bf_get_minmax(const rpt_bf* bf, int64_t* out_min, int64_t* out_max, int* out_has_value, rpt_stream_t stream) {
+  if (!bf || !out_min || !out_max || !out_has_value) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  RPT_ON_DEVICE(bf->device);
+  int64_t v[2];
+  RPT_HIP(hipMemcpyAsync(v, bf->stats, sizeof v, hipMemcpyDeviceToHost, as_stream(stream)));
+  RPT_HIP(hipStreamSynchronize(as_stream(stream)));
+  *out_has_value = v[0] <= v[1] ? 1 : 0;
+  *out_min = *out_has_value ? v[0] : 0;
+  *out_max = *out_has_value ? v[1] : 0;
+  return RPT_OK;
+}
+
+int rpt_bf_set_minmax(rpt_bf* bf, int64_t min_value, int64_t max_value, int has_value, rpt_stream_t stream) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  if (has_value && min_value > max_value) return fail(RPT_ERR_INVALID_ARGUMENT, "min > max");
+  RPT_ON_DEVICE(bf->device);
+  static thread_local int64_t v[2];  // pageable source: hipMemcpyAsync copies it before returning
+  v[0] = has_value ? min_value : INT64_MAX;
+  v[1] = has_value ? max_value : INT64_MIN;
+  RPT_HIP(hipMemcpyAsync(bf->stats, v, sizeof v, hipMemcpyHostToDevice, as_stream(stream)));
+  RPT_HIP(hipStreamSynchronize(as_stream(stream)));
   return RPT_OK;
 }
 
@@ -1319,7 +1465,7 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
   ProfScope prof_p("partition_kernel", s);
   RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense_ok(col, nullptr), static_cast<unsigned>(n_tiles), s, a, n,
-                  slices - 1, n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm);
+                  slices - 1, n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, bf->stats);
   prof_p.end();
   RPT_LAUNCHED("partition_kernel");
   ProfScope prof_t("runs_transpose_kernel", s);
@@ -1399,7 +1545,7 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     const unsigned g_tiles = static_cast<unsigned>(n_tiles);  // one tile per workgroup
     ProfScope prof5_("partition_kernel", s);
     RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense, g_tiles, s, a, n, slices - 1, n_tiles, ws.recs, ws.pos,
-                    ws.runs_tm);
+                    ws.runs_tm, static_cast<int64_t*>(nullptr));
     prof5_.end();
     RPT_LAUNCHED("partition_kernel");
     {
@@ -1478,25 +1624,13 @@ int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* ro
   return rpt_bf_probe_phase2(bf, row_sel, n, out_sel, out_count_dev, workspace, workspace_bytes, stream);
 }
 
+
+int rpt_hash_combine(const rpt_key_column* col, uint64_t n, uint64_t* inout_hashes, rpt_stream_t stream) {
+  return launch_hash<true>(col, n, inout_hashes, stream);
+}
+
 int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, rpt_stream_t stream) {
-  if (!out_hashes) return fail(RPT_ERR_INVALID_ARGUMENT, "null out");
-  if (n == 0) return RPT_OK;
-  int st = check_col(col);
-  if (st != RPT_OK) return st;
-  int dev = 0;
-  RPT_HIP(hipGetDevice(&dev));
-  const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 4096));
-  const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
-  hipStream_t s = as_stream(stream);
-  ProfScope prof11_("hash_kernel", s);
-  switch (col->key_type) {
-    case RPT_KEY_I64: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyI64>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
-    case RPT_KEY_I32: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyI32>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
-    default: hipLaunchKernelGGL(rpt::hash_kernel<rpt::kKeyHash>, dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
-  }
-  prof11_.end();
-  RPT_LAUNCHED("hash_kernel");
-  return RPT_OK;
+  return launch_hash<false>(col, n, out_hashes, stream);
 }
 
 int rpt_words_or_slices(uint64_t* dst, const uint64_t* srcs, uint32_t k, uint64_t n_words, rpt_stream_t stream) {
@@ -1530,8 +1664,11 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
                 dst->device, src->log_num_blocks, src->device);
   RPT_ON_DEVICE(dst->device);
   int st = rpt_words_or(dst->words, src->words, 1ULL << dst->log_num_blocks, stream);
-  if (st == RPT_OK && src->has_data.load()) dst->has_data.store(1);
-  return st;
+  if (st != RPT_OK) return st;
+  hipLaunchKernelGGL(stats_merge_kernel, dim3(1), dim3(1), 0, as_stream(stream), dst->stats, src->stats);
+  RPT_LAUNCHED("stats_merge_kernel");
+  if (src->has_data.load()) dst->has_data.store(1);
+  return RPT_OK;
 }
 
 int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out) {

@@ -111,10 +111,27 @@ uint64_t total_rows(const std::vector<const DataChunk*>& chunks) {
   return t;
 }
 
-void require_single_column(const std::vector<uint64_t>& cols) {
-  // The hot path always hashes exactly one column (physical_create_bf.cpp:225,403,
-  // physical_use_bf.cpp:163); composite keys (CombineHash) are SURVEY §8f row 4.
-  if (cols.size() != 1) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "exactly one key column per filter is supported");
+// The key column(s) of a filter on the device. One column (the hot path: physical_create_bf.cpp:225,
+// 403, physical_use_bf.cpp:163) is staged as is and hashed inside the insert / probe kernels. Several
+// columns are HashColumns' composite key (bloom_filter.cpp:11-24): Hash(col_0), then CombineHash
+// with each further column, into a device hash column (slot 5) that is inserted / probed as
+// RPT_KEY_HASH.
+rpt_key_column stage_key(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                         const std::vector<uint64_t>& cols, uint64_t total) {
+  if (cols.empty()) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "no key columns");
+  if (cols.size() == 1) return stage(ctx, chunks, cols[0], total);
+  auto* dh = static_cast<uint64_t*>(ctx.dev(5, total * 8));
+  for (size_t j = 0; j < cols.size(); j++) {
+    rpt_key_column kc = stage(ctx, chunks, cols[j], total);
+    check(j == 0 ? rpt_hash_keys(&kc, total, dh, ctx.stream()) : rpt_hash_combine(&kc, total, dh, ctx.stream()));
+    ctx.synchronize();  // the next column reuses the staging slots
+  }
+  rpt_key_column hc;
+  hc.key_type = RPT_KEY_HASH;
+  hc.keys = dh;
+  hc.key_sel = nullptr;
+  hc.validity = nullptr;
+  return hc;
 }
 
 }  // namespace
@@ -188,10 +205,9 @@ void PTBloomFilter::Insert(DeviceContext& ctx, const DataChunk& chunk, const std
 
 void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                                 const std::vector<uint64_t>& cols) {
-  require_single_column(cols);
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:72-74
-  rpt_key_column kc = stage(ctx, chunks, cols[0], total);
+  rpt_key_column kc = stage_key(ctx, chunks, cols, total);
   check(rpt_bf_insert(bf_, &kc, total, ctx.stream()));
   ctx.synchronize();  // the staging buffers are reused by the next call
 }
@@ -206,11 +222,10 @@ uint64_t PTBloomFilter::LookupSel(DeviceContext& ctx, const DataChunk& chunk, Se
 
 void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                                    std::vector<SelectionVector>& sels, const std::vector<uint64_t>& cols) const {
-  require_single_column(cols);
   sels.assign(chunks.size(), SelectionVector());
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:63-65
-  rpt_key_column kc = stage(ctx, chunks, cols[0], total);
+  rpt_key_column kc = stage_key(ctx, chunks, cols, total);
   rpt_bf_info info;
   check(rpt_bf_get_info(bf_, &info));
   const size_t ws_bytes = rpt_probe_workspace_bytes(total, info.log_num_blocks);
@@ -261,6 +276,12 @@ int PTBloomFilter::LogNumBlocks() const {
   rpt_bf_info i;
   check(rpt_bf_get_info(bf_, &i));
   return i.log_num_blocks;
+}
+
+bool PTBloomFilter::MinMax(int64_t& min_value, int64_t& max_value) const {
+  int has = 0;
+  check(rpt_bf_get_minmax(bf_, &min_value, &max_value, &has, nullptr));
+  return has != 0;
 }
 
 std::vector<uint64_t> PTBloomFilter::ExportWords() const {
@@ -333,6 +354,10 @@ void CreateBF::Finalize() {
     }
   }
   for (auto& bf : filters_) bf->finalized_ = true;  // physical_create_bf.cpp:409-413
+}
+
+bool CreateBF::MinMax(size_t build_column, int64_t& min_value, int64_t& max_value) const {
+  return filters_.at(build_column)->MinMax(min_value, max_value);
 }
 
 // ---- UseBF ---------------------------------------------------------------------------------------

@@ -22,6 +22,7 @@ from ._lib import (  # noqa: F401
 from .bloom import (  # noqa: F401
     BloomFilter,
     ProbeWorkspace,
+    hash_columns,
     hash_keys,
     log_num_blocks_for_rows,
     make_column,

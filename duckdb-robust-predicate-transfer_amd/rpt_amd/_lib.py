@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_int, c_int32, c_size_t, c_uint32, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_int, c_int32, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.path.join(PKG_DIR, "build", "librpt_gpu.so")
@@ -93,6 +93,8 @@ SIGNATURES = {
     "rpt_insert_workspace_bytes": (c_size_t, [c_uint64, c_int]),
     "rpt_bf_insert_ws": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p, c_size_t, c_void_p]),
     "rpt_bf_set_insert_strategy": (c_int, [c_void_p, c_int]),
+    "rpt_bf_get_minmax": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int), c_void_p]),
+    "rpt_bf_set_minmax": (c_int, [c_void_p, c_int64, c_int64, c_int, c_void_p]),
     "rpt_bf_probe": (
         c_int,
         [c_void_p, POINTER(KeyColumn), c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
@@ -105,6 +107,7 @@ SIGNATURES = {
     ),
     "rpt_bf_find_bits": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_hash_keys": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
+    "rpt_hash_combine": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_bf_merge_or": (c_int, [c_void_p, c_void_p, c_void_p]),
     "rpt_words_or": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_words_or_slices": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p]),

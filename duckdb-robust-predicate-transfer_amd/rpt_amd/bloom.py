@@ -206,6 +206,19 @@ class BloomFilter:
     def clear(self, stream=None) -> None:
         check(self._lib.rpt_bf_clear(self._h, _stream(self.device, stream)))
 
+    def minmax(self, stream=None) -> Optional[tuple[int, int]]:
+        """(min, max) of the valid I32/I64 keys inserted so far, or None (the CREATE_BF min/max
+        dynamic filter, physical_create_bf.cpp:82-176, computed inside the insert kernels)."""
+        mn, mx, has = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+        check(self._lib.rpt_bf_get_minmax(self._h, ctypes.byref(mn), ctypes.byref(mx), ctypes.byref(has),
+                                          _stream(self.device, stream)))
+        return (mn.value, mx.value) if has.value else None
+
+    def set_minmax(self, value: Optional[tuple[int, int]], stream=None) -> None:
+        mn, mx = value if value is not None else (0, 0)
+        check(self._lib.rpt_bf_set_minmax(self._h, int(mn), int(mx), int(value is not None),
+                                          _stream(self.device, stream)))
+
     # ---- probe -----------------------------------------------------------------------------
     def probe_async(self, keys: torch.Tensor, *, key_type: Optional[int] = None, key_sel=None, validity=None,
                     row_sel: Optional[torch.Tensor] = None, n: Optional[int] = None,
@@ -303,6 +316,27 @@ def hash_keys(keys: torch.Tensor, *, key_type: Optional[int] = None, key_sel=Non
     return out[:n]
 
 
+def hash_columns(columns: Sequence, stream=None) -> torch.Tensor:
+    """HashColumns (reference src/bloom_filter.cpp:11-24) for one or more key columns: Hash(col_0),
+    then CombineHash with col_1, col_2, ... on the device. Each column is a tensor or a dict of
+    make_column kwargs (keys=, key_type=, key_sel=, validity=). Insert / probe the result with
+    key_type=RPT_KEY_HASH."""
+    cols = [c if isinstance(c, dict) else {"keys": c} for c in columns]
+    if not cols:
+        raise RptError(1, "hash_columns needs at least one column")
+    first = cols[0]
+    out = hash_keys(first["keys"], key_type=first.get("key_type"), key_sel=first.get("key_sel"),
+                    validity=first.get("validity"), stream=stream)
+    n = out.numel()
+    for c in cols[1:]:
+        cn = c["key_sel"].numel() if c.get("key_sel") is not None else c["keys"].numel()
+        if cn != n:
+            raise RptError(1, f"composite key columns differ in length ({cn} vs {n})")
+        col = make_column(c["keys"], c.get("key_type"), c.get("key_sel"), c.get("validity"))
+        check(load().rpt_hash_combine(ctypes.byref(col), n, out.data_ptr(), _stream(out.device, stream)))
+    return out
+
+
 def words_or_slices(dst: torch.Tensor, srcs: torch.Tensor, k: int, n_words: int, stream=None) -> None:
     """dst[:n_words] = OR of k consecutive n_words slices of srcs (device tensors, 64-bit)."""
     check(load().rpt_words_or_slices(dst.data_ptr(), srcs.data_ptr(), int(k), int(n_words),
@@ -339,6 +373,7 @@ __all__: Sequence[str] = [
     "make_column",
     "validity_from_mask",
     "hash_keys",
+    "hash_columns",
     "words_or_slices",
     "synth_build_keys",
     "synth_probe_keys",

@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 OrSlices = Callable[[torch.Tensor, torch.Tensor, int, int], None]
+INT64_MAX, INT64_MIN = (1 << 63) - 1, -(1 << 63)
 
 
 def cpu_or_slices(dst: torch.Tensor, srcs: torch.Tensor, k: int, n_words: int) -> None:
@@ -63,7 +64,8 @@ def or_allreduce_words(full: torch.Tensor, group=None, or_slices: Optional[OrSli
 
 
 def allreduce_or_filter(bf, group=None) -> None:
-    """OR-merge a BloomFilter across all ranks (all ranks must hold the same log_num_blocks).
+    """OR-merge a BloomFilter across all ranks (all ranks must hold the same log_num_blocks), and
+    reduce its has_data flag and key min/max (CreateBF Combine, physical_create_bf.cpp:244-275).
 
     With RCCL the words stay on the device. A gloo group (CPU collectives; used to rehearse the
     multi-rank path on a box with fewer GPUs than ranks) stages the words through host memory."""
@@ -79,9 +81,16 @@ def allreduce_or_filter(bf, group=None) -> None:
         or_allreduce_words(host, group, or_slices=cpu_or_slices)
         buf.copy_(host)
     bf.copy_words_from(buf)
-    flag = torch.tensor([0 if bf.is_empty() else 1], dtype=torch.int64, device=bf.device if on_device else "cpu")
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-    bf.set_has_data(bool(flag.item()))
+    # has_data (OR) and the min/max dynamic filter (min / max) in ONE MIN all-reduce: the max and the
+    # flag are sent bit-complemented (~x = -x-1 reverses order without overflow).
+    mm = bf.minmax()
+    mn, mx = mm if mm is not None else (INT64_MAX, INT64_MIN)
+    v = torch.tensor([mn, ~mx, ~int(not bf.is_empty())], dtype=torch.int64,
+                     device=bf.device if on_device else "cpu")
+    dist.all_reduce(v, op=dist.ReduceOp.MIN, group=group)
+    g_mn, g_mx, g_has = int(v[0]), ~int(v[1]), ~int(v[2])
+    bf.set_minmax((g_mn, g_mx) if g_mn <= g_mx else None)
+    bf.set_has_data(bool(g_has))
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:

@@ -145,6 +145,16 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
                      rpt_stream_t stream);
 int rpt_bf_set_insert_strategy(rpt_bf* bf, int strategy);
 
+/* Min/max dynamic filter (PhysicalCreateBF::Sink/Combine, physical_create_bf.cpp:82-176, 229-272;
+ * pushed as >= min / <= max scan filters at :335-345): every insert of an I32/I64 column also folds
+ * the min and max of its valid (non-NULL) key values into the filter, fused into the insert kernels
+ * (HASH columns carry no values and are skipped). I32 values are sign-extended. Reset by
+ * rpt_bf_create / rpt_bf_clear / rpt_bf_reinitialize; rpt_bf_merge_or merges them. get: stream-ordered
+ * read, then synchronizes `stream`; *out_has_value = 0 (and min = max = 0) when no valid key was
+ * inserted. set: overwrite (the multi-GPU merge writes the all-reduced values back). */
+int rpt_bf_get_minmax(const rpt_bf* bf, int64_t* out_min, int64_t* out_max, int* out_has_value, rpt_stream_t stream);
+int rpt_bf_set_minmax(rpt_bf* bf, int64_t min_value, int64_t max_value, int has_value, rpt_stream_t stream);
+
 /* ---- probe ------------------------------------------------------------------------------- */
 /* PTBloomFilter::LookupSel (bloom_filter.cpp:60-68) for a batch of rows: writes the ids of rows
  * whose key may be in the filter to out_sel in ASCENDING order and the survivor count to
@@ -170,6 +180,11 @@ int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, ui
                      rpt_stream_t stream);
 /* Key hashes exactly as the filter sees them (DuckDB HashColumns restatement). */
 int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, rpt_stream_t stream);
+/* HashColumns' CombineHash step for composite keys (bloom_filter.cpp:15-17): inout_hashes[i] =
+ * (inout_hashes[i] * 0xbf58476d1ce4e5b9) ^ Hash(row i of col). rpt_hash_keys(col_0) followed by
+ * rpt_hash_combine(col_j) for j = 1, 2, ... is the composite-key hash; insert / probe it as an
+ * RPT_KEY_HASH column. */
+int rpt_hash_combine(const rpt_key_column* col, uint64_t n, uint64_t* inout_hashes, rpt_stream_t stream);
 
 /* ---- merge / fold / export ----------------------------------------------------------------- */
 /* dst |= src (same log_num_blocks, same device): merging per-thread or per-GPU partial filters

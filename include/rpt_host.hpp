@@ -92,7 +92,8 @@ class PTBloomFilter {
 
   // bloom_filter.cpp:27-32 (est_num_rows is uint32 as in physical_create_bf.cpp:187)
   void Initialize(int device, uint32_t est_num_rows);
-  // bloom_filter.cpp:70-78: thread-safe (device atomic OR); no-op on an empty chunk
+  // bloom_filter.cpp:70-78: thread-safe (device atomic OR); no-op on an empty chunk. Several `cols`
+  // form a composite key (HashColumns' CombineHash, bloom_filter.cpp:15-17), as in LookupSel.
   void Insert(DeviceContext& ctx, const DataChunk& chunk, const std::vector<uint64_t>& cols);
   void InsertBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, const std::vector<uint64_t>& cols);
   // bloom_filter.cpp:60-68: ascending surviving row ids; returns the count
@@ -108,6 +109,8 @@ class PTBloomFilter {
   uint64_t SizedForRows() const;
   bool IsEmpty() const;
   int LogNumBlocks() const;
+  // Min/max of the valid I32/I64 keys inserted (the min/max dynamic filter; false: none yet).
+  bool MinMax(int64_t& min_value, int64_t& max_value) const;
   std::vector<uint64_t> ExportWords() const;
   rpt_bf* native() const { return bf_; }
 
@@ -138,6 +141,9 @@ class CreateBF {
   std::shared_ptr<PTBloomFilter> GetBloomFilter(size_t build_column) const { return filters_.at(build_column); }
   uint64_t MaterializedRows() const { return total_rows_; }
   bool Resized(size_t build_column) const { return resized_.at(build_column); }
+  // CreateBFGlobalSinkState::column_min_max[i] (physical_create_bf.cpp:229-272): min / max of the
+  // valid keys of build column i, computed by the insert kernels; false when no valid key was seen.
+  bool MinMax(size_t build_column, int64_t& min_value, int64_t& max_value) const;
 
  private:
   int device_;

@@ -23,6 +23,8 @@
 //     container): MurmurHash64 finalizer, int32 zero-extended through uint32, NULL -> NULL_HASH.
 //     UNPINNED (no DuckDB here); restated identically in the HIP kernels.
 //   * Resize rule of PhysicalCreateBF::Finalize (physical_create_bf.cpp:386-406).
+//   * Composite-key CombineHash (bloom_filter.cpp:15-17; UNPINNED) and the build's min/max dynamic
+//     filter (TypedUpdateMinMax, physical_create_bf.cpp:86-119) for INTEGER / BIGINT keys.
 //   * CPU baseline: morsel-parallel build/probe in 2048-row vectors, like DuckDB's parallel sink
 //     (physical_create_bf.hpp:43-45) and parallel operator (physical_use_bf.hpp:47-49), with an
 //     atomic fetch_or insert (README.md:32).
@@ -178,6 +180,33 @@ void insert_keys(uint64_t* words, int log_nb, const T* keys, const uint32_t* key
 
 }  // namespace
 
+inline uint64_t combine_hash(uint64_t a, uint64_t b) { return (a * 0xbf58476d1ce4e5b9ULL) ^ b; }
+
+// TypedUpdateMinMax (reference physical_create_bf.cpp:86-119) for INTEGER / BIGINT: min and max of
+// the valid rows (row -> physical index through key_sel, validity by physical index). Returns 0 and
+// leaves out2 untouched when no row is valid.
+template <typename T>
+int minmax(const T* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n, int64_t* out2) {
+  bool has = false;
+  T lo{}, hi{};
+  for (uint64_t r = 0; r < n; r++) {
+    const uint64_t idx = key_sel ? key_sel[r] : r;
+    if (!row_valid(validity, idx)) continue;
+    const T v = keys[idx];
+    if (!has) {
+      lo = hi = v;
+      has = true;
+    } else {
+      if (v < lo) lo = v;
+      if (v > hi) hi = v;
+    }
+  }
+  if (!has) return 0;
+  out2[0] = static_cast<int64_t>(lo);
+  out2[1] = static_cast<int64_t>(hi);
+  return 1;
+}
+
 extern "C" {
 
 // ---- spec pieces --------------------------------------------------------------------------
@@ -213,6 +242,27 @@ void rpt_oracle_hash_i64(const int64_t* keys, const uint32_t* key_sel, const uin
 void rpt_oracle_hash_i32(const int32_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
                          uint64_t* out) {
   for (uint64_t i = 0; i < n; i++) out[i] = key_hash(keys, key_sel, validity, i);
+}
+
+// HashColumns' CombineHash (reference src/bloom_filter.cpp:15-17) for composite keys: DuckDB
+// CombineHashScalar(a, b) = (a * 0xbf58476d1ce4e5b9) ^ b with b = Hash(row of col_j). Restated from
+// DuckDB (vector_hash.cpp; source absent): UNPINNED, like the key hash.
+void rpt_oracle_hash_combine_i64(const int64_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
+                                 uint64_t* inout) {
+  for (uint64_t i = 0; i < n; i++) inout[i] = combine_hash(inout[i], key_hash(keys, key_sel, validity, i));
+}
+void rpt_oracle_hash_combine_i32(const int32_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
+                                 uint64_t* inout) {
+  for (uint64_t i = 0; i < n; i++) inout[i] = combine_hash(inout[i], key_hash(keys, key_sel, validity, i));
+}
+
+int rpt_oracle_minmax_i64(const int64_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
+                          int64_t* out2) {
+  return minmax(keys, key_sel, validity, n, out2);
+}
+int rpt_oracle_minmax_i32(const int32_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
+                          int64_t* out2) {
+  return minmax(keys, key_sel, validity, n, out2);
 }
 
 // ---- filter ops ---------------------------------------------------------------------------

@@ -26,6 +26,10 @@ _SIG = {
     "rpt_oracle_null_hash": (c_uint64, []),
     "rpt_oracle_hash_i64": (None, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_oracle_hash_i32": (None, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_hash_combine_i64": (None, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_hash_combine_i32": (None, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_minmax_i64": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
+    "rpt_oracle_minmax_i32": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_oracle_insert_hashes": (None, [c_void_p, c_int, c_void_p, c_uint64]),
     "rpt_oracle_insert_i64": (None, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64]),
     "rpt_oracle_insert_i32": (None, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint64]),
@@ -88,6 +92,36 @@ def hash_keys(keys: np.ndarray, key_sel=None, validity=None) -> np.ndarray:
     fn = lib().rpt_oracle_hash_i64 if keys.dtype.itemsize == 8 else lib().rpt_oracle_hash_i32
     fn(_p(keys), _p(key_sel), _p(validity), n, _p(out))
     return out
+
+
+def hash_combine(hashes: np.ndarray, keys: np.ndarray, key_sel=None, validity=None) -> np.ndarray:
+    """CombineHash(hashes, Hash(col)) for composite keys (bloom_filter.cpp:15-17); returns a new array."""
+    keys = np.ascontiguousarray(keys)
+    out = np.array(hashes, dtype=np.uint64, copy=True)
+    n = key_sel.size if key_sel is not None else keys.size
+    if out.size != n:
+        raise ValueError("hash / key column length mismatch")
+    fn = lib().rpt_oracle_hash_combine_i64 if keys.dtype.itemsize == 8 else lib().rpt_oracle_hash_combine_i32
+    fn(_p(keys), _p(key_sel), _p(validity), n, _p(out))
+    return out
+
+
+def hash_columns(columns) -> np.ndarray:
+    """HashColumns (bloom_filter.cpp:11-24): columns = [keys | dict(keys=, key_sel=, validity=)]."""
+    cols = [c if isinstance(c, dict) else {"keys": c} for c in columns]
+    h = hash_keys(cols[0]["keys"], cols[0].get("key_sel"), cols[0].get("validity"))
+    for c in cols[1:]:
+        h = hash_combine(h, c["keys"], c.get("key_sel"), c.get("validity"))
+    return h
+
+
+def minmax(keys: np.ndarray, key_sel=None, validity=None):
+    """(min, max) of the valid keys (TypedUpdateMinMax, physical_create_bf.cpp:86-119) or None."""
+    keys = np.ascontiguousarray(keys)
+    n = key_sel.size if key_sel is not None else keys.size
+    out = np.zeros(2, dtype=np.int64)
+    fn = lib().rpt_oracle_minmax_i64 if keys.dtype.itemsize == 8 else lib().rpt_oracle_minmax_i32
+    return (int(out[0]), int(out[1])) if fn(_p(keys), _p(key_sel), _p(validity), n, _p(out)) else None
 
 
 def new_words(log_nb: int) -> np.ndarray:

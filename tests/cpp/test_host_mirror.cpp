@@ -3,7 +3,8 @@
 //
 // CREATE_BF: 4 sink threads, 2048-row chunks (last one ragged), FLAT/CONSTANT/DICTIONARY vectors with
 // NULLs, an under-estimated cardinality so Finalize must ReinitializeAndRehash; then USE_BF with two
-// filters (chain = AND), the empty-build early exit, the not-finalized skip and passthrough.
+// filters (chain = AND), the empty-build early exit, the not-finalized skip and passthrough; the
+// build's min/max dynamic filter; a composite (two-column) key filter.
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -23,6 +24,16 @@ uint64_t rpt_oracle_probe_i64(const uint64_t* words, int log_nb, const int64_t* 
                               const uint64_t* validity, uint64_t n, uint32_t* sel);
 uint64_t rpt_oracle_probe_i32(const uint64_t* words, int log_nb, const int32_t* keys, const uint32_t* key_sel,
                               const uint64_t* validity, uint64_t n, uint32_t* sel);
+void rpt_oracle_hash_i64(const int64_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
+                         uint64_t* out);
+void rpt_oracle_hash_combine_i32(const int32_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
+                                 uint64_t* inout);
+void rpt_oracle_insert_hashes(uint64_t* words, int log_nb, const uint64_t* h, uint64_t n);
+uint64_t rpt_oracle_lookup_sel_hashes(const uint64_t* words, int log_nb, const uint64_t* h, uint64_t n, uint32_t* sel);
+int rpt_oracle_minmax_i64(const int64_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
+                          int64_t* out2);
+int rpt_oracle_minmax_i32(const int32_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
+                          int64_t* out2);
 }
 
 static int g_fail = 0;
@@ -194,6 +205,17 @@ int main() {
     EXPECT(f0->ExportWords() == w0, "filter 0 words differ from the oracle");
     EXPECT(f1->ExportWords() == w1, "filter 1 words differ from the oracle");
     EXPECT(f0->finalized_ && f1->finalized_ && !f0->IsEmpty(), "finalized / has data");
+    // min/max dynamic filter per build column (physical_create_bf.cpp:229-272), NULLs skipped
+    {
+      std::vector<uint64_t> va = pack(bt.v0, 0, nb), vb = pack(bt.v1, 0, nb);
+      int64_t e0[2], e1[2], mn = 0, mx = 0;
+      const int h0 = rpt_oracle_minmax_i64(bt.c0.data(), nullptr, va.data(), nb, e0);
+      const int h1 = rpt_oracle_minmax_i32(bt.c1.data(), nullptr, vb.data(), nb, e1);
+      EXPECT(h0 && create.MinMax(0, mn, mx) && mn == e0[0] && mx == e0[1], "column 0 min/max %lld..%lld vs %lld..%lld",
+             (long long)mn, (long long)mx, (long long)e0[0], (long long)e0[1]);
+      EXPECT(h1 && create.MinMax(1, mn, mx) && mn == e1[0] && mx == e1[1], "column 1 min/max %lld..%lld vs %lld..%lld",
+             (long long)mn, (long long)mx, (long long)e1[0], (long long)e1[1]);
+    }
 
     // ---------------- probe -------------------------------------------------------------------
     const size_t np = 20000;
@@ -255,11 +277,39 @@ int main() {
       bool threw = false;
       try {
         rpt::SelectionVector s2;
-        f0->LookupSel(ctx, pst.chunks[0], s2, {0, 1});
+        f0->LookupSel(ctx, pst.chunks[0], s2, {});
       } catch (const rpt::GpuError& e) {
         threw = e.status() == RPT_ERR_INVALID_ARGUMENT;
       }
-      EXPECT(threw, "multi-column keys are rejected with INVALID_ARGUMENT");
+      EXPECT(threw, "an empty key column list is rejected with INVALID_ARGUMENT");
+    }
+    // ---------------- composite key (HashColumns' CombineHash, bloom_filter.cpp:15-17) --------
+    {
+      rpt::PTBloomFilter fc;
+      fc.Initialize(dev, static_cast<uint32_t>(nb));
+      std::vector<const rpt::DataChunk*> ptrs;
+      for (const auto& ch : bst.chunks) ptrs.push_back(&ch);
+      fc.InsertBatch(ctx, ptrs, {0, 1});
+      const int lc = fc.LogNumBlocks();
+      std::vector<uint64_t> h(nb), wc(1ULL << lc, 0);
+      std::vector<uint64_t> va = pack(bt.v0, 0, nb), vb = pack(bt.v1, 0, nb);
+      rpt_oracle_hash_i64(bt.c0.data(), nullptr, va.data(), nb, h.data());
+      rpt_oracle_hash_combine_i32(bt.c1.data(), nullptr, vb.data(), nb, h.data());
+      rpt_oracle_insert_hashes(wc.data(), lc, h.data(), nb);
+      EXPECT(fc.ExportWords() == wc, "composite-key filter words differ from the oracle");
+      size_t base = 0;
+      std::vector<uint32_t> exp(2048);
+      for (const auto& ch : pst.chunks) {
+        rpt::SelectionVector out;
+        fc.LookupSel(ctx, ch, out, {0, 1});
+        std::vector<uint64_t> ph(ch.count);
+        std::vector<uint64_t> pa = pack(pt.v0, base, ch.count), pb = pack(pt.v1, base, ch.count);
+        rpt_oracle_hash_i64(pt.c0.data() + base, nullptr, pa.data(), ch.count, ph.data());
+        rpt_oracle_hash_combine_i32(pt.c1.data() + base, nullptr, pb.data(), ch.count, ph.data());
+        const uint64_t ne = rpt_oracle_lookup_sel_hashes(wc.data(), lc, ph.data(), ch.count, exp.data());
+        EXPECT(out == std::vector<uint32_t>(exp.begin(), exp.begin() + ne), "composite probe at row %zu", base);
+        base += ch.count;
+      }
     }
   } catch (const std::exception& e) {
     fprintf(stderr, "exception: %s\n", e.what());

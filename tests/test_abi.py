@@ -72,8 +72,8 @@ def test_workspace_size_grows_with_rows():
             b = lib.rpt_probe_workspace_bytes(n, L)
             assert b % 256 == 0 and b >= prev and b >= n // 8
             prev = b
-    # the partitioned strategy (128 KiB..128 MiB filters) needs records + row map + pass bytes
-    assert lib.rpt_probe_workspace_bytes(10**6, 21) >= 7 * 10**6 > lib.rpt_probe_workspace_bytes(10**6, 26)
+    # the partitioned strategy (128 KiB..128 MiB filters) needs records (4 B) + row map (2 B) + pass bits
+    assert lib.rpt_probe_workspace_bytes(10**6, 21) >= 6 * 10**6 > lib.rpt_probe_workspace_bytes(10**6, 26)
     # the partitioned insert needs records + run tables; filters it cannot partition need none
     assert lib.rpt_insert_workspace_bytes(10**6, 21) >= 4 * 10**6
     assert lib.rpt_insert_workspace_bytes(10**6, 10) == 0 and lib.rpt_insert_workspace_bytes(10**6, 26) == 0
