@@ -67,9 +67,12 @@ def pmc_traffic(kernel: str):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    k = d.get("kernels", {}).get(kernel)
-    if not k:
+    # the kernel's instantiations (name or name<template args>); the probe's is the longest-running
+    cands = [v for name, v in d.get("kernels", {}).items()
+             if (name == kernel or name.startswith(kernel + "<")) and "hbm_bytes_per_launch" in v]
+    if not cands:
         return None
+    k = max(cands, key=lambda v: v.get("avg_ms", 0.0))
     return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": f"profiles/pmc_latest.json ({d.get('round')})"}
 
 

@@ -14,8 +14,12 @@ import sys
 
 
 def short(name: str) -> str:
-    m = re.search(r"rpt::(\w+)", name)
-    return m.group(1) if m else name.split("(")[0][:48]
+    """rpt::kernel plus its template arguments (the probe and build instantiations of one kernel
+    differ there), e.g. partition_kernel<0,true,false>."""
+    m = re.search(r"rpt::(\w+)(<[^>]*>)?", name)
+    if not m:
+        return name.split("(")[0][:48]
+    return m.group(1) + (m.group(2).replace(" ", "") if m.group(2) else "")
 
 
 def main(pmc_dir, stats_csv, out_json, tag):
