@@ -38,11 +38,14 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--probe-rows", type=float, default=1e9, help="probe rows per GPU")
     ap.add_argument("--build-rows", type=float, default=1e7, help="global build rows")
+    ap.add_argument("--filter-rows", type=float, default=None,
+                    help="size the filter for this many rows (default: --build-rows). C5 on one GPU = one "
+                         "rank's share: --filter-rows 8e9 --build-rows 1e9")
     ap.add_argument("--p", type=float, default=0.10, help="fraction of probe rows drawn from the build keys")
     ap.add_argument("--cpu-sample", type=float, default=1e8, help="probe rows in the CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--strategy", default="auto", choices=["auto", "gather", "lds", "partitioned"],
+    ap.add_argument("--strategy", default="auto", choices=["auto", "gather", "lds", "partitioned", "bucketed"],
                     help="probe strategy (auto picks by filter size)")
     return ap.parse_args()
 
@@ -53,7 +56,7 @@ def algorithmic_bytes(kernel: str, n: int, survivors: int) -> int:
     counted in `traffic`); the compaction is charged the 4 B/survivor selection vector it writes."""
     if kernel.startswith("compact"):
         return SEL_BYTES * survivors
-    if kernel.startswith(("slice_probe", "unpermute", "group_")):
+    if kernel.startswith(("slice_probe", "unpermute", "group_", "bucket_unpermute", "bucket_scan", "runs_transpose")):
         return 0
     return KEY_BYTES * n
 
@@ -142,7 +145,10 @@ def main():
 
     n_probe = int(args.probe_rows)
     n_build = int(args.build_rows)
+    n_filter = int(args.filter_rows) if args.filter_rows else n_build
     p_permille = int(round(args.p * 1000))
+    cfg = {(10**7, 10**7): "C2", (10**8, 10**8): "C3", (10**9, 8 * 10**9): "C5 (one rank's share)",
+           (8 * 10**9, 8 * 10**9): "C5"}.get((n_build, n_filter), "custom")
 
     def barrier():
         if world > 1:
@@ -151,7 +157,7 @@ def main():
     # ---- CREATE_BF: sharded build + OR merge (reported, not the headline) -------------------------
     lo, hi = shard_range(n_build, rank, world)
     build_keys = rpt_amd.synth_build_keys(hi - lo, start=lo, device=device)
-    bf = rpt_amd.BloomFilter(n_build, device=device)
+    bf = rpt_amd.BloomFilter(n_filter, device=device)
     bf.insert(build_keys)  # warm-up: workspace allocation, code-object load
     build_reps = 5
     torch.cuda.synchronize()
@@ -169,7 +175,7 @@ def main():
     merge_check = None
     if world > 1:
         # untimed: the OR-merged filter must be bit-identical to a single-GPU build of all rows
-        ref = rpt_amd.BloomFilter(n_build, device=device)
+        ref = rpt_amd.BloomFilter(n_filter, device=device)
         ref.insert(rpt_amd.synth_build_keys(n_build, device=device))
         a = torch.empty(bf.num_blocks, dtype=torch.int64, device=device)
         b = torch.empty_like(a)
@@ -182,8 +188,8 @@ def main():
         del ref, a, b
         if not ok.item():
             raise SystemExit("OR-merged filter differs from the single-GPU build")
-    bf.probe_strategy = {"auto": 0, "gather": 1, "lds": 2, "partitioned": 3}[args.strategy]
-    strategy_name = {1: "gather", 2: "lds", 3: "partitioned"}[bf.probe_strategy]
+    bf.probe_strategy = {"auto": 0, "gather": 1, "lds": 2, "partitioned": 3, "bucketed": 4}[args.strategy]
+    strategy_name = {1: "gather", 2: "lds", 3: "partitioned", 4: "bucketed"}[bf.probe_strategy_for(n_probe)]
     del build_keys
 
     # ---- USE_BF probe workload: this rank's slice of the global probe column --------------------
@@ -255,9 +261,9 @@ def main():
             "dtype": "int64",
             "data": "synthetic: seeded splitmix64 int64 key columns generated on device (SURVEY §8d)",
             "config": {
-                "workload": (f"C2: USE_BF probe of {n_probe:.0e} int64 keys per GPU against a blocked Bloom filter "
-                             f"built from {n_build:.0e} keys (2^{bf.log_num_blocks} blocks = "
-                             f"{bf.num_blocks * 8 / 2**20:.0f} MiB), p={args.p}"),
+                "workload": (f"{cfg}: USE_BF probe of {n_probe:.0e} int64 keys per GPU against a blocked Bloom "
+                             f"filter built from {n_build:.0e} keys (sized for {n_filter:.0e}: "
+                             f"2^{bf.log_num_blocks} blocks = {bf.num_blocks * 8 / 2**20:.0f} MiB), p={args.p}"),
                 "probe_rows_per_gpu": n_probe,
                 "build_rows": n_build,
                 "filter_bytes": bf.num_blocks * 8,

@@ -58,6 +58,10 @@ __host__ __device__ constexpr uint32_t pad_run(uint32_t c) { return (c + kRunPad
 __host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices) {
   return (kTileRows + static_cast<uint64_t>(kRunPad) * n_slices + 127) & ~127ULL;
 }
+// Bucketed strategy (filters > 128 MiB): 16 MiB buckets of 128 slices, at most 1024 buckets (16 GiB).
+constexpr int kBucketSliceLog = 7;
+constexpr uint32_t kBucketSlices = 1u << kBucketSliceLog;
+constexpr uint32_t kMaxBuckets = 1024;
 constexpr int kTileThreads = 1024;                     // 16 waves
 constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
 constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave in the partition kernel
@@ -323,7 +327,11 @@ __device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_
 template <int K, bool DENSE, bool MM>
 __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(
     KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
-    uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm, int64_t* __restrict__ stats) {
+    uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm, int64_t* __restrict__ stats,
+    const uint32_t* __restrict__ dev_n_tiles) {
+  // dev_n_tiles (bucketed strategy): the tile count is only known on the device; the grid is an upper
+  // bound and surplus workgroups leave (their run-table rows are never read).
+  if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;
   extern __shared__ uint32_t s_dyn[];
   const uint64_t tile_cap = tile_cap_for(slice_mask + 1);
   uint32_t* s_rec = s_dyn;
@@ -467,18 +475,42 @@ __global__ __launch_bounds__(kBlockThreads) void runs_transpose_kernel(const uin
 // 16-B loads and one byte of pass bits per lane, 512 records per wave step. The (uniform) tile cursor
 // lives in scalar registers; a step visits only the few tiles its 512 records overlap. Record offsets
 // are 32-bit relative to the batch's first tile (a uniform base pointer).
+// Which tiles and run-table row a slice workgroup walks. Plain partitioned: all n_tiles tiles, run row
+// = slice. Bucketed (bucket_tiles != nullptr): global slice g = bucket * kBucketSlices + local slice;
+// the bucket's tiles are [bucket_tiles[b], bucket_tiles[b+1]) and the run row is the local slice.
+struct SliceWork {
+  uint32_t slice, run_row;
+  uint64_t t_lo, t_hi;
+};
+__device__ __forceinline__ SliceWork slice_work(uint32_t splits, uint64_t n_tiles, const uint32_t* bucket_tiles) {
+  const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
+  uint64_t lo = 0, cnt = n_tiles;
+  uint32_t row = slice;
+  if (bucket_tiles != nullptr) {
+    const uint32_t b = slice >> kBucketSliceLog;
+    lo = bucket_tiles[b];
+    cnt = bucket_tiles[b + 1] - lo;
+    row = slice & (kBucketSlices - 1);
+  }
+  return SliceWork{slice, row, lo + cnt * part / splits, lo + cnt * (part + 1) / splits};
+}
+
 __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64_t* __restrict__ words,
                                                                    uint32_t splits, uint64_t n_tiles,
                                                                    const uint32_t* __restrict__ recs,
                                                                    const uint32_t* __restrict__ runs,
-                                                                   uint8_t* __restrict__ passbits) {
+                                                                   uint8_t* __restrict__ passbits,
+                                                                   uint32_t tile_slices,
+                                                                   const uint32_t* __restrict__ bucket_tiles) {
   constexpr int kUnroll = RPT_SLICE_UNROLL;
   // one LDS array, table first: the slice's base offset folds into the ds_read immediate
   __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
   uint64_t* const s_rmasks = s_lds;
   uint64_t* const s_slice = s_lds + kRotMasks;
-  const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
-  const uint64_t t_lo = n_tiles * part / splits, t_hi = n_tiles * (part + 1) / splits;
+  const SliceWork sw = slice_work(splits, n_tiles, bucket_tiles);
+  const uint32_t slice = sw.slice;
+  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
+  if (t_lo >= t_hi) return;  // no rows reach this slice: skip its LDS fill (uniform)
   {
     const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(slice) * kSliceWords);
     u64x2* dst = reinterpret_cast<u64x2*>(s_slice);
@@ -488,8 +520,8 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
-  const uint32_t* my_runs = runs + static_cast<uint64_t>(slice) * n_tiles;
-  const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(gridDim.x / splits));
+  const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
+  const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(tile_slices));
   uint32_t info_next = (t_lo + wave * 64 + lane < t_hi) ? my_runs[t_lo + wave * 64 + lane] : 0u;
   for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
     const uint32_t info = info_next;  // the next batch's runs are fetched while this one is probed
@@ -545,20 +577,24 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* __restrict__ words, uint32_t splits,
                                                                     uint64_t n_tiles,
                                                                     const uint32_t* __restrict__ recs,
-                                                                    const uint32_t* __restrict__ runs) {
+                                                                    const uint32_t* __restrict__ runs,
+                                                                    uint32_t tile_slices,
+                                                                    const uint32_t* __restrict__ bucket_tiles) {
   // one LDS array, table first: the slice's base offset folds into the ds_read immediate
   __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
   uint64_t* const s_rmasks = s_lds;
   uint64_t* const s_slice = s_lds + kRotMasks;
-  const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
-  const uint64_t t_lo = n_tiles * part / splits, t_hi = n_tiles * (part + 1) / splits;
+  const SliceWork sw = slice_work(splits, n_tiles, bucket_tiles);
+  const uint32_t slice = sw.slice;
+  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
+  if (t_lo >= t_hi) return;  // no rows reach this slice (uniform)
   for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) s_slice[i] = 0;
   fill_rot_mask_table(s_rmasks);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
-  const uint32_t* my_runs = runs + static_cast<uint64_t>(slice) * n_tiles;
-  const uint64_t tile_cap = tile_cap_for(gridDim.x / splits);
+  const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
+  const uint64_t tile_cap = tile_cap_for(tile_slices);
   for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
     const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
     const uint32_t real = info & 0xFFFFu;      // records of the run
@@ -620,7 +656,9 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint
                                                                      const uint8_t* __restrict__ passbits, uint64_t n,
                                                                      uint64_t tile_cap,
                                                                      uint64_t* __restrict__ out_bits,
-                                                                     uint32_t* __restrict__ seg_counts) {
+                                                                     uint32_t* __restrict__ seg_counts,
+                                                                     const uint32_t* __restrict__ dev_n_tiles) {
+  if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;  // bucketed: grid is an upper bound
   extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
@@ -650,6 +688,289 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint
       byte |= ((static_cast<uint32_t>(s_pass[p >> 3]) >> (p & 7)) & 1u) << e;
     }
     const uint64_t row0 = seg * kSegRows + lane * 8;  // rows >= n (last segment) carry don't-care positions
+    if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
+    out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);
+    if (seg_counts != nullptr) {
+      const uint32_t cnt = wave_sum(__popc(byte));
+      if (lane == 0) seg_counts[seg] = cnt;
+    }
+  }
+}
+
+// ---- bucketed strategy (filters of 2^22..2^31 blocks) ----------------------------------------------
+// Level 1 cuts the rows by 16 MiB filter region ("bucket": 128 slices) into one contiguous hash array
+// per bucket, each padded to whole 16 Ki-row tiles; level 2 is the partitioned pipeline above over
+// those arrays, every bucket against its own 128 slices. bucket = block id >> 21 = hash bits 37...
+__device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t bucket_mask) {
+  return static_cast<uint32_t>(h >> (kLogNumMasks + 6 + kSliceLog + kBucketSliceLog)) & bucket_mask;
+}
+
+// B1: rows per bucket of every 16 Ki-row level-1 tile -> counts_tm[tile][bucket] (+ the build's min/max).
+template <int K, bool DENSE, bool MM>
+__global__ __launch_bounds__(kTileThreads) void bucket_count_kernel(KeyArgs a, uint64_t n, uint32_t bucket_mask,
+                                                                    uint32_t* __restrict__ counts_tm,
+                                                                    int64_t* __restrict__ stats) {
+  __shared__ uint32_t s_cnt[kMaxBuckets];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t nb = bucket_mask + 1;
+  for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_cnt[i] = 0;
+  __syncthreads();
+  const uint64_t tile = blockIdx.x, tile_base = tile * kTileRows;
+  int64_t wmn = kMinInit, wmx = kMaxInit;
+#pragma unroll
+  for (int sg = 0; sg < kSegsPerWaveA; sg++) {
+    const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+    uint64_t hh[8];
+    bool oo[8];
+    int64_t mm[2] = {kMinInit, kMaxInit};
+    load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
+    if constexpr (MM && K != kKeyHash) {
+      wave_minmax(mm[0], mm[1]);
+      wmn = min(wmn, mm[0]);
+      wmx = max(wmx, mm[1]);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if (oo[j]) atomicAdd(&s_cnt[bucket_of(hh[j], bucket_mask)], 1u);
+  }
+  if constexpr (MM && K != kKeyHash) publish_minmax(wmn, wmx, stats);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) counts_tm[tile * nb + i] = s_cnt[i];
+}
+
+// B2: in place, each bucket's row of counts_bm[bucket][tile] becomes its exclusive prefix over tiles
+// (where the tile's run starts inside the bucket's array); totals[bucket] = the bucket's rows.
+__global__ __launch_bounds__(1024) void bucket_scan_kernel(uint32_t* __restrict__ counts_bm, uint64_t n_tiles,
+                                                          uint32_t* __restrict__ totals) {
+  __shared__ uint32_t s_wave[16];
+  uint32_t* row = counts_bm + static_cast<uint64_t>(blockIdx.x) * n_tiles;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (uint64_t c0 = 0; c0 < n_tiles; c0 += 1024) {
+    const uint64_t i = c0 + threadIdx.x;
+    const uint32_t v = i < n_tiles ? row[i] : 0u;
+    const uint32_t incl = wave_inclusive_sum(v);
+    if (lane == 63) s_wave[wave] = incl;
+    __syncthreads();
+    uint32_t off = carry, chunk = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+      const uint32_t t = s_wave[w];
+      off += w < wave ? t : 0u;
+      chunk += t;
+    }
+    if (i < n_tiles) row[i] = off + incl - v;
+    carry += chunk;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+// B3: bucket bases in the level-2 array (each bucket padded to whole tiles) and its tile ranges:
+// base[b] (rows), bucket_tiles[b] = base[b] / kTileRows; base[nb], bucket_tiles[nb] = the totals.
+__global__ __launch_bounds__(1024) void bucket_base_kernel(const uint32_t* __restrict__ totals, uint32_t nb,
+                                                          uint64_t* __restrict__ base,
+                                                          uint32_t* __restrict__ bucket_tiles) {
+  __shared__ uint32_t s_wave[16];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t b = threadIdx.x;
+  const uint32_t tiles = b < nb ? static_cast<uint32_t>((totals[b] + kTileRows - 1) / kTileRows) : 0u;
+  const uint32_t incl = wave_inclusive_sum(tiles);
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  uint32_t off = 0, all = 0;
+  for (uint32_t w = 0; w < 16; w++) {
+    off += w < wave ? s_wave[w] : 0u;
+    all += s_wave[w];
+  }
+  const uint32_t first = off + incl - tiles;
+  if (b < nb) {
+    bucket_tiles[b] = first;
+    base[b] = static_cast<uint64_t>(first) * kTileRows;
+  }
+  if (b == 0) {
+    bucket_tiles[nb] = all;
+    base[nb] = static_cast<uint64_t>(all) * kTileRows;
+  }
+}
+
+// B4: hash every row of a level-1 tile again, sort the tile's hashes by bucket in LDS and copy each
+// bucket's run to its place in that bucket's array: hashes[base[b] + pre_tm[tile][b] + i]. pos_out (u16,
+// probe only) records each row's position in the tile's bucket-sorted order.
+template <int K, bool DENSE>
+__global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a, uint64_t n, uint32_t bucket_mask,
+                                                                      const uint32_t* __restrict__ counts_tm,
+                                                                      const uint32_t* __restrict__ pre_tm,
+                                                                      const uint64_t* __restrict__ base,
+                                                                      uint64_t* __restrict__ hashes,
+                                                                      uint16_t* __restrict__ pos_out) {
+  extern __shared__ uint64_t s_h[];  // kTileRows hashes, bucket-sorted
+  __shared__ uint32_t s_start[kMaxBuckets], s_cur[kMaxBuckets];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t nb = bucket_mask + 1;
+  const uint64_t tile = blockIdx.x, tile_base = tile * kTileRows;
+  const uint32_t* cnt = counts_tm + tile * nb;
+  if (wave == 0) {  // exclusive scan of this tile's bucket counts, kMaxBuckets / 64 per lane
+    constexpr int kPer = kMaxBuckets / 64;
+    uint32_t c[kPer], t = 0;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+      const uint32_t idx = lane * kPer + i;
+      c[i] = idx < nb ? cnt[idx] : 0u;
+      t += c[i];
+    }
+    uint32_t off = wave_inclusive_sum(t) - t;
+#pragma unroll
+    for (int i = 0; i < kPer; i++) {
+      const uint32_t idx = lane * kPer + i;
+      if (idx < nb) s_start[idx] = s_cur[idx] = off;
+      off += c[i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int sg = 0; sg < kSegsPerWaveA; sg++) {
+    const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+    const uint64_t sbase = tile_base + seg_local;
+    uint64_t hh[8];
+    bool oo[8];
+    load_hashes<K, DENSE>(a, sbase, n, lane, hh, oo);
+    uint16_t pv[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      uint32_t p = 0;
+      if (oo[j]) {
+        p = atomicAdd(&s_cur[bucket_of(hh[j], bucket_mask)], 1u);
+        s_h[p] = hh[j];
+      }
+      pv[j] = static_cast<uint16_t>(p);
+    }
+    if (pos_out != nullptr) {  // padded to whole tiles: rows >= n get don't-care values
+#pragma unroll
+      for (int j = 0; j < 8; j++) pos_out[sbase + seg_row<K, DENSE>(j, lane)] = pv[j];
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {
+    const uint32_t c = cnt[b];
+    if (c == 0) continue;
+    uint64_t* dst = hashes + base[b] + pre_tm[tile * nb + b];
+    const uint64_t* src = s_h + s_start[b];
+    for (uint32_t i = lane; i < c; i += 64) dst[i] = src[i];
+  }
+}
+
+// B5: pad each bucket's array to whole tiles with copies of its first hash (re-inserting or re-probing
+// a present hash changes nothing, and the pads' results are never read).
+__global__ __launch_bounds__(kBlockThreads) void bucket_pad_kernel(const uint32_t* __restrict__ totals,
+                                                                  const uint64_t* __restrict__ base,
+                                                                  uint64_t* __restrict__ hashes) {
+  const uint32_t b = blockIdx.x;
+  const uint64_t t = totals[b], b0 = base[b], end = base[b + 1];
+  if (t == 0) return;
+  const uint64_t v = hashes[b0];
+  for (uint64_t i = b0 + t + threadIdx.x; i < end; i += kBlockThreads) hashes[i] = v;
+}
+
+// B6: level-1 unpermute. Per level-1 tile: gather the pass bits of its bucket runs out of the level-2
+// result bits (bits2, level-2 array order) into LDS in the tile's bucket-sorted order, 64-bit pieces
+// per item (run, piece), then map every row through its position (pos1) -> result bits + counts.
+constexpr int kBucketUnpermuteThreads = 256;
+__global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kernel(
+    const uint16_t* __restrict__ pos1, const uint64_t* __restrict__ bits2, uint64_t n, uint32_t bucket_mask,
+    const uint32_t* __restrict__ counts_tm, const uint32_t* __restrict__ pre_tm, const uint64_t* __restrict__ base,
+    uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
+  __shared__ uint32_t s_bits[kTileRows / 32];
+  __shared__ uint32_t s_start[kMaxBuckets], s_item[kMaxBuckets + 1], s_cnt[kMaxBuckets];
+  __shared__ uint64_t s_g[kMaxBuckets];
+  __shared__ uint32_t s_wave[kBucketUnpermuteThreads / 64][2];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr uint32_t kWaves = kBucketUnpermuteThreads / 64;
+  const uint32_t nb = bucket_mask + 1;
+  const uint64_t tile = blockIdx.x;
+  const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
+  constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / kWaves;
+  const uint64_t seg0 = tile * (kTileRows / kSegRows) + wave * kSegsPerWave;
+  u32x4 pv[kSegsPerWave];  // row positions, in flight while the bits are staged
+#pragma unroll
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    pv[sg] = u32x4{0, 0, 0, 0};
+    if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos1 + (seg0 + sg) * kSegRows + lane * 8);
+  }
+  for (uint32_t i = threadIdx.x; i < kTileRows / 32; i += kBucketUnpermuteThreads) s_bits[i] = 0;
+  // per bucket: run length, start in the tile's sorted order, start in bits2, 64-bit pieces (scans by
+  // the whole workgroup, kMaxBuckets / 256 buckets per thread)
+  constexpr int kPer = kMaxBuckets / kBucketUnpermuteThreads;
+  uint32_t c[kPer], k[kPer], tc = 0, tk = 0;
+#pragma unroll
+  for (int i = 0; i < kPer; i++) {
+    const uint32_t b = threadIdx.x * kPer + i;
+    c[i] = b < nb ? counts_tm[tile * nb + b] : 0u;
+    k[i] = (c[i] + 63) / 64;
+    tc += c[i];
+    tk += k[i];
+    if (b < nb) {
+      s_cnt[b] = c[i];
+      s_g[b] = base[b] + pre_tm[tile * nb + b];
+    }
+  }
+  const uint32_t ic = wave_inclusive_sum(tc), ik = wave_inclusive_sum(tk);
+  if (lane == 63) {
+    s_wave[wave][0] = ic;
+    s_wave[wave][1] = ik;
+  }
+  __syncthreads();
+  uint32_t oc = ic - tc, ok_ = ik - tk, total_items = 0;
+  for (uint32_t w = 0; w < kWaves; w++) {
+    oc += w < wave ? s_wave[w][0] : 0u;
+    ok_ += w < wave ? s_wave[w][1] : 0u;
+    total_items += s_wave[w][1];
+  }
+#pragma unroll
+  for (int i = 0; i < kPer; i++) {
+    const uint32_t b = threadIdx.x * kPer + i;
+    if (b < nb) {
+      s_start[b] = oc;
+      s_item[b] = ok_;
+    }
+    oc += c[i];
+    ok_ += k[i];
+  }
+  if (threadIdx.x == 0) s_item[nb] = total_items;
+  __syncthreads();
+  for (uint32_t it = threadIdx.x; it < total_items; it += kBucketUnpermuteThreads) {
+    uint32_t lo = 0, hi = nb;  // last bucket whose first item <= it
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_item[mid] <= it) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t b = lo, piece = it - s_item[b];
+    const uint32_t len = min(64u, s_cnt[b] - piece * 64);
+    const uint64_t q = s_g[b] + piece * 64ULL;
+    const uint32_t sh = static_cast<uint32_t>(q & 63);
+    const uint64_t w0 = bits2[q >> 6];
+    uint64_t v = w0 >> sh;
+    if (sh != 0 && sh + len > 64) v |= bits2[(q >> 6) + 1] << (64 - sh);
+    if (len < 64) v &= (1ULL << len) - 1;
+    const uint32_t d = s_start[b] + piece * 64;  // destination bit in the tile's sorted order
+    const uint32_t dw = d >> 5, ds = d & 31;
+    atomicOr(&s_bits[dw], static_cast<uint32_t>(v << ds));
+    if (len + ds > 32) atomicOr(&s_bits[dw + 1], static_cast<uint32_t>(v >> (32 - ds)));
+    if (len + ds > 64) atomicOr(&s_bits[dw + 2], static_cast<uint32_t>(v >> (64 - ds)));
+  }
+  __syncthreads();
+  uint8_t* out_bytes = reinterpret_cast<uint8_t*>(out_bits);
+#pragma unroll
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    const uint64_t seg = seg0 + sg;
+    if (seg >= n_segs) break;
+    uint32_t byte = 0;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+      byte |= ((s_bits[p >> 5] >> (p & 31)) & 1u) << e;
+    }
+    const uint64_t row0 = seg * kSegRows + lane * 8;
     if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
     out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);
     const uint32_t cnt = wave_sum(__popc(byte));
@@ -1003,12 +1324,22 @@ struct ProbeWorkspace {
   uint32_t* seg_counts;
   uint32_t* group_sums;
   uint32_t* group_offs;
-  // partitioned strategy only
+  // partitioned strategy (and level 2 of the bucketed one)
   uint32_t* recs;
   uint16_t* pos;
   uint8_t* passb;
   uint32_t* runs;     // slice-major [slice][tile]
   uint32_t* runs_tm;  // tile-major [tile][slice] (partition kernel output)
+  // bucketed strategy, level 1
+  uint32_t* counts_tm;     // [tile1][bucket] rows
+  uint32_t* pre_bm;        // [bucket][tile1] run start inside the bucket's array
+  uint32_t* pre_tm;        // [tile1][bucket] the same, tile-major
+  uint32_t* totals;        // [bucket] rows
+  uint64_t* bbase;         // [bucket + 1] first row of the bucket in the level-2 array
+  uint32_t* bucket_tiles;  // [bucket + 1] first level-2 tile of the bucket; [nb] = level-2 tile count
+  uint64_t* hashes;        // level-2 array: per bucket, its rows' hashes padded to whole tiles
+  uint16_t* pos1;          // row -> position in its level-1 tile's bucket-sorted order
+  uint64_t* bits2;         // level-2 result bits (level-2 array order)
 };
 
 uint32_t slice_count(int log_num_blocks) {
@@ -1017,88 +1348,169 @@ uint32_t slice_count(int log_num_blocks) {
 
 // Strategy a probe of this filter will run: explicit choice, else by filter size
 // (<= 64 KiB: LDS-resident filter; <= 16 MiB: partitioned into LDS slices; larger: direct gather).
-int resolve_strategy(int requested, int log_num_blocks) {
-  if (requested != RPT_PROBE_AUTO) return requested;
-  if (log_num_blocks <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
-  if (slice_count(log_num_blocks) <= static_cast<uint32_t>(rpt::kMaxSliceCount)) return RPT_PROBE_PARTITIONED;
-  return RPT_PROBE_GATHER;
+uint32_t bucket_count(int log_num_blocks) {
+  return 1u << std::max(0, log_num_blocks - rpt::kSliceLog - rpt::kBucketSliceLog);
 }
 
 int strategy_supported(int strategy, int log_num_blocks) {
+  constexpr int kBucketLog = rpt::kSliceLog + rpt::kBucketSliceLog;  // log2 blocks per bucket (21)
   switch (strategy) {
     case RPT_PROBE_GATHER: return 1;
     case RPT_PROBE_LDS: return log_num_blocks <= rpt::kLdsDirectMaxLog;
     case RPT_PROBE_PARTITIONED:
       return log_num_blocks >= rpt::kSliceLog && slice_count(log_num_blocks) <= static_cast<uint32_t>(rpt::kMaxSliceCount);
+    case RPT_PROBE_BUCKETED:  // 2..1024 buckets of 16 MiB
+      return log_num_blocks > kBucketLog && bucket_count(log_num_blocks) <= rpt::kMaxBuckets;
     default: return 0;
   }
 }
 
-// Layout (all 256-aligned): bits | seg_counts | group_sums | group_offs [| recs | pos | passb | runs].
-// The partitioned part is sized for whole 16 Ki-row tiles and only present when `partitioned`.
-size_t workspace_layout(uint64_t n, int log_num_blocks, bool partitioned, void* base, ProbeWorkspace* ws) {
+// The routed strategies (partitioned, bucketed) make one pass over the whole filter (every slice is
+// staged in LDS once), so they pay off only when the batch is large against the filter: n >= blocks/8
+// (measured break-even against the gather: ~0.1 x blocks).
+bool worth_routing(int log_num_blocks, uint64_t n) { return n >= ((1ULL << log_num_blocks) >> 3); }
+
+// AUTO: LDS for small filters; else a routed strategy for large batches; else the gather. n = ~0 is
+// "a batch of unknown, large size" (rpt_bf_probe_strategy).
+int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
+  if (requested != RPT_PROBE_AUTO) return requested;
+  if (log_num_blocks <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
+  if (!worth_routing(log_num_blocks, n)) return RPT_PROBE_GATHER;
+  if (strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks)) return RPT_PROBE_PARTITIONED;
+  if (strategy_supported(RPT_PROBE_BUCKETED, log_num_blocks)) return RPT_PROBE_BUCKETED;
+  return RPT_PROBE_GATHER;
+}
+
+// Tile-count bound of the bucketed level-2 array: every non-empty bucket pads < 1 tile.
+uint64_t level2_tiles_max(uint64_t n, int log_num_blocks) {
+  return ceil_div(n, rpt::kTileRows) + std::min<uint64_t>(bucket_count(log_num_blocks), n);
+}
+
+// Layout (all 256-aligned): bits | seg_counts | group_sums | group_offs, then for the partitioned
+// strategy recs | pos | passb | runs | runs_tm (whole 16 Ki-row tiles), and for the bucketed one the
+// same level-2 arrays over level2_tiles_max tiles of 128 slices plus the level-1 arrays.
+size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base, ProbeWorkspace* ws) {
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
-  const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
-  const uint64_t padded = n_tiles * rpt::kTileRows;
-  size_t sz[10] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
-                   align256(n_groups * 4), align256(n_groups * 4), 0, 0, 0, 0, 0, 0};
-  if (partitioned) {
-    const uint64_t cap = rpt::tile_cap_for(slice_count(log_num_blocks));
-    sz[4] = align256(n_tiles * cap * 4);
-    sz[5] = align256(padded * 2);
-    sz[6] = align256(n_tiles * cap / 8);
-    sz[7] = align256(static_cast<uint64_t>(slice_count(log_num_blocks)) * n_tiles * 4);
+  const uint64_t T = rpt::kTileRows;
+  constexpr int kParts = 19;
+  size_t sz[kParts] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
+                       align256(n_groups * 4), align256(n_groups * 4)};
+  const bool part = strategy == RPT_PROBE_PARTITIONED, buck = strategy == RPT_PROBE_BUCKETED;
+  if (part || buck) {
+    const uint64_t tiles = part ? ceil_div(n, T) : level2_tiles_max(n, log_num_blocks);
+    const uint32_t slices = part ? slice_count(log_num_blocks) : rpt::kBucketSlices;
+    const uint64_t cap = rpt::tile_cap_for(slices);
+    sz[4] = align256(tiles * cap * 4);
+    sz[5] = align256(tiles * T * 2);
+    sz[6] = align256(tiles * cap / 8);
+    sz[7] = align256(static_cast<uint64_t>(slices) * tiles * 4);
     sz[8] = sz[7];
   }
-  size_t off[10], total = 0;
-  for (int i = 0; i < 10; i++) {
+  if (buck) {
+    const uint64_t t1 = ceil_div(n, T), t2 = level2_tiles_max(n, log_num_blocks);
+    const uint64_t nb = bucket_count(log_num_blocks);
+    sz[9] = sz[10] = sz[11] = align256(t1 * nb * 4);
+    sz[12] = align256(nb * 4);
+    sz[13] = align256((nb + 1) * 8);
+    sz[14] = align256((nb + 1) * 4);
+    sz[15] = align256(t2 * T * 8);
+    sz[16] = align256(t1 * T * 2);
+    sz[17] = align256(t2 * T / 8);
+  }
+  size_t off[kParts], total = 0;
+  for (int i = 0; i < kParts; i++) {
     off[i] = total;
     total += sz[i];
   }
   if (ws) {
     char* p = static_cast<char*>(base);
-    ws->bits = reinterpret_cast<uint64_t*>(p + off[0]);
-    ws->seg_counts = reinterpret_cast<uint32_t*>(p + off[1]);
-    ws->group_sums = reinterpret_cast<uint32_t*>(p + off[2]);
-    ws->group_offs = reinterpret_cast<uint32_t*>(p + off[3]);
-    ws->recs = partitioned ? reinterpret_cast<uint32_t*>(p + off[4]) : nullptr;
-    ws->pos = partitioned ? reinterpret_cast<uint16_t*>(p + off[5]) : nullptr;
-    ws->passb = partitioned ? reinterpret_cast<uint8_t*>(p + off[6]) : nullptr;
-    ws->runs = partitioned ? reinterpret_cast<uint32_t*>(p + off[7]) : nullptr;
-    ws->runs_tm = partitioned ? reinterpret_cast<uint32_t*>(p + off[8]) : nullptr;
+    auto at = [&](int i) -> void* { return sz[i] ? p + off[i] : nullptr; };
+    ws->bits = static_cast<uint64_t*>(at(0));
+    ws->seg_counts = static_cast<uint32_t*>(at(1));
+    ws->group_sums = static_cast<uint32_t*>(at(2));
+    ws->group_offs = static_cast<uint32_t*>(at(3));
+    ws->recs = static_cast<uint32_t*>(at(4));
+    ws->pos = static_cast<uint16_t*>(at(5));
+    ws->passb = static_cast<uint8_t*>(at(6));
+    ws->runs = static_cast<uint32_t*>(at(7));
+    ws->runs_tm = static_cast<uint32_t*>(at(8));
+    ws->counts_tm = static_cast<uint32_t*>(at(9));
+    ws->pre_bm = static_cast<uint32_t*>(at(10));
+    ws->pre_tm = static_cast<uint32_t*>(at(11));
+    ws->totals = static_cast<uint32_t*>(at(12));
+    ws->bbase = static_cast<uint64_t*>(at(13));
+    ws->bucket_tiles = static_cast<uint32_t*>(at(14));
+    ws->hashes = static_cast<uint64_t*>(at(15));
+    ws->pos1 = static_cast<uint16_t*>(at(16));
+    ws->bits2 = static_cast<uint64_t*>(at(17));
   }
   return total;
 }
 
-// Build workspace (partitioned insert): records | runs (slice-major) | runs (tile-major).
+// Build workspace: records | runs (slice-major) | runs (tile-major) (partitioned, or level 2 of the
+// bucketed insert), then the bucketed level-1 arrays.
 struct InsertWorkspace {
   uint32_t* recs;
   uint32_t* runs;
   uint32_t* runs_tm;
+  uint32_t* counts_tm;
+  uint32_t* pre_bm;
+  uint32_t* pre_tm;
+  uint32_t* totals;
+  uint64_t* bbase;
+  uint32_t* bucket_tiles;
+  uint64_t* hashes;
 };
 
-size_t insert_workspace_layout(uint64_t n, int log_num_blocks, void* base, InsertWorkspace* ws) {
-  const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
-  const uint32_t slices = slice_count(log_num_blocks);
-  const size_t b0 = align256(n_tiles * rpt::tile_cap_for(slices) * 4);
-  const size_t b1 = align256(static_cast<uint64_t>(slices) * n_tiles * 4);
+size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base, InsertWorkspace* ws) {
+  const bool buck = strategy == RPT_INSERT_BUCKETED;
+  if (strategy != RPT_INSERT_PARTITIONED && !buck) return 0;
+  const uint64_t T = rpt::kTileRows;
+  const uint64_t tiles = buck ? level2_tiles_max(n, log_num_blocks) : ceil_div(n, T);
+  const uint32_t slices = buck ? rpt::kBucketSlices : slice_count(log_num_blocks);
+  constexpr int kParts = 10;
+  size_t sz[kParts] = {align256(tiles * rpt::tile_cap_for(slices) * 4), align256(static_cast<uint64_t>(slices) * tiles * 4),
+                       align256(static_cast<uint64_t>(slices) * tiles * 4)};
+  if (buck) {
+    const uint64_t t1 = ceil_div(n, T), nb = bucket_count(log_num_blocks);
+    sz[3] = sz[4] = sz[5] = align256(t1 * nb * 4);
+    sz[6] = align256(nb * 4);
+    sz[7] = align256((nb + 1) * 8);
+    sz[8] = align256((nb + 1) * 4);
+    sz[9] = align256(tiles * T * 8);
+  }
+  size_t off[kParts], total = 0;
+  for (int i = 0; i < kParts; i++) {
+    off[i] = total;
+    total += sz[i];
+  }
   if (ws) {
     char* p = static_cast<char*>(base);
-    ws->recs = reinterpret_cast<uint32_t*>(p);
-    ws->runs = reinterpret_cast<uint32_t*>(p + b0);
-    ws->runs_tm = reinterpret_cast<uint32_t*>(p + b0 + b1);
+    auto at = [&](int i) -> void* { return sz[i] ? p + off[i] : nullptr; };
+    ws->recs = static_cast<uint32_t*>(at(0));
+    ws->runs = static_cast<uint32_t*>(at(1));
+    ws->runs_tm = static_cast<uint32_t*>(at(2));
+    ws->counts_tm = static_cast<uint32_t*>(at(3));
+    ws->pre_bm = static_cast<uint32_t*>(at(4));
+    ws->pre_tm = static_cast<uint32_t*>(at(5));
+    ws->totals = static_cast<uint32_t*>(at(6));
+    ws->bbase = static_cast<uint64_t*>(at(7));
+    ws->bucket_tiles = static_cast<uint32_t*>(at(8));
+    ws->hashes = static_cast<uint64_t*>(at(9));
   }
-  return b0 + 2 * b1;
+  return total;
 }
 
 constexpr uint64_t kPartitionedInsertMinRows = 1ULL << 20;
 
 int resolve_insert_strategy(int requested, int log_num_blocks, uint64_t n) {
-  const bool part_ok = strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks);
-  if (requested == RPT_INSERT_AUTO)
-    return (part_ok && n >= kPartitionedInsertMinRows) ? RPT_INSERT_PARTITIONED : RPT_INSERT_ATOMIC;
-  return requested;
+  if (requested != RPT_INSERT_AUTO) return requested;
+  if (n < kPartitionedInsertMinRows) return RPT_INSERT_ATOMIC;
+  if (strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks)) return RPT_INSERT_PARTITIONED;
+  if (strategy_supported(RPT_PROBE_BUCKETED, log_num_blocks) && worth_routing(log_num_blocks, n))
+    return RPT_INSERT_BUCKETED;
+  return RPT_INSERT_ATOMIC;
 }
 
 int check_col(const rpt_key_column* col) {
@@ -1135,34 +1547,64 @@ void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, con
                      (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
 }
 
+// Let `fn` use all of the CU's 160 KiB of LDS: dynamic allowance = 160 KiB - its static LDS.
+void allow_dynamic_lds(const void* fn) {
+  hipFuncAttributes at{};
+  size_t stat = 0;
+  if (hipFuncGetAttributes(&at, fn) == hipSuccess) stat = at.sharedSizeBytes;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>((160u << 10) - stat));
+  (void)hipGetLastError();
+}
+
 template <int K, bool D, bool MM>
 void launch_partition_mm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
-                         uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats) {
+                         uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
+                         const uint32_t* dev_n_tiles = nullptr) {
   const uint32_t slices = slice_mask + 1;
   const size_t lds = rpt::tile_cap_for(slices) * 4 + 2ULL * slices * 4;
   static std::once_flag once;  // per instantiation; > 64 KiB of dynamic LDS must be opted into
-  std::call_once(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  });
+  std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM>)); });
   hipLaunchKernelGGL((rpt::partition_kernel<K, D, MM>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, slice_mask,
-                     n_tiles, recs, pos, runs, stats);
+                     n_tiles, recs, pos, runs, stats, dev_n_tiles);
 }
 
 // stats == nullptr: probe (no min/max); otherwise the build's key min/max is folded into stats.
 template <int K, bool D>
 void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
-                        uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats) {
+                        uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
+                        const uint32_t* dev_n_tiles) {
   if (K != rpt::kKeyHash && stats != nullptr)
-    launch_partition_mm<K, D, true>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats);
+    launch_partition_mm<K, D, true>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
   else
-    launch_partition_mm<K, D, false>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, nullptr);
+    launch_partition_mm<K, D, false>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, nullptr, dev_n_tiles);
 }
 
 template <int K, bool D>
 void launch_insert_t(unsigned grid, hipStream_t s, rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n, uint64_t n_segs) {
   hipLaunchKernelGGL((rpt::insert_kernel<K, D>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
                      (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bf->stats);
+}
+
+template <int K, bool D>
+void launch_bucket_count_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
+                           uint32_t* counts_tm, int64_t* stats) {
+  if (K != rpt::kKeyHash && stats != nullptr)
+    hipLaunchKernelGGL((rpt::bucket_count_kernel<K, D, true>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n,
+                       bucket_mask, counts_tm, stats);
+  else
+    hipLaunchKernelGGL((rpt::bucket_count_kernel<K, D, false>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n,
+                       bucket_mask, counts_tm, static_cast<int64_t*>(nullptr));
+}
+
+template <int K, bool D>
+void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
+                             const uint32_t* counts_tm, const uint32_t* pre_tm, const uint64_t* bbase, uint64_t* hashes,
+                             uint16_t* pos1) {
+  const size_t lds = rpt::kTileRows * 8;
+  static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into (160 KiB minus the static part)
+  std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D>)); });
+  hipLaunchKernelGGL((rpt::bucket_scatter_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, bucket_mask,
+                     counts_tm, pre_tm, bbase, hashes, pos1);
 }
 
 #define RPT_DISPATCH_KD(fn, kt, dense, ...)                  \
@@ -1182,6 +1624,57 @@ void launch_insert_t(unsigned grid, hipStream_t s, rpt_bf* bf, const rpt::KeyArg
         break;                                               \
     }                                                        \
   } while (0)
+
+// [rows][cols] u32 matrix -> [cols][rows] (the run-table transpose kernel).
+int transpose_u32(hipStream_t s, const uint32_t* in, uint64_t rows, uint64_t cols, uint32_t* out) {
+  if (ceil_div(cols, 64) > 65535) return fail(RPT_ERR_INVALID_ARGUMENT, "transpose of %llu columns", (unsigned long long)cols);
+  ProfScope prof_t("runs_transpose_kernel", s);
+  hipLaunchKernelGGL(rpt::runs_transpose_kernel, dim3(static_cast<unsigned>(ceil_div(rows, 64)), static_cast<unsigned>(ceil_div(cols, 64))),
+                     dim3(rpt::kBlockThreads), 0, s, in, static_cast<uint32_t>(cols), rows, out);
+  prof_t.end();
+  RPT_LAUNCHED("runs_transpose_kernel");
+  return RPT_OK;
+}
+
+// Level 1 of the bucketed strategies: rows per (tile, bucket) [+ the build's min/max], the buckets'
+// prefix tables and bases, every row's hash copied into its bucket's array (+ its position in the
+// tile's bucket-sorted order when pos1 != nullptr), each array padded to whole tiles.
+struct BucketLevel1 {
+  uint32_t *counts_tm, *pre_bm, *pre_tm, *totals, *bucket_tiles;
+  uint64_t *bbase, *hashes;
+  uint16_t* pos1;
+};
+int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool dense, uint64_t n, int L,
+                      const BucketLevel1& w, int64_t* stats) {
+  const uint32_t nb = bucket_count(L);
+  const uint64_t t1 = ceil_div(n, rpt::kTileRows);
+  {
+    ProfScope prof_c("bucket_count_kernel", s);
+    RPT_DISPATCH_KD(launch_bucket_count_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm, stats);
+    prof_c.end();
+    RPT_LAUNCHED("bucket_count_kernel");
+  }
+  int st = transpose_u32(s, w.counts_tm, t1, nb, w.pre_bm);
+  if (st != RPT_OK) return st;
+  {
+    ProfScope prof_s("bucket_scan_kernel", s);
+    hipLaunchKernelGGL(rpt::bucket_scan_kernel, dim3(nb), dim3(1024), 0, s, w.pre_bm, t1, w.totals);
+    hipLaunchKernelGGL(rpt::bucket_base_kernel, dim3(1), dim3(1024), 0, s, w.totals, nb, w.bbase, w.bucket_tiles);
+    prof_s.end();
+    RPT_LAUNCHED("bucket_scan_kernel");
+  }
+  st = transpose_u32(s, w.pre_bm, nb, t1, w.pre_tm);
+  if (st != RPT_OK) return st;
+  {
+    ProfScope prof_x("bucket_scatter_kernel", s);
+    RPT_DISPATCH_KD(launch_bucket_scatter_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm,
+                    w.pre_tm, w.bbase, w.hashes, w.pos1);
+    hipLaunchKernelGGL(rpt::bucket_pad_kernel, dim3(nb), dim3(rpt::kBlockThreads), 0, s, w.totals, w.bbase, w.hashes);
+    prof_x.end();
+    RPT_LAUNCHED("bucket_scatter_kernel");
+  }
+  return RPT_OK;
+}
 
 int alloc_words(rpt_bf* bf, int log_nb) {
   const uint64_t nw = 1ULL << log_nb;
@@ -1281,9 +1774,22 @@ int rpt_bf_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows) {
 }
 
 size_t rpt_probe_workspace_bytes(uint64_t n_rows, int log_num_blocks) {
-  // enough for any strategy the filter may run (the partitioned one needs the most)
-  const bool part = strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks);
-  return workspace_layout(n_rows, log_num_blocks, part, nullptr, nullptr);
+  // enough for any strategy the filter may run
+  size_t m = 0;
+  for (int st : {RPT_PROBE_GATHER, RPT_PROBE_LDS, RPT_PROBE_PARTITIONED, RPT_PROBE_BUCKETED})
+    if (strategy_supported(st, log_num_blocks)) m = std::max(m, workspace_layout(n_rows, log_num_blocks, st, nullptr, nullptr));
+  return m;
+}
+
+int rpt_bf_probe_strategy_for(const rpt_bf* bf, uint64_t n_rows) {
+  if (!bf) return -fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  return resolve_strategy(bf->probe_strategy.load(), bf->log_num_blocks, n_rows);
+}
+
+size_t rpt_bf_probe_workspace_bytes(const rpt_bf* bf, uint64_t n_rows) {
+  if (!bf) return 0;
+  const int st = resolve_strategy(bf->probe_strategy.load(), bf->log_num_blocks, n_rows);
+  return workspace_layout(n_rows, bf->log_num_blocks, st, nullptr, nullptr);
 }
 
 int rpt_probe_strategy_supported(int strategy, int log_num_blocks) {
@@ -1292,7 +1798,7 @@ int rpt_probe_strategy_supported(int strategy, int log_num_blocks) {
 
 int rpt_bf_set_probe_strategy(rpt_bf* bf, int strategy) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
-  if (strategy < RPT_PROBE_AUTO || strategy > RPT_PROBE_PARTITIONED)
+  if (strategy < RPT_PROBE_AUTO || strategy > RPT_PROBE_BUCKETED)
     return fail(RPT_ERR_INVALID_ARGUMENT, "unknown probe strategy %d", strategy);
   bf->probe_strategy.store(strategy);
   return RPT_OK;
@@ -1300,7 +1806,7 @@ int rpt_bf_set_probe_strategy(rpt_bf* bf, int strategy) {
 
 int rpt_bf_probe_strategy(const rpt_bf* bf) {
   if (!bf) return -fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
-  return resolve_strategy(bf->probe_strategy.load(), bf->log_num_blocks);
+  return resolve_strategy(bf->probe_strategy.load(), bf->log_num_blocks, ~0ULL);
 }
 
 int rpt_bf_create_log_blocks(int device, int log_num_blocks, rpt_bf** out) {
@@ -1428,13 +1934,28 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
 }
 
 size_t rpt_insert_workspace_bytes(uint64_t n_rows, int log_num_blocks) {
-  return strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks) ? insert_workspace_layout(n_rows, log_num_blocks, nullptr, nullptr)
-                                                                    : 0;
+  size_t m = 0;
+  if (strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks))
+    m = std::max(m, insert_workspace_layout(n_rows, log_num_blocks, RPT_INSERT_PARTITIONED, nullptr, nullptr));
+  if (strategy_supported(RPT_PROBE_BUCKETED, log_num_blocks))
+    m = std::max(m, insert_workspace_layout(n_rows, log_num_blocks, RPT_INSERT_BUCKETED, nullptr, nullptr));
+  return m;
+}
+
+int rpt_bf_insert_strategy_for(const rpt_bf* bf, uint64_t n_rows) {
+  if (!bf) return -fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  return resolve_insert_strategy(bf->insert_strategy.load(), bf->log_num_blocks, n_rows);
+}
+
+size_t rpt_bf_insert_workspace_bytes(const rpt_bf* bf, uint64_t n_rows) {
+  if (!bf) return 0;
+  const int st = resolve_insert_strategy(bf->insert_strategy.load(), bf->log_num_blocks, n_rows);
+  return insert_workspace_layout(n_rows, bf->log_num_blocks, st, nullptr, nullptr);
 }
 
 int rpt_bf_set_insert_strategy(rpt_bf* bf, int strategy) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
-  if (strategy < RPT_INSERT_AUTO || strategy > RPT_INSERT_PARTITIONED)
+  if (strategy < RPT_INSERT_AUTO || strategy > RPT_INSERT_BUCKETED)
     return fail(RPT_ERR_INVALID_ARGUMENT, "unknown insert strategy %d", strategy);
   bf->insert_strategy.store(strategy);
   return RPT_OK;
@@ -1447,37 +1968,60 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   const int L = bf->log_num_blocks;
   const int strategy = resolve_insert_strategy(bf->insert_strategy.load(), L, n);
   if (strategy == RPT_INSERT_ATOMIC) return rpt_bf_insert(bf, col, n, stream);
-  if (!strategy_supported(RPT_PROBE_PARTITIONED, L))
-    return fail(RPT_ERR_INVALID_ARGUMENT, "partitioned insert unsupported for a 2^%d-block filter", L);
+  const bool buck = strategy == RPT_INSERT_BUCKETED;
+  if (!strategy_supported(buck ? RPT_PROBE_BUCKETED : RPT_PROBE_PARTITIONED, L))
+    return fail(RPT_ERR_INVALID_ARGUMENT, "%s insert unsupported for a 2^%d-block filter",
+                buck ? "bucketed" : "partitioned", L);
   int st = check_col(col);
   if (st != RPT_OK) return st;
-  const size_t need = insert_workspace_layout(n, L, nullptr, nullptr);
+  const size_t need = insert_workspace_layout(n, L, strategy, nullptr, nullptr);
   if (!workspace || workspace_bytes < need)
     return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   RPT_ON_DEVICE(bf->device);
   bf->has_data.store(1);  // bloom_filter.cpp:75
   InsertWorkspace ws;
-  insert_workspace_layout(n, L, workspace, &ws);
+  insert_workspace_layout(n, L, strategy, workspace, &ws);
   hipStream_t s = as_stream(stream);
-  const uint32_t slices = slice_count(L);
-  const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
   const int cus = num_cus(bf->device);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  const bool dense = dense_ok(col, nullptr);
+  // the partition input: the key column itself, or (bucketed) the level-2 hash array
+  uint32_t tile_slices = slice_count(L);
+  uint64_t n_tiles = ceil_div(n, rpt::kTileRows), n_part = n;
+  rpt::KeyArgs pa = a;
+  int p_type = col->key_type;
+  bool p_dense = dense;
+  int64_t* p_stats = bf->stats;
+  const uint32_t* bucket_tiles = nullptr;
+  const uint32_t* dev_n_tiles = nullptr;
+  uint32_t grid_slices = tile_slices;
+  if (buck) {
+    const BucketLevel1 l1{ws.counts_tm, ws.pre_bm, ws.pre_tm, ws.totals, ws.bucket_tiles, ws.bbase, ws.hashes, nullptr};
+    st = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, bf->stats);
+    if (st != RPT_OK) return st;
+    tile_slices = rpt::kBucketSlices;
+    n_tiles = level2_tiles_max(n, L);
+    n_part = n_tiles * rpt::kTileRows;
+    pa = rpt::KeyArgs{ws.hashes, nullptr, nullptr, nullptr};
+    p_type = RPT_KEY_HASH;
+    p_dense = true;
+    p_stats = nullptr;  // min/max came from the key read of level 1
+    bucket_tiles = ws.bucket_tiles;
+    dev_n_tiles = ws.bucket_tiles + bucket_count(L);
+    grid_slices = bucket_count(L) * rpt::kBucketSlices;
+  }
   ProfScope prof_p("partition_kernel", s);
-  RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense_ok(col, nullptr), static_cast<unsigned>(n_tiles), s, a, n,
-                  slices - 1, n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, bf->stats);
+  RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
+                  n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, p_stats, dev_n_tiles);
   prof_p.end();
   RPT_LAUNCHED("partition_kernel");
-  ProfScope prof_t("runs_transpose_kernel", s);
-  hipLaunchKernelGGL(rpt::runs_transpose_kernel, dim3(static_cast<unsigned>(ceil_div(n_tiles, 64)), ceil_div(slices, 64)),
-                     dim3(rpt::kBlockThreads), 0, s, ws.runs_tm, slices, n_tiles, ws.runs);
-  prof_t.end();
-  RPT_LAUNCHED("runs_transpose_kernel");
+  st = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
+  if (st != RPT_OK) return st;
   const uint32_t splits = static_cast<uint32_t>(
-      std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) / slices)));
+      std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) / grid_slices)));
   ProfScope prof_i("slice_insert_kernel", s);
-  hipLaunchKernelGGL(rpt::slice_insert_kernel, dim3(slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words, splits,
-                     n_tiles, ws.recs, ws.runs);
+  hipLaunchKernelGGL(rpt::slice_insert_kernel, dim3(grid_slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words, splits,
+                     n_tiles, ws.recs, ws.runs, tile_slices, bucket_tiles);
   prof_i.end();
   RPT_LAUNCHED("slice_insert_kernel");
   return RPT_OK;
@@ -1509,16 +2053,15 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
   int st = check_col(col);
   if (st != RPT_OK) return st;
   const int L = bf->log_num_blocks;
-  const int strategy = resolve_strategy(bf->probe_strategy.load(), L);
+  const int strategy = resolve_strategy(bf->probe_strategy.load(), L, n);
   if (!strategy_supported(strategy, L))
     return fail(RPT_ERR_INVALID_ARGUMENT, "probe strategy %d unsupported for a 2^%d-block filter", strategy, L);
-  const bool part = strategy == RPT_PROBE_PARTITIONED;
-  const size_t need = workspace_layout(n, L, part, nullptr, nullptr);
+  const size_t need = workspace_layout(n, L, strategy, nullptr, nullptr);
   if (!workspace || workspace_bytes < need)
     return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   RPT_ON_DEVICE(bf->device);
   ProbeWorkspace ws;
-  workspace_layout(n, L, part, workspace, &ws);
+  workspace_layout(n, L, strategy, workspace, &ws);
   hipStream_t s = as_stream(stream);
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, row_sel};
@@ -1539,39 +2082,68 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     prof4_.end();
     RPT_LAUNCHED("probe_bits_kernel<lds>");
   } else {
-    const uint32_t slices = slice_count(L);
-    const uint64_t n_tiles = ceil_div(n, rpt::kTileRows);
+    // PARTITIONED: the key column, tiles of slice_count(L) slices. BUCKETED: level 1 first, then the
+    // same pipeline over the level-2 hash array (tiles of 128 slices, bucket by bucket), then level 1's
+    // unpermute.
+    const bool buck = strategy == RPT_PROBE_BUCKETED;
+    uint32_t tile_slices = slice_count(L), grid_slices = tile_slices;
+    uint64_t n_tiles = ceil_div(n, rpt::kTileRows), n_part = n;
+    rpt::KeyArgs pa = a;
+    int p_type = col->key_type;
+    bool p_dense = dense;
+    const uint32_t* bucket_tiles = nullptr;
+    const uint32_t* dev_n_tiles = nullptr;
+    uint64_t* part_bits = ws.bits;
+    uint32_t* part_counts = ws.seg_counts;
+    if (buck) {
+      const BucketLevel1 l1{ws.counts_tm, ws.pre_bm, ws.pre_tm, ws.totals, ws.bucket_tiles, ws.bbase, ws.hashes, ws.pos1};
+      int st1 = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, nullptr);
+      if (st1 != RPT_OK) return st1;
+      tile_slices = rpt::kBucketSlices;
+      grid_slices = bucket_count(L) * rpt::kBucketSlices;
+      n_tiles = level2_tiles_max(n, L);
+      n_part = n_tiles * rpt::kTileRows;
+      pa = rpt::KeyArgs{ws.hashes, nullptr, nullptr, nullptr};
+      p_type = RPT_KEY_HASH;
+      p_dense = true;
+      bucket_tiles = ws.bucket_tiles;
+      dev_n_tiles = ws.bucket_tiles + bucket_count(L);
+      part_bits = ws.bits2;
+      part_counts = nullptr;
+    }
     const int cus = num_cus(bf->device);
-    const unsigned g_tiles = static_cast<unsigned>(n_tiles);  // one tile per workgroup
     ProfScope prof5_("partition_kernel", s);
-    RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense, g_tiles, s, a, n, slices - 1, n_tiles, ws.recs, ws.pos,
-                    ws.runs_tm, static_cast<int64_t*>(nullptr));
+    RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
+                    n_tiles, ws.recs, ws.pos, ws.runs_tm, static_cast<int64_t*>(nullptr), dev_n_tiles);
     prof5_.end();
     RPT_LAUNCHED("partition_kernel");
-    {
-      ProfScope prof_t("runs_transpose_kernel", s);
-      hipLaunchKernelGGL(rpt::runs_transpose_kernel, dim3(static_cast<unsigned>(ceil_div(n_tiles, 64)), ceil_div(slices, 64)),
-                         dim3(rpt::kBlockThreads), 0, s, ws.runs_tm, slices, n_tiles, ws.runs);
-      prof_t.end();
-      RPT_LAUNCHED("runs_transpose_kernel");
-    }
+    int st2 = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
+    if (st2 != RPT_OK) return st2;
     // exactly one resident round of slice workgroups (LDS decides how many fit per CU), never more
     // splits than tiles
     const uint64_t slice_lds = rpt::kSliceWords * 8 + 8ULL * rpt::kRotMasks;
     const uint64_t per_cu = std::max<uint64_t>(1, (160ULL << 10) / slice_lds);
     const uint32_t splits = static_cast<uint32_t>(std::max<uint64_t>(
-        1, std::min<uint64_t>(n_tiles, (static_cast<uint64_t>(cus) * per_cu) / slices)));
+        1, std::min<uint64_t>(n_tiles, (static_cast<uint64_t>(cus) * per_cu) / grid_slices)));
     ProfScope prof6_("slice_probe_kernel", s);
-    hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words,
-                       splits, n_tiles, ws.recs, ws.runs, ws.passb);
+    hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(grid_slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words,
+                       splits, n_tiles, ws.recs, ws.runs, ws.passb, tile_slices, bucket_tiles);
     prof6_.end();
     RPT_LAUNCHED("slice_probe_kernel");
     ProfScope prof7_("unpermute_kernel", s);
-    const uint64_t cap = rpt::tile_cap_for(slices);
+    const uint64_t cap = rpt::tile_cap_for(tile_slices);
     hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8, s,
-                       ws.pos, ws.passb, n, cap, ws.bits, ws.seg_counts);
+                       ws.pos, ws.passb, n_part, cap, part_bits, part_counts, dev_n_tiles);
     prof7_.end();
     RPT_LAUNCHED("unpermute_kernel");
+    if (buck) {
+      ProfScope prof8b_("bucket_unpermute_kernel", s);
+      hipLaunchKernelGGL(rpt::bucket_unpermute_kernel, dim3(static_cast<unsigned>(ceil_div(n, rpt::kTileRows))),
+                         dim3(rpt::kBucketUnpermuteThreads), 0, s, ws.pos1, ws.bits2, n, bucket_count(L) - 1,
+                         ws.counts_tm, ws.pre_tm, ws.bbase, ws.bits, ws.seg_counts);
+      prof8b_.end();
+      RPT_LAUNCHED("bucket_unpermute_kernel");
+    }
   }
   return RPT_OK;
 }
@@ -1588,12 +2160,12 @@ int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, u
   }
   if (!out_sel) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_sel");
   const int L = bf->log_num_blocks;
-  const bool part = resolve_strategy(bf->probe_strategy.load(), L) == RPT_PROBE_PARTITIONED;
-  const size_t need = workspace_layout(n, L, part, nullptr, nullptr);
+  const int strategy = resolve_strategy(bf->probe_strategy.load(), L, n);
+  const size_t need = workspace_layout(n, L, strategy, nullptr, nullptr);
   if (!workspace || workspace_bytes < need)
     return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   ProbeWorkspace ws;
-  workspace_layout(n, L, part, workspace, &ws);
+  workspace_layout(n, L, strategy, workspace, &ws);
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
   ProfScope prof8_("group_sum_kernel", s);

@@ -208,7 +208,10 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:72-74
   rpt_key_column kc = stage_key(ctx, chunks, cols, total);
-  check(rpt_bf_insert(bf_, &kc, total, ctx.stream()));
+  // large batches take the partitioned / bucketed insert (same filter bits)
+  const size_t ws_bytes = rpt_bf_insert_workspace_bytes(bf_, total);
+  if (ws_bytes) check(rpt_bf_insert_ws(bf_, &kc, total, ctx.dev(6, ws_bytes), ws_bytes, ctx.stream()));
+  else check(rpt_bf_insert(bf_, &kc, total, ctx.stream()));
   ctx.synchronize();  // the staging buffers are reused by the next call
 }
 
@@ -226,9 +229,7 @@ void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const D
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:63-65
   rpt_key_column kc = stage_key(ctx, chunks, cols, total);
-  rpt_bf_info info;
-  check(rpt_bf_get_info(bf_, &info));
-  const size_t ws_bytes = rpt_probe_workspace_bytes(total, info.log_num_blocks);
+  const size_t ws_bytes = rpt_bf_probe_workspace_bytes(bf_, total);  // for the strategy this batch runs
   void* ws = ctx.dev(2, ws_bytes);
   auto* d_sel = static_cast<uint32_t*>(ctx.dev(3, total * 4));
   auto* d_cnt = static_cast<uint64_t*>(ctx.dev(4, 8));

@@ -8,8 +8,10 @@ from ._lib import (  # noqa: F401
     LIB_PATH,
     RPT_INSERT_ATOMIC,
     RPT_INSERT_AUTO,
+    RPT_INSERT_BUCKETED,
     RPT_INSERT_PARTITIONED,
     RPT_PROBE_AUTO,
+    RPT_PROBE_BUCKETED,
     RPT_PROBE_GATHER,
     RPT_PROBE_LDS,
     RPT_PROBE_PARTITIONED,

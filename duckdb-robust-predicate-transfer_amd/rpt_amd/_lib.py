@@ -24,10 +24,12 @@ RPT_PROBE_AUTO = 0
 RPT_PROBE_GATHER = 1
 RPT_PROBE_LDS = 2
 RPT_PROBE_PARTITIONED = 3
+RPT_PROBE_BUCKETED = 4
 
 RPT_INSERT_AUTO = 0
 RPT_INSERT_ATOMIC = 1
 RPT_INSERT_PARTITIONED = 2
+RPT_INSERT_BUCKETED = 3
 
 RPT_KEY_I64 = 0
 RPT_KEY_I32 = 1
@@ -82,6 +84,9 @@ SIGNATURES = {
     "rpt_bf_set_probe_strategy": (c_int, [c_void_p, c_int]),
     "rpt_probe_strategy_supported": (c_int, [c_int, c_int]),
     "rpt_bf_probe_strategy": (c_int, [c_void_p]),
+    "rpt_bf_probe_strategy_for": (c_int, [c_void_p, c_uint64]),
+    "rpt_bf_insert_strategy_for": (c_int, [c_void_p, c_uint64]),
+    "rpt_bf_probe_workspace_bytes": (c_size_t, [c_void_p, c_uint64]),
     "rpt_bf_create": (c_int, [c_int, c_uint64, POINTER(c_void_p)]),
     "rpt_bf_create_log_blocks": (c_int, [c_int, c_int, POINTER(c_void_p)]),
     "rpt_bf_destroy": (c_int, [c_void_p]),
@@ -91,6 +96,7 @@ SIGNATURES = {
     "rpt_bf_clear": (c_int, [c_void_p, c_void_p]),
     "rpt_bf_insert": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p]),
     "rpt_insert_workspace_bytes": (c_size_t, [c_uint64, c_int]),
+    "rpt_bf_insert_workspace_bytes": (c_size_t, [c_void_p, c_uint64]),
     "rpt_bf_insert_ws": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p, c_size_t, c_void_p]),
     "rpt_bf_set_insert_strategy": (c_int, [c_void_p, c_int]),
     "rpt_bf_get_minmax": (c_int, [c_void_p, POINTER(c_int64), POINTER(c_int64), POINTER(c_int), c_void_p]),

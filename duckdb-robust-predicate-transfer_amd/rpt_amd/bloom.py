@@ -17,7 +17,6 @@ import numpy as np
 import torch
 
 from ._lib import (
-    RPT_INSERT_PARTITIONED,
     RPT_KEY_HASH,
     RPT_KEY_I32,
     RPT_KEY_I64,
@@ -87,11 +86,15 @@ class ProbeWorkspace:
         self.device = device
         self.buf: Optional[torch.Tensor] = None
 
-    def get(self, n: int, log_num_blocks: int) -> torch.Tensor:
-        need = int(load().rpt_probe_workspace_bytes(n, log_num_blocks))
+    def get_bytes(self, need: int) -> torch.Tensor:
         if self.buf is None or self.buf.numel() < need:
+            self.buf = None  # release before growing
             self.buf = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         return self.buf
+
+    def get(self, n: int, log_num_blocks: int) -> torch.Tensor:
+        """Enough for any strategy on a 2^log_num_blocks-block filter."""
+        return self.get_bytes(int(load().rpt_probe_workspace_bytes(n, log_num_blocks)))
 
 
 class BloomFilter:
@@ -170,7 +173,20 @@ class BloomFilter:
         check(self._lib.rpt_bf_set_probe_strategy(self._h, int(strategy)))
 
     def workspace_bytes(self, n: int) -> int:
-        return int(self._lib.rpt_probe_workspace_bytes(n, self.log_num_blocks))
+        """Probe workspace for n rows with the strategy this filter would run (AUTO resolved with n)."""
+        return int(self._lib.rpt_bf_probe_workspace_bytes(self._h, n))
+
+    def probe_strategy_for(self, n: int) -> int:
+        v = self._lib.rpt_bf_probe_strategy_for(self._h, n)
+        if v < 0:
+            check(-v)
+        return v
+
+    def insert_strategy_for(self, n: int) -> int:
+        v = self._lib.rpt_bf_insert_strategy_for(self._h, n)
+        if v < 0:
+            check(-v)
+        return v
 
     def set_has_data(self, v: bool) -> None:
         check(self._lib.rpt_bf_set_has_data(self._h, int(bool(v))))
@@ -178,14 +194,14 @@ class BloomFilter:
     # ---- build -----------------------------------------------------------------------------
     def insert(self, keys: torch.Tensor, *, key_type: Optional[int] = None, key_sel=None, validity=None,
                n: Optional[int] = None, stream=None, strategy: Optional[int] = None) -> None:
-        """PTBloomFilter::Insert. Large batches use the partitioned insert (workspace allocated here)
-        unless strategy=RPT_INSERT_ATOMIC; results are identical."""
+        """PTBloomFilter::Insert. Large batches use the partitioned / bucketed insert (workspace
+        allocated here) unless strategy=RPT_INSERT_ATOMIC; results are identical."""
         n = keys.numel() if (n is None and key_sel is None) else (key_sel.numel() if n is None else n)
         col = make_column(keys, key_type, key_sel, validity)
         if strategy is not None:
             check(self._lib.rpt_bf_set_insert_strategy(self._h, int(strategy)))
-        ws_bytes = int(self._lib.rpt_insert_workspace_bytes(n, self.log_num_blocks))
-        if ws_bytes and (strategy == RPT_INSERT_PARTITIONED or (strategy in (None, 0) and n >= (1 << 20))):
+        ws_bytes = int(self._lib.rpt_bf_insert_workspace_bytes(self._h, n))  # 0: atomic insert
+        if ws_bytes:
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device)
             check(self._lib.rpt_bf_insert_ws(self._h, ctypes.byref(col), n, ws.data_ptr(), ws_bytes,
                                              _stream(self.device, stream)))
@@ -234,7 +250,7 @@ class BloomFilter:
             out_sel = torch.empty(max(n, 1), dtype=torch.int32, device=self.device)
         if out_count is None:
             out_count = self._count
-        ws = workspace if workspace is not None else self._ws.get(n, self.log_num_blocks)
+        ws = workspace if workspace is not None else self._ws.get_bytes(self.workspace_bytes(n))
         check(self._lib.rpt_bf_probe(self._h, ctypes.byref(col), _ptr(row_sel), n, out_sel.data_ptr(),
                                      out_count.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(),
                                      _stream(self.device, stream)))

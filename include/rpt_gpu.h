@@ -50,19 +50,24 @@ typedef enum rpt_key_type {
 
 /* How a probe reaches the filter blocks (rpt_bf_set_probe_strategy). All give identical results. */
 typedef enum rpt_probe_strategy {
-  RPT_PROBE_AUTO = 0,       /* by filter size: LDS (<= 64 KiB), PARTITIONED (<= 16 MiB), else GATHER */
-  RPT_PROBE_GATHER = 1,     /* one random 8-byte gather per key from L2 / Infinity Cache / HBM */
-  RPT_PROBE_LDS = 2,        /* whole filter staged in each workgroup's LDS (filters <= 64 KiB) */
-  RPT_PROBE_PARTITIONED = 3 /* rows bucketed per 16 Ki-row tile by 64 KiB filter slice; each slice is
-                               probed from LDS, then row order is restored (filters 64 KiB..16 MiB) */
+  RPT_PROBE_AUTO = 0,        /* LDS (<= 64 KiB); for n >= blocks/8: PARTITIONED (<= 128 MiB), BUCKETED
+                                (<= 16 GiB); otherwise GATHER */
+  RPT_PROBE_GATHER = 1,      /* one random 8-byte gather per key from L2 / Infinity Cache / HBM */
+  RPT_PROBE_LDS = 2,         /* whole filter staged in each workgroup's LDS (filters <= 64 KiB) */
+  RPT_PROBE_PARTITIONED = 3, /* rows bucketed per 16 Ki-row tile by 128 KiB filter slice; each slice is
+                                probed from LDS, then row order is restored (filters 128 KiB..128 MiB) */
+  RPT_PROBE_BUCKETED = 4     /* two levels: rows first bucketed by 16 MiB filter region into contiguous
+                                hash arrays, then PARTITIONED per region (filters 32 MiB..16 GiB) */
 } rpt_probe_strategy;
 
 /* How an insert reaches the filter (rpt_bf_set_insert_strategy). All give identical filters. */
 typedef enum rpt_insert_strategy {
-  RPT_INSERT_AUTO = 0,       /* PARTITIONED for >= 2^20 rows when the filter supports it, else ATOMIC */
-  RPT_INSERT_ATOMIC = 1,     /* one device-scope 64-bit atomic OR per key */
-  RPT_INSERT_PARTITIONED = 2 /* rows bucketed by 128 KiB filter slice; each slice ORed in LDS, then
-                                merged with coalesced atomic ORs (filters 128 KiB..128 MiB) */
+  RPT_INSERT_AUTO = 0,        /* for >= 2^20 rows: PARTITIONED when the filter supports it, BUCKETED for
+                                 larger filters when n >= blocks/8; otherwise ATOMIC */
+  RPT_INSERT_ATOMIC = 1,      /* one device-scope 64-bit atomic OR per key */
+  RPT_INSERT_PARTITIONED = 2, /* rows bucketed by 128 KiB filter slice; each slice ORed in LDS, then
+                                 merged with coalesced atomic ORs (filters 128 KiB..128 MiB) */
+  RPT_INSERT_BUCKETED = 3     /* two levels as RPT_PROBE_BUCKETED (filters 32 MiB..16 GiB) */
 } rpt_insert_strategy;
 
 /* A hipStream_t, passed opaquely so this header needs no HIP include. NULL = the null stream. */
@@ -104,7 +109,8 @@ int rpt_bf_log_num_blocks_for_rows(uint64_t n_rows);
  * 1 iff actual_rows > 0 and actual_rows*8 > NextPow2(max(512, sized_for_rows*12)). */
 int rpt_bf_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows);
 /* Device workspace a probe of n rows against a 2^log_num_blocks-block filter needs, for any
- * strategy (bytes, 256-aligned). */
+ * strategy (bytes, 256-aligned). rpt_bf_probe_workspace_bytes: for the strategy a probe of n rows
+ * of this filter runs now (AUTO resolved), usually far less for very large filters. */
 size_t rpt_probe_workspace_bytes(uint64_t n_rows, int log_num_blocks);
 
 /* ---- lifecycle --------------------------------------------------------------------------- */
@@ -127,6 +133,10 @@ int rpt_bf_set_probe_strategy(rpt_bf* bf, int strategy);
 /* 1 if `strategy` can probe a 2^log_num_blocks-block filter, else 0. */
 int rpt_probe_strategy_supported(int strategy, int log_num_blocks);
 int rpt_bf_probe_strategy(const rpt_bf* bf);
+/* The strategy a probe / insert of n rows runs now (AUTO resolved with n), or a negative status. */
+int rpt_bf_probe_strategy_for(const rpt_bf* bf, uint64_t n_rows);
+int rpt_bf_insert_strategy_for(const rpt_bf* bf, uint64_t n_rows);
+size_t rpt_bf_probe_workspace_bytes(const rpt_bf* bf, uint64_t n_rows);
 /* Zero every block and clear has_data (stream-ordered). */
 int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
 
@@ -137,10 +147,13 @@ int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
  * no-op; otherwise has_data becomes 1. */
 int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_t stream);
 
-/* rpt_bf_insert with a caller workspace, which enables the partitioned insert for large batches
- * (same result, same thread-safety). workspace: rpt_insert_workspace_bytes(n, log_num_blocks)
- * bytes of device memory (0 when the filter only supports atomic inserts). */
+/* rpt_bf_insert with a caller workspace, which enables the partitioned / bucketed inserts for large
+ * batches (same result, same thread-safety). workspace: rpt_insert_workspace_bytes(n,
+ * log_num_blocks) bytes of device memory (the largest any insert strategy needs; 0 when the filter
+ * only supports atomic inserts), or rpt_bf_insert_workspace_bytes(bf, n) for the strategy this
+ * insert will run (0 = atomic, no workspace needed). */
 size_t rpt_insert_workspace_bytes(uint64_t n_rows, int log_num_blocks);
+size_t rpt_bf_insert_workspace_bytes(const rpt_bf* bf, uint64_t n_rows);
 int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* workspace, size_t workspace_bytes,
                      rpt_stream_t stream);
 int rpt_bf_set_insert_strategy(rpt_bf* bf, int strategy);

@@ -73,10 +73,13 @@ def test_workspace_size_grows_with_rows():
             assert b % 256 == 0 and b >= prev and b >= n // 8
             prev = b
     # the partitioned strategy (128 KiB..128 MiB filters) needs records (4 B) + row map (2 B) + pass bits
-    assert lib.rpt_probe_workspace_bytes(10**6, 21) >= 6 * 10**6 > lib.rpt_probe_workspace_bytes(10**6, 26)
+    assert lib.rpt_probe_workspace_bytes(10**6, 21) >= 6 * 10**6 > lib.rpt_probe_workspace_bytes(10**6, 32)
     # the partitioned insert needs records + run tables; filters it cannot partition need none
     assert lib.rpt_insert_workspace_bytes(10**6, 21) >= 4 * 10**6
-    assert lib.rpt_insert_workspace_bytes(10**6, 10) == 0 and lib.rpt_insert_workspace_bytes(10**6, 26) == 0
+    assert lib.rpt_insert_workspace_bytes(10**6, 10) == 0 and lib.rpt_insert_workspace_bytes(10**6, 32) == 0
+    # bucketed (filters > 128 MiB): level-1 hash arrays (8 B/row) + level-2 records (4 B/row)
+    assert lib.rpt_insert_workspace_bytes(10**6, 26) >= 12 * 10**6
+    assert lib.rpt_probe_workspace_bytes(10**6, 26) >= 18 * 10**6 > lib.rpt_probe_workspace_bytes(10**6, 32)
 
 
 def test_argument_errors_are_reported():
@@ -97,8 +100,11 @@ def test_strategy_support_rules():
         assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_GATHER, L) == 1
         assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_AUTO, L) == 1
         assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_LDS, L) == (L <= 13)
-    # partitioned: at least one full LDS slice, at most 256 slices
-    part = [L for L in range(0, 30) if lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_PARTITIONED, L)]
-    assert part == list(range(part[0], part[-1] + 1)) and part[0] in (13, 14) and len(part) >= 9
+    # partitioned: at least one full LDS slice, at most 1024 slices (128 KiB .. 128 MiB)
+    part = [L for L in range(0, 34) if lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_PARTITIONED, L)]
+    assert part == list(range(14, 25))
+    # bucketed: 2 .. 1024 buckets of 16 MiB (32 MiB .. 16 GiB), overlapping the partitioned range
+    buck = [L for L in range(0, 40) if lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_BUCKETED, L)]
+    assert buck == list(range(22, 32))
     assert lib.rpt_probe_strategy_supported(99, 10) == 0
     assert lib.rpt_synth_probe_keys(None, 1, 10, 0, 10, None) == _lib.RPT_ERR_INVALID_ARGUMENT

@@ -1,0 +1,143 @@
+"""Bucketed (two-level) strategy for filters > 128 MiB, on the HIP path vs the oracle and vs the other
+strategies. Bit-exact. Filters of 2^22..2^23 blocks (32/64 MiB) are used where the partitioned
+strategy also applies, so both can be compared on the same filter; 2^25 (256 MiB) exercises the AUTO
+choice at a size only the bucketed strategy routes."""
+import numpy as np
+import pytest
+import torch
+
+import golden_util as gu
+import rpt_oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+GATHER, PARTITIONED, BUCKETED = 1, 3, 4
+INS_ATOMIC, INS_PARTITIONED, INS_BUCKETED = 1, 2, 3
+
+
+@pytest.fixture(scope="module")
+def rpt():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test run without a visible GPU")
+    import rpt_amd
+
+    rpt_amd.load()
+    torch.cuda.set_device(0)
+    return rpt_amd
+
+
+def dev(a: np.ndarray) -> torch.Tensor:
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+
+
+def keys_of(dtype, n, seed):
+    rng = np.random.default_rng(seed)
+    info = np.iinfo(dtype)
+    return rng.integers(info.min, info.max, size=n, dtype=dtype, endpoint=True)
+
+
+def oracle_filter(log_nb, keys, **kw):
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, keys, **kw)
+    return w
+
+
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+@pytest.mark.parametrize("log_nb,n_build,n_probe", [(22, 300_000, 1), (22, 300_000, 100_003), (23, 2_000_000, 1_000_000)])
+def test_bucketed_probe_vs_oracle(rpt, dtype, log_nb, n_build, n_probe):
+    build = keys_of(dtype, n_build, log_nb)
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.insert(dev(build), strategy=INS_ATOMIC)
+    w = oracle_filter(log_nb, build)
+    assert np.array_equal(bf.export_words(), w)
+    rng = np.random.default_rng(n_probe)
+    probe = np.where(rng.random(n_probe) < 0.3, build[rng.integers(0, n_build, n_probe)], keys_of(dtype, n_probe, 5))
+    probe = probe.astype(dtype)
+    ref = orc.probe_keys(w, log_nb, probe)
+    for st in (BUCKETED, PARTITIONED, GATHER):
+        bf.probe_strategy = st
+        assert bf.probe_strategy_for(n_probe) == st
+        sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
+        assert np.array_equal(sel, ref), f"strategy {st}"
+
+
+def test_bucketed_probe_nulls_dictionary_rowsel(rpt):
+    log_nb, n = 22, 400_000
+    build = keys_of(np.int64, 200_000, 1)
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.insert(dev(build))
+    w = oracle_filter(log_nb, build)
+    rng = np.random.default_rng(2)
+    dict_keys = np.concatenate([build[:50_000], keys_of(np.int64, 50_000, 3)])
+    valid = rng.random(dict_keys.size) > 0.2
+    vw = gu.validity_words(valid)
+    key_sel = rng.integers(0, dict_keys.size, n).astype(np.uint32)
+    row_sel = np.sort(rng.choice(n, size=n // 3, replace=False)).astype(np.uint32)
+    # oracle: the dictionary vector sliced by row_sel
+    ref_rows = orc.probe_keys(w, log_nb, dict_keys, key_sel=np.ascontiguousarray(key_sel[row_sel]), validity=vw)
+    ref = row_sel[ref_rows]
+    bf.probe_strategy = BUCKETED
+    sel = bf.lookup_sel(dev(dict_keys), key_sel=dev(key_sel), validity=dev(vw), row_sel=dev(row_sel)).cpu().numpy()
+    assert np.array_equal(sel.astype(np.uint32), ref)
+
+
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+@pytest.mark.parametrize("n", [1, 5_000, 1_200_000])
+def test_bucketed_insert_vs_oracle(rpt, dtype, n):
+    log_nb = 22
+    keys = keys_of(dtype, n, n + 7)
+    valid = np.random.default_rng(n).random(n) > 0.05
+    vw = gu.validity_words(valid)
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.insert(dev(keys), validity=dev(vw), strategy=INS_BUCKETED)
+    assert np.array_equal(bf.export_words(), oracle_filter(log_nb, keys, validity=vw))
+    assert bf.minmax() == orc.minmax(keys, validity=vw)
+    # a second insert into the same filter ORs (thread-safe merge of the slices)
+    more = keys_of(dtype, 1000, 99)
+    bf.insert(dev(more), strategy=INS_BUCKETED)
+    w = oracle_filter(log_nb, keys, validity=vw)
+    orc.insert_keys(w, log_nb, more)
+    assert np.array_equal(bf.export_words(), w)
+
+
+def test_auto_routes_large_filters(rpt):
+    """2^25 blocks (256 MiB): AUTO picks the bucketed insert / probe for large batches and the
+    atomic insert / gather for small ones; all give the oracle's bits and survivors."""
+    log_nb = 25
+    n_build = 5_000_000
+    build = keys_of(np.int64, n_build, 11)
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    assert bf.insert_strategy_for(n_build) == INS_BUCKETED and bf.insert_strategy_for(1000) == INS_ATOMIC
+    assert bf.probe_strategy_for(10**7) == BUCKETED and bf.probe_strategy_for(10**5) == GATHER
+    bf.insert(dev(build))
+    w = oracle_filter(log_nb, build)
+    assert np.array_equal(bf.export_words(), w)
+    rng = np.random.default_rng(12)
+    n_probe = 6_000_000
+    probe = np.where(rng.random(n_probe) < 0.1, build[rng.integers(0, n_build, n_probe)], keys_of(np.int64, n_probe, 13))
+    ref = orc.probe_keys(w, log_nb, probe)
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
+    assert np.array_equal(sel, ref)
+    small = bf.lookup_sel(dev(probe[:100_000])).cpu().numpy().astype(np.uint32)
+    assert np.array_equal(small, ref[ref < 100_000])
+
+
+def test_bucketed_skewed_keys(rpt):
+    """Every key in one bucket (and one slice): the level-2 array is a single padded bucket."""
+    log_nb = 22
+    base = keys_of(np.int64, 20_000, 21)
+    h = orc.hash_keys(base)
+    same = base[(h >> np.uint64(37)) & np.uint64(1) == 0][:5000]  # all keys of bucket 0
+    keys = np.repeat(same, 200)  # 1e6 rows, heavy duplicates
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.insert(dev(keys), strategy=INS_BUCKETED)
+    w = oracle_filter(log_nb, keys)
+    assert np.array_equal(bf.export_words(), w)
+    bf.probe_strategy = BUCKETED
+    probe = np.concatenate([keys, base])
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
