@@ -69,7 +69,7 @@ static_assert(kRowsPerThread == 8 || kRowsPerThread == 16 || kRowsPerThread == 3
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
 constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
 #ifndef RPT_SLICE_UNROLL
-#define RPT_SLICE_UNROLL 8                             // 256-record groups in flight per wave
+#define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
 #endif
 #ifndef RPT_PARTITION_MIN_WAVES
 #define RPT_PARTITION_MIN_WAVES 8                      // 2 partition workgroups per CU (64 VGPRs)
@@ -482,8 +482,9 @@ struct SliceWork {
   uint32_t slice, run_row;
   uint64_t t_lo, t_hi;
 };
-__device__ __forceinline__ SliceWork slice_work(uint32_t splits, uint64_t n_tiles, const uint32_t* bucket_tiles) {
-  const uint32_t slice = blockIdx.x / splits, part = blockIdx.x % splits;
+__device__ __forceinline__ SliceWork slice_work(uint32_t item, uint32_t splits, uint64_t n_tiles,
+                                                const uint32_t* bucket_tiles) {
+  const uint32_t slice = item / splits, part = item % splits;
   uint64_t lo = 0, cnt = n_tiles;
   uint32_t row = slice;
   if (bucket_tiles != nullptr) {
@@ -495,37 +496,30 @@ __device__ __forceinline__ SliceWork slice_work(uint32_t splits, uint64_t n_tile
   return SliceWork{slice, row, lo + cnt * part / splits, lo + cnt * (part + 1) / splits};
 }
 
-__global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64_t* __restrict__ words,
-                                                                   uint32_t splits, uint64_t n_tiles,
-                                                                   const uint32_t* __restrict__ recs,
-                                                                   const uint32_t* __restrict__ runs,
-                                                                   uint8_t* __restrict__ passbits,
-                                                                   uint32_t tile_slices,
-                                                                   const uint32_t* __restrict__ bucket_tiles) {
+// Probe the runs of tiles [sw.t_lo, sw.t_hi) of one slice held in LDS (see above).
+// Tiles per wave batch: 64 (one run per lane), or fewer so that all kSliceThreads/64 waves get work.
+__device__ __forceinline__ uint32_t batch_tiles(uint64_t n_t) {
+  constexpr uint64_t kWaves = kSliceThreads / 64;
+  return static_cast<uint32_t>(n_t >= 64 * kWaves ? 64 : (n_t + kWaves - 1) / kWaves);
+}
+
+__device__ __forceinline__ void probe_slice_runs(const uint64_t* s_slice, const uint64_t* s_rmasks, const SliceWork& sw,
+                                                 uint64_t n_tiles, const uint32_t* __restrict__ recs,
+                                                 const uint32_t* __restrict__ runs, uint8_t* __restrict__ passbits,
+                                                 uint32_t tile_cap) {
   constexpr int kUnroll = RPT_SLICE_UNROLL;
-  // one LDS array, table first: the slice's base offset folds into the ds_read immediate
-  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
-  uint64_t* const s_rmasks = s_lds;
-  uint64_t* const s_slice = s_lds + kRotMasks;
-  const SliceWork sw = slice_work(splits, n_tiles, bucket_tiles);
-  const uint32_t slice = sw.slice;
-  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
-  if (t_lo >= t_hi) return;  // no rows reach this slice: skip its LDS fill (uniform)
-  {
-    const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(slice) * kSliceWords);
-    u64x2* dst = reinterpret_cast<u64x2*>(s_slice);
-    for (uint32_t i = threadIdx.x; i < kSliceWords / 2; i += kSliceThreads) dst[i] = src[i];
-  }
-  fill_rot_mask_table(s_rmasks);
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
+  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
-  const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(tile_slices));
-  uint32_t info_next = (t_lo + wave * 64 + lane < t_hi) ? my_runs[t_lo + wave * 64 + lane] : 0u;
-  for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
+  // a wave walks batches of bt <= 64 consecutive tiles (one run per lane); few tiles per slice (the
+  // bucketed strategy) are spread over all waves in smaller batches
+  const uint32_t bt = batch_tiles(t_hi - t_lo);
+  const uint32_t my = lane < bt ? lane : ~0u >> 1;  // lanes >= bt hold no run
+  uint32_t info_next = (t_lo + wave * bt + my < t_hi) ? my_runs[t_lo + wave * bt + my] : 0u;
+  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
     const uint32_t info = info_next;  // the next batch's runs are fetched while this one is probed
-    info_next = (tb + kWaves * 64 + lane < t_hi) ? my_runs[tb + kWaves * 64 + lane] : 0u;
+    info_next = (tb + kWaves * bt + my < t_hi) ? my_runs[tb + kWaves * bt + my] : 0u;
     const uint32_t cnt = pad_run(info & 0xFFFFu);  // padded run length (multiple of kRunPad)
     const uint32_t start = lane * tile_cap + (info >> 16);
     const uint32_t* brecs = recs + tb * tile_cap;  // uniform
@@ -570,6 +564,63 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   }
 }
 
+// First work item >= item (stepping by gridDim.x) that has tiles; n_items if none.
+__device__ __forceinline__ uint32_t next_item(uint32_t item, uint32_t n_items, uint32_t splits, uint64_t n_tiles,
+                                              const uint32_t* bucket_tiles, SliceWork& sw) {
+  for (; item < n_items; item += gridDim.x) {
+    sw = slice_work(item, splits, n_tiles, bucket_tiles);
+    if (sw.t_lo < sw.t_hi) break;
+  }
+  return item;
+}
+
+// Work items (slice, split) are walked by a resident grid; when a workgroup has several (filters with
+// more slices than the chip has CUs: the bucketed strategy), the next item's slice is fetched into
+// registers (128 B per thread) while the current one is probed, then stored to LDS.
+__global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64_t* __restrict__ words,
+                                                                   uint32_t splits, uint64_t n_tiles,
+                                                                   const uint32_t* __restrict__ recs,
+                                                                   const uint32_t* __restrict__ runs,
+                                                                   uint8_t* __restrict__ passbits,
+                                                                   uint32_t tile_slices,
+                                                                   const uint32_t* __restrict__ bucket_tiles,
+                                                                   uint32_t n_items) {
+  // one LDS array, table first: the slice's base offset folds into the ds_read immediate
+  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
+  uint64_t* const s_rmasks = s_lds;
+  uint64_t* const s_slice = s_lds + kRotMasks;
+  u64x2* const s_slice2 = reinterpret_cast<u64x2*>(s_slice);
+  constexpr uint32_t kPre = kSliceWords / 2 / kSliceThreads;  // 16-B pieces of a slice per thread
+  SliceWork cur;
+  uint32_t item = next_item(blockIdx.x, n_items, splits, n_tiles, bucket_tiles, cur);
+  if (item >= n_items) return;  // uniform
+  {
+    const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(cur.slice) * kSliceWords);
+#pragma unroll
+    for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = src[threadIdx.x + i * kSliceThreads];
+  }
+  fill_rot_mask_table(s_rmasks);
+  const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(tile_slices));
+  while (true) {
+    __syncthreads();
+    SliceWork nxt;
+    const uint32_t nitem = next_item(item + gridDim.x, n_items, splits, n_tiles, bucket_tiles, nxt);
+    u64x2 pre[kPre];
+    if (nitem < n_items) {
+      const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(nxt.slice) * kSliceWords);
+#pragma unroll
+      for (uint32_t i = 0; i < kPre; i++) pre[i] = src[threadIdx.x + i * kSliceThreads];
+    }
+    probe_slice_runs(s_slice, s_rmasks, cur, n_tiles, recs, runs, passbits, tile_cap);
+    if (nitem >= n_items) break;
+    __syncthreads();  // every wave is done with this slice
+#pragma unroll
+    for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = pre[i];
+    item = nitem;
+    cur = nxt;
+  }
+}
+
 // ---- partitioned build: OR each slice's records into an LDS copy, then merge into the filter ----
 // Same flattened run walk as slice_probe_kernel. The slice starts from zero in LDS (ds_or_b64 per
 // record) and is merged into the filter with coalesced 64-bit device-scope atomic ORs of its non-zero
@@ -584,7 +635,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
   uint64_t* const s_rmasks = s_lds;
   uint64_t* const s_slice = s_lds + kRotMasks;
-  const SliceWork sw = slice_work(splits, n_tiles, bucket_tiles);
+  const SliceWork sw = slice_work(blockIdx.x, splits, n_tiles, bucket_tiles);
   const uint32_t slice = sw.slice;
   const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
   if (t_lo >= t_hi) return;  // no rows reach this slice (uniform)
@@ -595,8 +646,9 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   constexpr uint32_t kWaves = kSliceThreads / 64;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
   const uint64_t tile_cap = tile_cap_for(tile_slices);
-  for (uint64_t tb = t_lo + wave * 64; tb < t_hi; tb += kWaves * 64) {
-    const uint32_t info = (tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
+  const uint32_t bt = batch_tiles(t_hi - t_lo);  // as slice_probe_kernel
+  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
+    const uint32_t info = (lane < bt && tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
     const uint32_t real = info & 0xFFFFu;      // records of the run
     const uint32_t cnt = pad_run(real);          // padded length (k-space)
     const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
@@ -805,10 +857,17 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
                                                                       uint16_t* __restrict__ pos_out) {
   extern __shared__ uint64_t s_h[];  // kTileRows hashes, bucket-sorted
   __shared__ uint32_t s_start[kMaxBuckets], s_cur[kMaxBuckets];
+  __shared__ uint64_t s_dst[kMaxBuckets];  // where each bucket's run goes in the level-2 array
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t nb = bucket_mask + 1;
-  const uint64_t tile = blockIdx.x, tile_base = tile * kTileRows;
+  // Workgroups go round-robin to the 8 XCDs; give each XCD a contiguous range of tiles, so the runs of
+  // neighbouring tiles (adjacent in each bucket's array) are written through the same L2 and leave it
+  // as whole lines.
+  const uint32_t per_xcd = gridDim.x / 8, xcd = blockIdx.x % 8;
+  const uint64_t tile = blockIdx.x < per_xcd * 8 ? static_cast<uint64_t>(xcd) * per_xcd + blockIdx.x / 8 : blockIdx.x;
+  const uint64_t tile_base = tile * kTileRows;
   const uint32_t* cnt = counts_tm + tile * nb;
+  for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_dst[i] = base[i] + pre_tm[tile * nb + i];
   if (wave == 0) {  // exclusive scan of this tile's bucket counts, kMaxBuckets / 64 per lane
     constexpr int kPer = kMaxBuckets / 64;
     uint32_t c[kPer], t = 0;
@@ -850,10 +909,9 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
     }
   }
   __syncthreads();
-  for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {
-    const uint32_t c = cnt[b];
-    if (c == 0) continue;
-    uint64_t* dst = hashes + base[b] + pre_tm[tile * nb + b];
+  for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {  // LDS only: no global latency in the chain
+    const uint32_t c = s_cur[b] - s_start[b];
+    uint64_t* dst = hashes + s_dst[b];
     const uint64_t* src = s_h + s_start[b];
     for (uint32_t i = lane; i < c; i += 64) dst[i] = src[i];
   }
@@ -2123,11 +2181,13 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     // splits than tiles
     const uint64_t slice_lds = rpt::kSliceWords * 8 + 8ULL * rpt::kRotMasks;
     const uint64_t per_cu = std::max<uint64_t>(1, (160ULL << 10) / slice_lds);
-    const uint32_t splits = static_cast<uint32_t>(std::max<uint64_t>(
-        1, std::min<uint64_t>(n_tiles, (static_cast<uint64_t>(cus) * per_cu) / grid_slices)));
+    const uint64_t resident = static_cast<uint64_t>(cus) * per_cu;
+    const uint32_t splits = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident / grid_slices)));
+    const uint32_t n_items = grid_slices * splits;
     ProfScope prof6_("slice_probe_kernel", s);
-    hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(grid_slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words,
-                       splits, n_tiles, ws.recs, ws.runs, ws.passb, tile_slices, bucket_tiles);
+    hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(n_items, resident))),
+                       dim3(rpt::kSliceThreads), 0, s, bf->words, splits, n_tiles, ws.recs, ws.runs, ws.passb, tile_slices,
+                       bucket_tiles, n_items);
     prof6_.end();
     RPT_LAUNCHED("slice_probe_kernel");
     ProfScope prof7_("unpermute_kernel", s);
