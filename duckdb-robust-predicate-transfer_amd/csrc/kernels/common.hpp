@@ -1,0 +1,184 @@
+// common.hpp — launch constants, key-column access (load_hashes) and min/max helpers.
+// Part of librpt_gpu.so: included by rpt_gpu.hip (one translation unit: kernels and their launches
+// stay together without relocatable device code).
+#pragma once
+
+namespace rpt {
+
+constexpr int kBlockThreads = 256;
+constexpr int kWavesPerBlock = kBlockThreads / 64;
+constexpr uint64_t kSegRows = 512;                 // rows per wave segment (8 per lane)
+constexpr uint64_t kWordsPerSeg = kSegRows / 64;   // result-bit words per segment
+constexpr uint64_t kGroupSegs = 256;               // segments per scan group (one compaction workgroup)
+constexpr int kBlocksPerCU = 8;
+
+// Partitioned ("routed") probe: the filter is cut into 128 KiB slices that fit in LDS; probe rows are
+// bucketed by slice per 16 Ki-row tile so that every filter access is an LDS read.
+#ifndef RPT_SLICE_LOG
+#define RPT_SLICE_LOG 14
+#endif
+constexpr int kSliceLog = RPT_SLICE_LOG;               // 2^13 blocks = 64 KiB (or 2^14 = 128 KiB) per slice
+constexpr uint64_t kSliceWords = 1ULL << kSliceLog;
+constexpr int kMaxSliceCount = 1024;                   // P <= 1024 slices (filters <= 128 MiB at 128 KiB slices)
+#ifndef RPT_TILE_ROWS
+#define RPT_TILE_ROWS 16384
+#endif
+constexpr uint64_t kTileRows = RPT_TILE_ROWS;          // rows per partition tile (8 or 16 per thread)
+// Runs are padded to kRunPad records so a lane owns kRunPad aligned records of one run and its pass
+// results form one byte of bits. Tile capacity is a multiple of 128 so the tile's pass bits are
+// whole 16-byte vectors.
+constexpr uint32_t kRunPad = 8;
+__host__ __device__ constexpr uint32_t pad_run(uint32_t c) { return (c + kRunPad - 1) & ~(kRunPad - 1); }
+__host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices) {
+  return (kTileRows + static_cast<uint64_t>(kRunPad) * n_slices + 127) & ~127ULL;
+}
+// Bucketed strategy (filters > 128 MiB): 16 MiB buckets of 128 slices, at most 1024 buckets (16 GiB).
+constexpr int kBucketSliceLog = 7;
+constexpr uint32_t kBucketSlices = 1u << kBucketSliceLog;
+constexpr uint32_t kMaxBuckets = 1024;
+constexpr int kTileThreads = 1024;                     // 16 waves
+constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
+constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave in the partition kernel
+static_assert(kRowsPerThread == 8 || kRowsPerThread == 16 || kRowsPerThread == 32, "tile = 8, 16 or 32 Ki rows");
+constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
+constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
+#ifndef RPT_SLICE_UNROLL
+#define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
+#endif
+#ifndef RPT_PARTITION_MIN_WAVES
+#define RPT_PARTITION_MIN_WAVES 8                      // 2 partition workgroups per CU (64 VGPRs)
+#endif
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct KeyArgs {
+  const void* keys;
+  const uint32_t* key_sel;
+  const uint64_t* validity;
+  const uint32_t* row_sel;
+};
+
+__device__ __forceinline__ bool valid_at(const uint64_t* validity, uint64_t idx) {
+  return validity == nullptr || ((validity[idx >> 6] >> (idx & 63)) & 1ULL);
+}
+
+// Hashes of the 8 rows a lane owns in a segment.
+//  DENSE   (flat column, no selections, 16-B aligned): row(c, e) = base + c*64*V + lane*V + e,
+//          one 16-byte load per (c): fully coalesced 1 KiB per wave instruction.
+//  GENERAL (dictionary key_sel and/or row_sel):        row(c) = base + c*64 + lane.
+// MM: also fold the valid (non-NULL, in-range) key values into mm[0] = min, mm[1] = max (the build's
+// min/max dynamic filter, physical_create_bf.cpp:82-119, fused into the key read).
+template <int K, bool DENSE, bool MM = false>
+__device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uint64_t n, uint32_t lane,
+                                            uint64_t (&h)[8], bool (&ok)[8], int64_t* mm = nullptr) {
+  using Tr = KeyTraits<K>;
+  using T = typename Tr::T;
+  // rows left from `base` (uniform), so per-row bounds checks are 32-bit and addresses are
+  // uniform-base + 32-bit lane offset
+  const uint32_t rem = n > base ? static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows) : 0u;
+  if constexpr (DENSE) {
+    constexpr int V = Tr::kVec;
+    const T* kb = static_cast<const T*>(a.keys) + base;
+    const uint64_t* vb = a.validity ? a.validity + (base >> 6) : nullptr;  // base is a multiple of 512
+#pragma unroll
+    for (int c = 0; c < 8 / V; c++) {
+      const uint32_t off = static_cast<uint32_t>(c * 64 * V) + lane * V;
+      T v[V];
+      if (off + V <= rem) {
+        if constexpr (V == 2) {
+          const u64x2 x = *reinterpret_cast<const u64x2*>(kb + off);
+          v[0] = static_cast<T>(x[0]);
+          v[1] = static_cast<T>(x[1]);
+        } else {
+          const u32x4 x = *reinterpret_cast<const u32x4*>(kb + off);
+#pragma unroll
+          for (int e = 0; e < V; e++) v[e] = static_cast<T>(x[e]);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; e++) v[e] = (off + e < rem) ? kb[off + e] : T(0);
+      }
+      // validity bits of this lane's V rows, shifted down to bits 0..V-1 (V | 64: one word)
+      uint32_t vbits = (1u << V) - 1;
+      if (K != kKeyHash && vb != nullptr && off < rem) vbits = static_cast<uint32_t>(vb[off >> 6] >> (off & 63));
+#pragma unroll
+      for (int e = 0; e < V; e++) {
+        ok[c * V + e] = off + e < rem;
+        uint64_t hv = Tr::hash(v[e]);
+        if (K != kKeyHash && !((vbits >> e) & 1u)) hv = kNullHash;
+        h[c * V + e] = hv;
+        if constexpr (MM && K != kKeyHash) {
+          if (off + e < rem && ((vbits >> e) & 1u)) {
+            mm[0] = min(mm[0], static_cast<int64_t>(v[e]));
+            mm[1] = max(mm[1], static_cast<int64_t>(v[e]));
+          }
+        }
+      }
+    }
+  } else {
+    const T* keys = static_cast<const T*>(a.keys);
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint32_t off = static_cast<uint32_t>(c * 64) + lane;
+      ok[c] = off < rem;
+      uint64_t hv = 0;
+      if (ok[c]) {
+        const uint64_t i = base + off;
+        const uint64_t r = a.row_sel ? a.row_sel[i] : i;
+        const uint64_t k = a.key_sel ? a.key_sel[r] : r;
+        const T kv = keys[k];
+        hv = Tr::hash(kv);
+        const bool valid = valid_at(a.validity, k);
+        if (K != kKeyHash && !valid) hv = kNullHash;
+        if constexpr (MM && K != kKeyHash) {
+          if (valid) {
+            mm[0] = min(mm[0], static_cast<int64_t>(kv));
+            mm[1] = max(mm[1], static_cast<int64_t>(kv));
+          }
+        }
+      }
+      h[c] = hv;
+    }
+  }
+}
+
+// Row offset inside a 512-row segment of the j-th hash load_hashes<K, DENSE> returns for `lane`.
+template <int K, bool DENSE>
+__device__ __forceinline__ uint32_t seg_row(int j, uint32_t lane) {
+  if constexpr (DENSE) {
+    constexpr int V = KeyTraits<K>::kVec;
+    return static_cast<uint32_t>((j / V) * 64 * V) + lane * V + static_cast<uint32_t>(j % V);
+  } else {
+    return static_cast<uint32_t>(j * 64) + lane;
+  }
+}
+
+// Wave-wide (min, max) of per-lane values, returned wave-uniform (scalar registers).
+__device__ __forceinline__ void wave_minmax(int64_t& mn, int64_t& mx) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    mn = min(mn, static_cast<int64_t>(__shfl_xor(static_cast<long long>(mn), d, 64)));
+    mx = max(mx, static_cast<int64_t>(__shfl_xor(static_cast<long long>(mx), d, 64)));
+  }
+  auto uniform = [](int64_t v) {
+    const uint64_t u = static_cast<uint64_t>(v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u));
+    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u >> 32));
+    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  mn = uniform(mn);
+  mx = uniform(mx);
+}
+// Fold a wave's uniform (min, max) into stats[0..1] (int64, device). A wave whose values cannot lower
+// the min or raise the max — the common case once a few waves have reported — skips the atomics.
+__device__ __forceinline__ void publish_minmax(int64_t mn, int64_t mx, int64_t* stats) {
+  if ((threadIdx.x & 63) == 0) {
+    if (mn < __hip_atomic_load(stats, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      __hip_atomic_fetch_min(stats, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (mx > __hip_atomic_load(stats + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      __hip_atomic_fetch_max(stats + 1, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+constexpr int64_t kMinInit = INT64_MAX, kMaxInit = INT64_MIN;  // "no value yet"
+}  // namespace rpt

@@ -1,0 +1,113 @@
+// misc.hpp — atomic insert, hashing, OR merge, popcount, synthetic workload generators.
+// Part of librpt_gpu.so: included by rpt_gpu.hip (one translation unit: kernels and their launches
+// stay together without relocatable device code).
+#pragma once
+
+namespace rpt {
+
+// ---- k2: insert ----------------------------------------------------------------------------------
+template <int K, bool DENSE>
+__global__ __launch_bounds__(kBlockThreads) void insert_kernel(uint64_t* __restrict__ words, uint64_t block_mask,
+                                                              KeyArgs a, uint64_t n, uint64_t n_segs,
+                                                              int64_t* __restrict__ stats) {
+  constexpr bool MM = K != kKeyHash;
+  __shared__ uint64_t s_masks[kNumMasks];
+  fill_mask_table(s_masks);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
+  int64_t mm[2] = {kMinInit, kMaxInit};
+  for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6); seg < n_segs;
+       seg += total_waves) {
+    uint64_t h[8];
+    bool ok[8];
+    load_hashes<K, DENSE, MM>(a, seg * kSegRows, n, lane, h, ok, mm);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      if (ok[j]) {
+        __hip_atomic_fetch_or(words + block_of(h[j], block_mask), mask_of(s_masks, h[j]), __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  if constexpr (MM) {
+    wave_minmax(mm[0], mm[1]);
+    publish_minmax(mm[0], mm[1], stats);
+  }
+}
+
+// ---- hashing only (parity / debugging) ---------------------------------------------------------
+template <int K, bool COMBINE>
+__global__ __launch_bounds__(kBlockThreads) void hash_kernel(KeyArgs a, uint64_t n, uint64_t* __restrict__ out) {
+  using Tr = KeyTraits<K>;
+  const typename Tr::T* keys = static_cast<const typename Tr::T*>(a.keys);
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t k = a.key_sel ? a.key_sel[i] : i;
+    uint64_t hv = Tr::hash(keys[k]);
+    if (K != kKeyHash && !valid_at(a.validity, k)) hv = kNullHash;
+    out[i] = COMBINE ? combine_hash(out[i], hv) : hv;
+  }
+}
+
+// ---- k4: OR merge --------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlockThreads) void or_slices_kernel(uint64_t* __restrict__ dst,
+                                                                 const uint64_t* __restrict__ srcs, uint32_t k,
+                                                                 uint64_t n_words, int accumulate) {
+  const uint64_t n_pairs = n_words / 2;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_pairs; i += stride) {
+    u64x2 acc = accumulate ? reinterpret_cast<const u64x2*>(dst)[i] : u64x2{0, 0};
+    for (uint32_t s = 0; s < k; s++) acc |= reinterpret_cast<const u64x2*>(srcs + s * n_words)[i];
+    reinterpret_cast<u64x2*>(dst)[i] = acc;
+  }
+  if ((n_words & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+    uint64_t acc = accumulate ? dst[n_words - 1] : 0ULL;
+    for (uint32_t s = 0; s < k; s++) acc |= srcs[s * n_words + n_words - 1];
+    dst[n_words - 1] = acc;
+  }
+}
+
+// ---- popcount ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlockThreads) void popcount_kernel(const uint64_t* __restrict__ w, uint64_t n_words,
+                                                                unsigned long long* __restrict__ out) {
+  __shared__ uint32_t s_part[kWavesPerBlock];
+  uint32_t s = 0;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_words;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    s += __popcll(w[i]);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    atomicAdd(out, static_cast<unsigned long long>(s_part[0]) + s_part[1] + s_part[2] + s_part[3]);
+  }
+}
+
+// ---- synthetic workload (bench / tests) ----------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint64_t sm64(uint64_t seed, uint64_t i) { return mix64(seed + (i + 1) * 0x9e3779b97f4a7c15ULL); }
+
+__global__ __launch_bounds__(kBlockThreads) void synth_build_kernel(int64_t* __restrict__ out, uint64_t start,
+                                                                   uint64_t n) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    out[i] = static_cast<int64_t>(sm64(RPT_SYNTH_SEED_BUILD, start + i));
+}
+
+__global__ __launch_bounds__(kBlockThreads) void synth_probe_kernel(int64_t* __restrict__ out, uint64_t n_build,
+                                                                   uint32_t p_permille, uint64_t start, uint64_t n) {
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t r = start + i;
+    const uint64_t u = sm64(RPT_SYNTH_SEED_PROBE_SEL, r);
+    out[i] = (n_build > 0 && (u % 1000) < p_permille)
+                 ? static_cast<int64_t>(sm64(RPT_SYNTH_SEED_BUILD, (u >> 20) % n_build))
+                 : static_cast<int64_t>(sm64(RPT_SYNTH_SEED_PROBE_MISS, r));
+  }
+}
+}  // namespace rpt

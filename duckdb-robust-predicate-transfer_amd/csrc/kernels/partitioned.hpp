@@ -1,0 +1,476 @@
+// partitioned.hpp — slice records, partition / transpose / slice probe / slice insert / unpermute.
+// Part of librpt_gpu.so: included by rpt_gpu.hip (one translation unit: kernels and their launches
+// stay together without relocatable device code).
+#pragma once
+
+namespace rpt {
+
+// ---- slice records -------------------------------------------------------------------------------
+// A record carries the 30 hash bits a filter slice needs, laid out for the slice kernels' 32-bit ALU:
+//   [0..4]   rotation & 31  (v_alignbit reads the low 5 bits of its shift operand: no extract)
+//   [5..15]  index into the 2048-entry rotated-mask table: mask id (h & 1023) | rotation bit 5 << 10
+//   [16..29] block within the slice ([30..31]: slice bits, masked off)
+// Table entry (id, r5) = ROTL64(mask(id), 32 * r5). With r = 32 * r5 + t:
+//   (w & ROTL(mask, r)) == ROTL(mask, r)  <=>  (ROTR(w, t) & entry) == entry
+// and ROTR(w, t) for t < 32 is two v_alignbit_b32 — no 64-bit shifts, no rotation of the mask.
+__device__ __forceinline__ uint32_t slice_record(uint64_t h) {
+  const uint32_t x = static_cast<uint32_t>(h);
+  return ((x >> kLogNumMasks) & 31u) | ((x & (kNumMasks - 1)) << 5) | (x & 0xFFFF8000u);
+}
+constexpr uint32_t kRotMasks = 2 * kNumMasks;
+__device__ __forceinline__ void fill_rot_mask_table(uint64_t* s_rmasks) {
+  for (int i = threadIdx.x; i < static_cast<int>(kRotMasks); i += blockDim.x) {
+    const int id = i & (kNumMasks - 1), w = id >> 6, s = id & 63;
+    const uint64_t lo = kMaskBits[w], hi = kMaskBits[w + 1];
+    const uint64_t m = ((lo >> s) | ((hi << 1) << (63 - s))) & kFullMask;
+    s_rmasks[i] = (i >> kLogNumMasks) ? rotl64(m, 32) : m;
+  }
+}
+__device__ __forceinline__ uint64_t rot_entry(const uint64_t* s_rmasks, uint32_t rec) {
+  return s_rmasks[(rec >> 5) & (kRotMasks - 1)];
+}
+__device__ __forceinline__ uint32_t rec_word(uint32_t rec) { return (rec >> 16) & (kSliceWords - 1); }
+// the filter mask of a record: ROTL(entry, t)
+__device__ __forceinline__ uint64_t rec_mask(const uint64_t* s_rmasks, uint32_t rec) {
+  return rotl64(rot_entry(s_rmasks, rec), rec & 31u);
+}
+__device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_t* s_rmasks, uint32_t rec) {
+  const uint64_t e = rot_entry(s_rmasks, rec);
+  const uint64_t w = s_slice[rec_word(rec)];
+  const uint32_t wl = static_cast<uint32_t>(w), wh = static_cast<uint32_t>(w >> 32);
+  const uint32_t xl = __builtin_amdgcn_alignbit(wh, wl, rec), xh = __builtin_amdgcn_alignbit(wl, wh, rec);
+  return ((~xl & static_cast<uint32_t>(e)) | (~xh & static_cast<uint32_t>(e >> 32))) == 0u;
+}
+
+// ---- partitioned probe, A: bucket a 16 Ki-row tile by filter slice --------------------------------
+// Row r of the tile gets record slice_record(hash) stored at position pos(r) of the tile's
+// slice-sorted record array (runs padded to kRunPad records); pos(r) is
+// written per row (u16) so the unpermute step can restore row order. Per tile the padded runs
+// (start << 16 | length) are written tile-major (one coalesced 4*P-byte row); runs_transpose_kernel
+// turns them slice-major for the slice kernel. Two passes over the rows held in registers: count per
+// slice (LDS atomics), scan, then claim positions with an LDS cursor per slice and scatter.
+// Dynamic LDS: tile_cap record slots, then the per-slice count and cursor arrays.
+template <int K, bool DENSE, bool MM>
+__global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(
+    KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
+    uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm, int64_t* __restrict__ stats,
+    const uint32_t* __restrict__ dev_n_tiles) {
+  // dev_n_tiles (bucketed strategy): the tile count is only known on the device; the grid is an upper
+  // bound and surplus workgroups leave (their run-table rows are never read).
+  if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;
+  extern __shared__ uint32_t s_dyn[];
+  const uint64_t tile_cap = tile_cap_for(slice_mask + 1);
+  uint32_t* s_rec = s_dyn;
+  uint32_t* s_cnt = s_dyn + tile_cap;                  // rows per slice in this tile
+  uint32_t* s_cur = s_dyn + tile_cap + slice_mask + 1;  // run start, then scatter cursor (start + count)
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t n_slices = slice_mask + 1;
+  {  // one tile per workgroup (no persistent loop: keeps per-lane invariants out of registers)
+    const uint64_t tile = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads) s_cnt[i] = 0;
+    __syncthreads();
+    const uint64_t tile_base = tile * kTileRows;
+    // pass 1: hash, stage the record at its row position in LDS, count rows per slice; only the 16-bit
+    // slice ids stay in registers (2 per word).
+    static_assert(kMaxSliceCount <= 65536, "slice ids are packed as 16 bits");
+    uint32_t sl2[kRowsPerThread / 2] = {};
+    int64_t wmn = kMinInit, wmx = kMaxInit;  // wave-uniform: the key min/max stays out of VGPRs
+#pragma unroll
+    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
+      const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+      uint64_t hh[8];
+      bool oo[8];
+      int64_t mm[2] = {kMinInit, kMaxInit};
+      load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
+      if constexpr (MM && K != kKeyHash) {
+        wave_minmax(mm[0], mm[1]);
+        wmn = min(wmn, mm[0]);
+        wmx = max(wmx, mm[1]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
+        s_rec[seg_local + seg_row<K, DENSE>(j, lane)] = slice_record(hh[j]);
+        sl2[(sg * 8 + j) >> 1] |= sl << (16 * (j & 1));
+        if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
+      }
+    }
+    if constexpr (MM && K != kKeyHash) publish_minmax(wmn, wmx, stats);
+    __syncthreads();
+    if (wave == 0) {  // exclusive scan of the slice counts, each padded to 4 records: kMaxSliceCount/64 per lane
+      constexpr int kPer = kMaxSliceCount / 64;
+      uint32_t c[kPer], t = 0;
+#pragma unroll
+      for (int i = 0; i < kPer; i++) {
+        const uint32_t idx = lane * kPer + i;
+        c[i] = idx < n_slices ? pad_run(s_cnt[idx]) : 0u;
+        t += c[i];
+      }
+      uint32_t off = wave_inclusive_sum(t) - t;
+#pragma unroll
+      for (int i = 0; i < kPer; i++) {
+        if (lane * kPer + i < n_slices) s_cur[lane * kPer + i] = off;
+        off += c[i];
+      }
+    }
+    // pass 2: pull this thread's records back out of the row-ordered staging ...
+    uint32_t rec[kRowsPerThread];
+#pragma unroll
+    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
+      const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+#pragma unroll
+      for (int j = 0; j < 8; j++) rec[sg * 8 + j] = s_rec[seg_local + seg_row<K, DENSE>(j, lane)];
+    }
+    __syncthreads();
+    // ... and scatter them to their slice-sorted positions
+#pragma unroll
+    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
+      const uint64_t base = tile_base + wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+      const uint32_t seg_rem = n > base ? static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows) : 0u;
+      uint16_t pv[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int jj = sg * 8 + j;
+        const uint32_t sl = (sl2[jj >> 1] >> (16 * (jj & 1))) & 0xFFFFu;
+        const bool ok = seg_row<K, DENSE>(j, lane) < seg_rem;
+        uint32_t p = 0;
+        if (ok) {
+          p = atomicAdd(&s_cur[sl], 1u);
+          s_rec[p] = rec[jj];
+        }
+        pv[j] = static_cast<uint16_t>(p);
+      }
+      // pos is padded to whole tiles: rows >= n get don't-care values. (nullptr: build, no row map)
+      if (pos_out == nullptr) {
+      } else if constexpr (DENSE) {
+        constexpr int V = KeyTraits<K>::kVec;
+#pragma unroll
+        for (int c = 0; c < 8 / V; c++) {
+          const uint64_t row0 = base + static_cast<uint64_t>(c) * 64 * V + static_cast<uint64_t>(lane) * V;
+          if constexpr (V == 2) {
+            *reinterpret_cast<uint32_t*>(pos_out + row0) =
+                static_cast<uint32_t>(pv[c * 2]) | (static_cast<uint32_t>(pv[c * 2 + 1]) << 16);
+          } else {
+            *reinterpret_cast<uint64_t*>(pos_out + row0) =
+                static_cast<uint64_t>(pv[c * 4]) | (static_cast<uint64_t>(pv[c * 4 + 1]) << 16) |
+                (static_cast<uint64_t>(pv[c * 4 + 2]) << 32) | (static_cast<uint64_t>(pv[c * 4 + 3]) << 48);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < 8; c++) pos_out[base + c * 64 + lane] = pv[c];
+      }
+    }
+    __syncthreads();
+    // records of the tile (pad slots hold stale values: probed, never read back); the scatter left
+    // s_cur[i] = start_i + count_i
+    const uint32_t used = s_cur[slice_mask] - s_cnt[slice_mask] + pad_run(s_cnt[slice_mask]);
+    u32x4* dst = reinterpret_cast<u32x4*>(recs + tile * tile_cap);
+    const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
+    for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
+      runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i]) << 16) | s_cnt[i];  // start | true count
+    __syncthreads();
+  }
+}
+
+// runs_sm[slice][tile] = runs_tm[tile][slice], through 64 x 64 LDS tiles (both sides coalesced).
+__global__ __launch_bounds__(kBlockThreads) void runs_transpose_kernel(const uint32_t* __restrict__ runs_tm,
+                                                                      uint32_t n_slices, uint64_t n_tiles,
+                                                                      uint32_t* __restrict__ runs_sm) {
+  __shared__ uint32_t s_t[64][65];
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * 64;
+  const uint32_t s0 = blockIdx.y * 64;
+  const uint32_t c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  for (uint32_t r = r0; r < 64; r += 4) {
+    const uint64_t t = t0 + r;
+    s_t[r][c] = (t < n_tiles && s0 + c < n_slices) ? runs_tm[t * n_slices + s0 + c] : 0u;
+  }
+  __syncthreads();
+  for (uint32_t r = r0; r < 64; r += 4) {
+    const uint64_t t = t0 + c;
+    if (t < n_tiles && s0 + r < n_slices) runs_sm[static_cast<uint64_t>(s0 + r) * n_tiles + t] = s_t[c][r];
+  }
+}
+
+// ---- partitioned probe, B: one workgroup per (slice, tile range) probes its records from LDS -------
+
+// The runs of 64 consecutive tiles are walked as ONE flattened record stream per wave: record k of
+// the stream belongs to the tile whose inclusive run-length prefix first exceeds k. Runs are padded
+// to kRunPad = 8 records, so each lane owns 8 consecutive, 32-byte aligned records of one run: two
+// 16-B loads and one byte of pass bits per lane, 512 records per wave step. The (uniform) tile cursor
+// lives in scalar registers; a step visits only the few tiles its 512 records overlap. Record offsets
+// are 32-bit relative to the batch's first tile (a uniform base pointer).
+// Which tiles and run-table row a slice workgroup walks. Plain partitioned: all n_tiles tiles, run row
+// = slice. Bucketed (bucket_tiles != nullptr): global slice g = bucket * kBucketSlices + local slice;
+// the bucket's tiles are [bucket_tiles[b], bucket_tiles[b+1]) and the run row is the local slice.
+struct SliceWork {
+  uint32_t slice, run_row;
+  uint64_t t_lo, t_hi;
+};
+__device__ __forceinline__ SliceWork slice_work(uint32_t item, uint32_t splits, uint64_t n_tiles,
+                                                const uint32_t* bucket_tiles) {
+  const uint32_t slice = item / splits, part = item % splits;
+  uint64_t lo = 0, cnt = n_tiles;
+  uint32_t row = slice;
+  if (bucket_tiles != nullptr) {
+    const uint32_t b = slice >> kBucketSliceLog;
+    lo = bucket_tiles[b];
+    cnt = bucket_tiles[b + 1] - lo;
+    row = slice & (kBucketSlices - 1);
+  }
+  return SliceWork{slice, row, lo + cnt * part / splits, lo + cnt * (part + 1) / splits};
+}
+
+// Probe the runs of tiles [sw.t_lo, sw.t_hi) of one slice held in LDS (see above).
+// Tiles per wave batch: 64 (one run per lane), or fewer so that all kSliceThreads/64 waves get work.
+__device__ __forceinline__ uint32_t batch_tiles(uint64_t n_t) {
+  constexpr uint64_t kWaves = kSliceThreads / 64;
+  return static_cast<uint32_t>(n_t >= 64 * kWaves ? 64 : (n_t + kWaves - 1) / kWaves);
+}
+
+__device__ __forceinline__ void probe_slice_runs(const uint64_t* s_slice, const uint64_t* s_rmasks, const SliceWork& sw,
+                                                 uint64_t n_tiles, const uint32_t* __restrict__ recs,
+                                                 const uint32_t* __restrict__ runs, uint8_t* __restrict__ passbits,
+                                                 uint32_t tile_cap) {
+  constexpr int kUnroll = RPT_SLICE_UNROLL;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr uint32_t kWaves = kSliceThreads / 64;
+  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
+  const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
+  // a wave walks batches of bt <= 64 consecutive tiles (one run per lane); few tiles per slice (the
+  // bucketed strategy) are spread over all waves in smaller batches
+  const uint32_t bt = batch_tiles(t_hi - t_lo);
+  const uint32_t my = lane < bt ? lane : ~0u >> 1;  // lanes >= bt hold no run
+  uint32_t info_next = (t_lo + wave * bt + my < t_hi) ? my_runs[t_lo + wave * bt + my] : 0u;
+  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
+    const uint32_t info = info_next;  // the next batch's runs are fetched while this one is probed
+    info_next = (tb + kWaves * bt + my < t_hi) ? my_runs[tb + kWaves * bt + my] : 0u;
+    const uint32_t cnt = pad_run(info & 0xFFFFu);  // padded run length (multiple of kRunPad)
+    const uint32_t start = lane * tile_cap + (info >> 16);
+    const uint32_t* brecs = recs + tb * tile_cap;  // uniform
+    uint8_t* bpass = passbits + tb * (tile_cap / kRunPad);
+    const uint32_t incl = wave_inclusive_sum(cnt);
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    uint32_t j = 0;  // uniform: first tile of the batch whose inclusive prefix exceeds the step start
+    constexpr uint32_t kStep = 64 * kRunPad;  // records per wave step
+    for (uint32_t k0 = 0; k0 < total; k0 += kStep * kUnroll) {
+      uint32_t off[kUnroll];
+      u32x4 rec[kUnroll][2];
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        const uint32_t kf = k0 + u * kStep;
+        const uint32_t k = kf + lane * kRunPad;
+        off[u] = ~0u;
+        if (kf < total) {
+          while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
+          const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
+          for (uint32_t jj = j;; jj++) {
+            const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
+            const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
+            const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(start), jj));
+            if (k >= inc - c && k < inc) off[u] = b + (k - (inc - c));
+            if (inc > kl) break;
+          }
+        }
+        rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
+        if (off[u] != ~0u) {
+          rec[u][0] = *reinterpret_cast<const u32x4*>(brecs + off[u]);
+          rec[u][1] = *reinterpret_cast<const u32x4*>(brecs + off[u] + 4);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
+        if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
+      }
+    }
+  }
+}
+
+// First work item >= item (stepping by gridDim.x) that has tiles; n_items if none.
+__device__ __forceinline__ uint32_t next_item(uint32_t item, uint32_t n_items, uint32_t splits, uint64_t n_tiles,
+                                              const uint32_t* bucket_tiles, SliceWork& sw) {
+  for (; item < n_items; item += gridDim.x) {
+    sw = slice_work(item, splits, n_tiles, bucket_tiles);
+    if (sw.t_lo < sw.t_hi) break;
+  }
+  return item;
+}
+
+// Work items (slice, split) are walked by a resident grid; when a workgroup has several (filters with
+// more slices than the chip has CUs: the bucketed strategy), the next item's slice is fetched into
+// registers (128 B per thread) while the current one is probed, then stored to LDS.
+__global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64_t* __restrict__ words,
+                                                                   uint32_t splits, uint64_t n_tiles,
+                                                                   const uint32_t* __restrict__ recs,
+                                                                   const uint32_t* __restrict__ runs,
+                                                                   uint8_t* __restrict__ passbits,
+                                                                   uint32_t tile_slices,
+                                                                   const uint32_t* __restrict__ bucket_tiles,
+                                                                   uint32_t n_items) {
+  // one LDS array, table first: the slice's base offset folds into the ds_read immediate
+  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
+  uint64_t* const s_rmasks = s_lds;
+  uint64_t* const s_slice = s_lds + kRotMasks;
+  u64x2* const s_slice2 = reinterpret_cast<u64x2*>(s_slice);
+  constexpr uint32_t kPre = kSliceWords / 2 / kSliceThreads;  // 16-B pieces of a slice per thread
+  SliceWork cur;
+  uint32_t item = next_item(blockIdx.x, n_items, splits, n_tiles, bucket_tiles, cur);
+  if (item >= n_items) return;  // uniform
+  {
+    const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(cur.slice) * kSliceWords);
+#pragma unroll
+    for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = src[threadIdx.x + i * kSliceThreads];
+  }
+  fill_rot_mask_table(s_rmasks);
+  const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(tile_slices));
+  while (true) {
+    __syncthreads();
+    SliceWork nxt;
+    const uint32_t nitem = next_item(item + gridDim.x, n_items, splits, n_tiles, bucket_tiles, nxt);
+    u64x2 pre[kPre];
+    if (nitem < n_items) {
+      const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(nxt.slice) * kSliceWords);
+#pragma unroll
+      for (uint32_t i = 0; i < kPre; i++) pre[i] = src[threadIdx.x + i * kSliceThreads];
+    }
+    probe_slice_runs(s_slice, s_rmasks, cur, n_tiles, recs, runs, passbits, tile_cap);
+    if (nitem >= n_items) break;
+    __syncthreads();  // every wave is done with this slice
+    for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = pre[i];  // unrolled by the compiler
+    item = nitem;
+    cur = nxt;
+  }
+}
+
+// ---- partitioned build: OR each slice's records into an LDS copy, then merge into the filter ----
+// Same flattened run walk as slice_probe_kernel. The slice starts from zero in LDS (ds_or_b64 per
+// record) and is merged into the filter with coalesced 64-bit device-scope atomic ORs of its non-zero
+// words, so concurrent inserts and several workgroups per slice compose (OR is idempotent).
+__global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* __restrict__ words, uint32_t splits,
+                                                                    uint64_t n_tiles,
+                                                                    const uint32_t* __restrict__ recs,
+                                                                    const uint32_t* __restrict__ runs,
+                                                                    uint32_t tile_slices,
+                                                                    const uint32_t* __restrict__ bucket_tiles) {
+  // one LDS array, table first: the slice's base offset folds into the ds_read immediate
+  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
+  uint64_t* const s_rmasks = s_lds;
+  uint64_t* const s_slice = s_lds + kRotMasks;
+  const SliceWork sw = slice_work(blockIdx.x, splits, n_tiles, bucket_tiles);
+  const uint32_t slice = sw.slice;
+  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
+  if (t_lo >= t_hi) return;  // no rows reach this slice (uniform)
+  for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) s_slice[i] = 0;
+  fill_rot_mask_table(s_rmasks);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr uint32_t kWaves = kSliceThreads / 64;
+  const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
+  const uint64_t tile_cap = tile_cap_for(tile_slices);
+  const uint32_t bt = batch_tiles(t_hi - t_lo);  // as slice_probe_kernel
+  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
+    const uint32_t info = (lane < bt && tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
+    const uint32_t real = info & 0xFFFFu;      // records of the run
+    const uint32_t cnt = pad_run(real);          // padded length (k-space)
+    const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
+    const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
+    const uint32_t incl = wave_inclusive_sum(cnt);
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    uint32_t j = 0;
+    constexpr uint32_t kStep = 64 * kRunPad;
+    for (uint32_t kf = 0; kf < total; kf += kStep) {
+      const uint32_t k = kf + lane * kRunPad;
+      while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
+      const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
+      uint64_t addr = ~0ULL;
+      uint32_t nreal = 0;  // how many of this lane's kRunPad slots are real records (pad slots are stale)
+      for (uint32_t jj = j;; jj++) {
+        const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
+        const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
+        const uint32_t rl = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(real), jj));
+        const uint64_t b =
+            static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_lo), jj))) |
+            (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_hi), jj))) << 32);
+        if (k >= inc - c && k < inc) {
+          const uint32_t off = k - (inc - c);
+          addr = b + off;
+          nreal = rl > off ? (rl - off < kRunPad ? rl - off : kRunPad) : 0;
+        }
+        if (inc > kl) break;
+      }
+      if (addr != ~0ULL) {
+        const u32x4 r0 = *reinterpret_cast<const u32x4*>(recs + addr);
+        const u32x4 r1 = *reinterpret_cast<const u32x4*>(recs + addr + 4);
+#pragma unroll
+        for (uint32_t e = 0; e < kRunPad; e++) {
+          if (e < nreal) {
+            const uint32_t rec = e < 4 ? r0[e] : r1[e - 4];
+            atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[rec_word(rec)]),
+                     static_cast<unsigned long long>(rec_mask(s_rmasks, rec)));
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
+  for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
+    const uint64_t v = s_slice[i];
+    if (v) __hip_atomic_fetch_or(dst + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---- partitioned probe, C: restore row order -> result bits + per-segment counts (P1's format) -----
+// One 256-thread workgroup per tile: the tile's pass bits (tile_cap / 8 bytes) are staged in LDS while
+// each wave's row positions are already in flight; a lane owns 8 consecutive rows of a segment (one
+// 16-B load of positions) and produces byte `lane` of the segment's 512-bit row-ordered result.
+constexpr int kUnpermuteThreads = 256;
+__global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
+                                                                     const uint8_t* __restrict__ passbits, uint64_t n,
+                                                                     uint64_t tile_cap,
+                                                                     uint64_t* __restrict__ out_bits,
+                                                                     uint32_t* __restrict__ seg_counts,
+                                                                     const uint32_t* __restrict__ dev_n_tiles) {
+  if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;  // bucketed: grid is an upper bound
+  extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
+  constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / (kUnpermuteThreads / 64);
+  const uint64_t tile = blockIdx.x;
+  const uint64_t seg0 = tile * (kTileRows / kSegRows) + wave * kSegsPerWave;
+  u32x4 pv[kSegsPerWave];  // 8 row positions (u16) per lane per segment
+#pragma unroll
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    pv[sg] = u32x4{0, 0, 0, 0};
+    if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos + (seg0 + sg) * kSegRows + lane * 8);
+  }
+  {
+    const u32x4* src = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / 8));
+    for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
+  }
+  __syncthreads();
+  uint8_t* out_bytes = reinterpret_cast<uint8_t*>(out_bits);
+#pragma unroll
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    const uint64_t seg = seg0 + sg;
+    if (seg >= n_segs) break;
+    uint32_t byte = 0;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+      byte |= ((static_cast<uint32_t>(s_pass[p >> 3]) >> (p & 7)) & 1u) << e;
+    }
+    const uint64_t row0 = seg * kSegRows + lane * 8;  // rows >= n (last segment) carry don't-care positions
+    if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
+    out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);
+    if (seg_counts != nullptr) {
+      const uint32_t cnt = wave_sum(__popc(byte));
+      if (lane == 0) seg_counts[seg] = cnt;
+    }
+  }
+}
+}  // namespace rpt

@@ -1,18 +1,20 @@
-// rpt_gpu.hip — HIP kernels (gfx950) and the C-ABI of librpt_gpu.so (include/rpt_gpu.h).
+// rpt_gpu.hip — the C-ABI of librpt_gpu.so (include/rpt_gpu.h) and its host runtime; the gfx950
+// kernels live in kernels/*.hpp, included below into this one translation unit.
 //
 // Hot path: PTBloomFilter::Insert / LookupSel (reference src/bloom_filter.cpp:60-78),
 // called per DataChunk by PhysicalCreateBF::Sink (physical_create_bf.cpp:221-227) and
 // PhysicalUseBF::ExecuteInternal (physical_use_bf.cpp:163). Re-designed for MI355X:
 //
-//   insert   : one pass over the key column, 16-B coalesced loads, hash in registers, mask from an
-//              8 KiB LDS table, one device-scope 64-bit atomic OR per key (k2).
-//   probe    : P1 hash + gather + wave ballot -> result bit vector (Arrow Find layout) + one
-//              survivor count per 512-row wave segment;  P2 two-level scan of the counts;
-//              P3 expand bits into an ascending uint32 selection vector (k1).
-//   merge    : OR of partial filters / peer slices (k4);  fold (k3);  popcount.
-//
-// All kernels are persistent grid-stride loops over 512-row wave segments: a wave owns a segment
-// end to end, so P1 needs no barrier after the LDS mask-table fill.
+//   probe   : phase 1 = hash + filter test -> result bit vector (Arrow Find layout) + one survivor
+//             count per 512-row segment, by one of four strategies (rpt_probe_strategy):
+//               GATHER       probe_direct.hpp  one 8-B gather per key
+//               LDS          probe_direct.hpp  filters <= 64 KiB staged whole in LDS
+//               PARTITIONED  partitioned.hpp   rows routed by 128 KiB filter slice; slices in LDS
+//               BUCKETED     bucketed.hpp      two levels for filters of 32 MiB..16 GiB
+//             phase 2 = two-level scan + expansion into an ascending uint32 sel (compaction.hpp).
+//   insert  : atomic OR per key (misc.hpp), or the partitioned / bucketed routing with the slices
+//             ORed in LDS; the build's key min/max is folded in on the way.
+//   merge   : OR of partial filters / peer slices;  fold;  popcount (misc.hpp).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -29,1217 +31,12 @@
 #include "rpt_gpu.h"
 #include "rpt_gpu_synth.h"
 
-namespace rpt {
-
-constexpr int kBlockThreads = 256;
-constexpr int kWavesPerBlock = kBlockThreads / 64;
-constexpr uint64_t kSegRows = 512;                 // rows per wave segment (8 per lane)
-constexpr uint64_t kWordsPerSeg = kSegRows / 64;   // result-bit words per segment
-constexpr uint64_t kGroupSegs = 256;               // segments per scan group (one compaction workgroup)
-constexpr int kBlocksPerCU = 8;
-
-// Partitioned ("routed") probe: the filter is cut into 128 KiB slices that fit in LDS; probe rows are
-// bucketed by slice per 16 Ki-row tile so that every filter access is an LDS read.
-#ifndef RPT_SLICE_LOG
-#define RPT_SLICE_LOG 14
-#endif
-constexpr int kSliceLog = RPT_SLICE_LOG;               // 2^13 blocks = 64 KiB (or 2^14 = 128 KiB) per slice
-constexpr uint64_t kSliceWords = 1ULL << kSliceLog;
-constexpr int kMaxSliceCount = 1024;                   // P <= 1024 slices (filters <= 128 MiB at 128 KiB slices)
-#ifndef RPT_TILE_ROWS
-#define RPT_TILE_ROWS 16384
-#endif
-constexpr uint64_t kTileRows = RPT_TILE_ROWS;          // rows per partition tile (8 or 16 per thread)
-// Runs are padded to kRunPad records so a lane owns kRunPad aligned records of one run and its pass
-// results form one byte of bits. Tile capacity is a multiple of 128 so the tile's pass bits are
-// whole 16-byte vectors.
-constexpr uint32_t kRunPad = 8;
-__host__ __device__ constexpr uint32_t pad_run(uint32_t c) { return (c + kRunPad - 1) & ~(kRunPad - 1); }
-__host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices) {
-  return (kTileRows + static_cast<uint64_t>(kRunPad) * n_slices + 127) & ~127ULL;
-}
-// Bucketed strategy (filters > 128 MiB): 16 MiB buckets of 128 slices, at most 1024 buckets (16 GiB).
-constexpr int kBucketSliceLog = 7;
-constexpr uint32_t kBucketSlices = 1u << kBucketSliceLog;
-constexpr uint32_t kMaxBuckets = 1024;
-constexpr int kTileThreads = 1024;                     // 16 waves
-constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
-constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave in the partition kernel
-static_assert(kRowsPerThread == 8 || kRowsPerThread == 16 || kRowsPerThread == 32, "tile = 8, 16 or 32 Ki rows");
-constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
-constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
-#ifndef RPT_SLICE_UNROLL
-#define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
-#endif
-#ifndef RPT_PARTITION_MIN_WAVES
-#define RPT_PARTITION_MIN_WAVES 8                      // 2 partition workgroups per CU (64 VGPRs)
-#endif
-
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
-struct KeyArgs {
-  const void* keys;
-  const uint32_t* key_sel;
-  const uint64_t* validity;
-  const uint32_t* row_sel;
-};
-
-__device__ __forceinline__ bool valid_at(const uint64_t* validity, uint64_t idx) {
-  return validity == nullptr || ((validity[idx >> 6] >> (idx & 63)) & 1ULL);
-}
-
-// Hashes of the 8 rows a lane owns in a segment.
-//  DENSE   (flat column, no selections, 16-B aligned): row(c, e) = base + c*64*V + lane*V + e,
-//          one 16-byte load per (c): fully coalesced 1 KiB per wave instruction.
-//  GENERAL (dictionary key_sel and/or row_sel):        row(c) = base + c*64 + lane.
-// MM: also fold the valid (non-NULL, in-range) key values into mm[0] = min, mm[1] = max (the build's
-// min/max dynamic filter, physical_create_bf.cpp:82-119, fused into the key read).
-template <int K, bool DENSE, bool MM = false>
-__device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uint64_t n, uint32_t lane,
-                                            uint64_t (&h)[8], bool (&ok)[8], int64_t* mm = nullptr) {
-  using Tr = KeyTraits<K>;
-  using T = typename Tr::T;
-  // rows left from `base` (uniform), so per-row bounds checks are 32-bit and addresses are
-  // uniform-base + 32-bit lane offset
-  const uint32_t rem = n > base ? static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows) : 0u;
-  if constexpr (DENSE) {
-    constexpr int V = Tr::kVec;
-    const T* kb = static_cast<const T*>(a.keys) + base;
-    const uint64_t* vb = a.validity ? a.validity + (base >> 6) : nullptr;  // base is a multiple of 512
-#pragma unroll
-    for (int c = 0; c < 8 / V; c++) {
-      const uint32_t off = static_cast<uint32_t>(c * 64 * V) + lane * V;
-      T v[V];
-      if (off + V <= rem) {
-        if constexpr (V == 2) {
-          const u64x2 x = *reinterpret_cast<const u64x2*>(kb + off);
-          v[0] = static_cast<T>(x[0]);
-          v[1] = static_cast<T>(x[1]);
-        } else {
-          const u32x4 x = *reinterpret_cast<const u32x4*>(kb + off);
-#pragma unroll
-          for (int e = 0; e < V; e++) v[e] = static_cast<T>(x[e]);
-        }
-      } else {
-#pragma unroll
-        for (int e = 0; e < V; e++) v[e] = (off + e < rem) ? kb[off + e] : T(0);
-      }
-      // validity bits of this lane's V rows, shifted down to bits 0..V-1 (V | 64: one word)
-      uint32_t vbits = (1u << V) - 1;
-      if (K != kKeyHash && vb != nullptr && off < rem) vbits = static_cast<uint32_t>(vb[off >> 6] >> (off & 63));
-#pragma unroll
-      for (int e = 0; e < V; e++) {
-        ok[c * V + e] = off + e < rem;
-        uint64_t hv = Tr::hash(v[e]);
-        if (K != kKeyHash && !((vbits >> e) & 1u)) hv = kNullHash;
-        h[c * V + e] = hv;
-        if constexpr (MM && K != kKeyHash) {
-          if (off + e < rem && ((vbits >> e) & 1u)) {
-            mm[0] = min(mm[0], static_cast<int64_t>(v[e]));
-            mm[1] = max(mm[1], static_cast<int64_t>(v[e]));
-          }
-        }
-      }
-    }
-  } else {
-    const T* keys = static_cast<const T*>(a.keys);
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const uint32_t off = static_cast<uint32_t>(c * 64) + lane;
-      ok[c] = off < rem;
-      uint64_t hv = 0;
-      if (ok[c]) {
-        const uint64_t i = base + off;
-        const uint64_t r = a.row_sel ? a.row_sel[i] : i;
-        const uint64_t k = a.key_sel ? a.key_sel[r] : r;
-        const T kv = keys[k];
-        hv = Tr::hash(kv);
-        const bool valid = valid_at(a.validity, k);
-        if (K != kKeyHash && !valid) hv = kNullHash;
-        if constexpr (MM && K != kKeyHash) {
-          if (valid) {
-            mm[0] = min(mm[0], static_cast<int64_t>(kv));
-            mm[1] = max(mm[1], static_cast<int64_t>(kv));
-          }
-        }
-      }
-      h[c] = hv;
-    }
-  }
-}
-
-// Row offset inside a 512-row segment of the j-th hash load_hashes<K, DENSE> returns for `lane`.
-template <int K, bool DENSE>
-__device__ __forceinline__ uint32_t seg_row(int j, uint32_t lane) {
-  if constexpr (DENSE) {
-    constexpr int V = KeyTraits<K>::kVec;
-    return static_cast<uint32_t>((j / V) * 64 * V) + lane * V + static_cast<uint32_t>(j % V);
-  } else {
-    return static_cast<uint32_t>(j * 64) + lane;
-  }
-}
-
-// Wave-wide (min, max) of per-lane values, returned wave-uniform (scalar registers).
-__device__ __forceinline__ void wave_minmax(int64_t& mn, int64_t& mx) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    mn = min(mn, static_cast<int64_t>(__shfl_xor(static_cast<long long>(mn), d, 64)));
-    mx = max(mx, static_cast<int64_t>(__shfl_xor(static_cast<long long>(mx), d, 64)));
-  }
-  auto uniform = [](int64_t v) {
-    const uint64_t u = static_cast<uint64_t>(v);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u));
-    const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(u >> 32));
-    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
-  };
-  mn = uniform(mn);
-  mx = uniform(mx);
-}
-// Fold a wave's uniform (min, max) into stats[0..1] (int64, device). A wave whose values cannot lower
-// the min or raise the max — the common case once a few waves have reported — skips the atomics.
-__device__ __forceinline__ void publish_minmax(int64_t mn, int64_t mx, int64_t* stats) {
-  if ((threadIdx.x & 63) == 0) {
-    if (mn < __hip_atomic_load(stats, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      __hip_atomic_fetch_min(stats, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (mx > __hip_atomic_load(stats + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      __hip_atomic_fetch_max(stats + 1, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-constexpr int64_t kMinInit = INT64_MAX, kMaxInit = INT64_MIN;  // "no value yet"
-
-// ---- P1: probe -> result bits + per-segment survivor counts ------------------------------------
-// FILTER_IN_LDS: the whole filter (<= 64 KiB) is staged in LDS and every gather is an LDS read.
-template <int K, bool DENSE, bool FILTER_IN_LDS>
-__global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_t* __restrict__ words,
-                                                                  uint64_t block_mask, KeyArgs a, uint64_t n,
-                                                                  uint64_t n_segs, uint64_t* __restrict__ out_bits,
-                                                                  uint32_t* __restrict__ seg_counts) {
-  __shared__ uint64_t s_masks[kNumMasks];
-  extern __shared__ uint64_t s_filter[];
-  fill_mask_table(s_masks);
-  if constexpr (FILTER_IN_LDS) {
-    for (uint64_t i = threadIdx.x; i <= block_mask; i += blockDim.x) s_filter[i] = words[i];
-  }
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-  for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6); seg < n_segs;
-       seg += total_waves) {
-    const uint64_t base = seg * kSegRows;
-    uint64_t h[8];
-    bool ok[8];
-    load_hashes<K, DENSE>(a, base, n, lane, h, ok);
-    uint64_t w[8], m[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      m[j] = mask_of(s_masks, h[j]);
-      if constexpr (FILTER_IN_LDS) {
-        w[j] = s_filter[block_of(h[j], block_mask)];
-      } else {
-        w[j] = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
-      }
-    }
-    uint64_t word[8];
-    uint32_t cnt = 0;
-    if constexpr (DENSE) {
-      constexpr int V = KeyTraits<K>::kVec;
-      uint64_t b[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        b[j] = ballot64(ok[j] && (w[j] & m[j]) == m[j]);
-        cnt += __popcll(b[j]);
-      }
-#pragma unroll
-      for (int c = 0; c < 8 / V; c++) {
-#pragma unroll
-        for (int q = 0; q < V; q++) {
-          uint64_t x = 0;
-          if constexpr (V == 2) {
-            x = spread2(b[c * 2 + 0] >> (32 * q)) | (spread2(b[c * 2 + 1] >> (32 * q)) << 1);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; e++) x |= spread4(b[c * 4 + e] >> (16 * q)) << e;
-          }
-          word[c * V + q] = x;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        word[j] = ballot64(ok[j] && (w[j] & m[j]) == m[j]);
-        cnt += __popcll(word[j]);
-      }
-    }
-    uint64_t mine = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) mine = (lane == static_cast<uint32_t>(j)) ? word[j] : mine;
-    if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
-    if (seg_counts != nullptr && lane == 0) seg_counts[seg] = cnt;
-  }
-}
-
-// ---- slice records -------------------------------------------------------------------------------
-// A record carries the 30 hash bits a filter slice needs, laid out for the slice kernels' 32-bit ALU:
-//   [0..4]   rotation & 31  (v_alignbit reads the low 5 bits of its shift operand: no extract)
-//   [5..15]  index into the 2048-entry rotated-mask table: mask id (h & 1023) | rotation bit 5 << 10
-//   [16..29] block within the slice ([30..31]: slice bits, masked off)
-// Table entry (id, r5) = ROTL64(mask(id), 32 * r5). With r = 32 * r5 + t:
-//   (w & ROTL(mask, r)) == ROTL(mask, r)  <=>  (ROTR(w, t) & entry) == entry
-// and ROTR(w, t) for t < 32 is two v_alignbit_b32 — no 64-bit shifts, no rotation of the mask.
-__device__ __forceinline__ uint32_t slice_record(uint64_t h) {
-  const uint32_t x = static_cast<uint32_t>(h);
-  return ((x >> kLogNumMasks) & 31u) | ((x & (kNumMasks - 1)) << 5) | (x & 0xFFFF8000u);
-}
-constexpr uint32_t kRotMasks = 2 * kNumMasks;
-__device__ __forceinline__ void fill_rot_mask_table(uint64_t* s_rmasks) {
-  for (int i = threadIdx.x; i < static_cast<int>(kRotMasks); i += blockDim.x) {
-    const int id = i & (kNumMasks - 1), w = id >> 6, s = id & 63;
-    const uint64_t lo = kMaskBits[w], hi = kMaskBits[w + 1];
-    const uint64_t m = ((lo >> s) | ((hi << 1) << (63 - s))) & kFullMask;
-    s_rmasks[i] = (i >> kLogNumMasks) ? rotl64(m, 32) : m;
-  }
-}
-__device__ __forceinline__ uint64_t rot_entry(const uint64_t* s_rmasks, uint32_t rec) {
-  return s_rmasks[(rec >> 5) & (kRotMasks - 1)];
-}
-__device__ __forceinline__ uint32_t rec_word(uint32_t rec) { return (rec >> 16) & (kSliceWords - 1); }
-// the filter mask of a record: ROTL(entry, t)
-__device__ __forceinline__ uint64_t rec_mask(const uint64_t* s_rmasks, uint32_t rec) {
-  return rotl64(rot_entry(s_rmasks, rec), rec & 31u);
-}
-__device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_t* s_rmasks, uint32_t rec) {
-  const uint64_t e = rot_entry(s_rmasks, rec);
-  const uint64_t w = s_slice[rec_word(rec)];
-  const uint32_t wl = static_cast<uint32_t>(w), wh = static_cast<uint32_t>(w >> 32);
-  const uint32_t xl = __builtin_amdgcn_alignbit(wh, wl, rec), xh = __builtin_amdgcn_alignbit(wl, wh, rec);
-  return ((~xl & static_cast<uint32_t>(e)) | (~xh & static_cast<uint32_t>(e >> 32))) == 0u;
-}
-
-// ---- partitioned probe, A: bucket a 16 Ki-row tile by filter slice --------------------------------
-// Row r of the tile gets record slice_record(hash) stored at position pos(r) of the tile's
-// slice-sorted record array (runs padded to kRunPad records); pos(r) is
-// written per row (u16) so the unpermute step can restore row order. Per tile the padded runs
-// (start << 16 | length) are written tile-major (one coalesced 4*P-byte row); runs_transpose_kernel
-// turns them slice-major for the slice kernel. Two passes over the rows held in registers: count per
-// slice (LDS atomics), scan, then claim positions with an LDS cursor per slice and scatter.
-// Dynamic LDS: tile_cap record slots, then the per-slice count and cursor arrays.
-template <int K, bool DENSE, bool MM>
-__global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(
-    KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
-    uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm, int64_t* __restrict__ stats,
-    const uint32_t* __restrict__ dev_n_tiles) {
-  // dev_n_tiles (bucketed strategy): the tile count is only known on the device; the grid is an upper
-  // bound and surplus workgroups leave (their run-table rows are never read).
-  if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;
-  extern __shared__ uint32_t s_dyn[];
-  const uint64_t tile_cap = tile_cap_for(slice_mask + 1);
-  uint32_t* s_rec = s_dyn;
-  uint32_t* s_cnt = s_dyn + tile_cap;                  // rows per slice in this tile
-  uint32_t* s_cur = s_dyn + tile_cap + slice_mask + 1;  // run start, then scatter cursor (start + count)
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t n_slices = slice_mask + 1;
-  {  // one tile per workgroup (no persistent loop: keeps per-lane invariants out of registers)
-    const uint64_t tile = blockIdx.x;
-    for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads) s_cnt[i] = 0;
-    __syncthreads();
-    const uint64_t tile_base = tile * kTileRows;
-    // pass 1: hash, stage the record at its row position in LDS, count rows per slice; only the 16-bit
-    // slice ids stay in registers (2 per word).
-    static_assert(kMaxSliceCount <= 65536, "slice ids are packed as 16 bits");
-    uint32_t sl2[kRowsPerThread / 2] = {};
-    int64_t wmn = kMinInit, wmx = kMaxInit;  // wave-uniform: the key min/max stays out of VGPRs
-#pragma unroll
-    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-      const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
-      uint64_t hh[8];
-      bool oo[8];
-      int64_t mm[2] = {kMinInit, kMaxInit};
-      load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
-      if constexpr (MM && K != kKeyHash) {
-        wave_minmax(mm[0], mm[1]);
-        wmn = min(wmn, mm[0]);
-        wmx = max(wmx, mm[1]);
-      }
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
-        s_rec[seg_local + seg_row<K, DENSE>(j, lane)] = slice_record(hh[j]);
-        sl2[(sg * 8 + j) >> 1] |= sl << (16 * (j & 1));
-        if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
-      }
-    }
-    if constexpr (MM && K != kKeyHash) publish_minmax(wmn, wmx, stats);
-    __syncthreads();
-    if (wave == 0) {  // exclusive scan of the slice counts, each padded to 4 records: kMaxSliceCount/64 per lane
-      constexpr int kPer = kMaxSliceCount / 64;
-      uint32_t c[kPer], t = 0;
-#pragma unroll
-      for (int i = 0; i < kPer; i++) {
-        const uint32_t idx = lane * kPer + i;
-        c[i] = idx < n_slices ? pad_run(s_cnt[idx]) : 0u;
-        t += c[i];
-      }
-      uint32_t off = wave_inclusive_sum(t) - t;
-#pragma unroll
-      for (int i = 0; i < kPer; i++) {
-        if (lane * kPer + i < n_slices) s_cur[lane * kPer + i] = off;
-        off += c[i];
-      }
-    }
-    // pass 2: pull this thread's records back out of the row-ordered staging ...
-    uint32_t rec[kRowsPerThread];
-#pragma unroll
-    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-      const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
-#pragma unroll
-      for (int j = 0; j < 8; j++) rec[sg * 8 + j] = s_rec[seg_local + seg_row<K, DENSE>(j, lane)];
-    }
-    __syncthreads();
-    // ... and scatter them to their slice-sorted positions
-#pragma unroll
-    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-      const uint64_t base = tile_base + wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
-      const uint32_t seg_rem = n > base ? static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows) : 0u;
-      uint16_t pv[8];
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int jj = sg * 8 + j;
-        const uint32_t sl = (sl2[jj >> 1] >> (16 * (jj & 1))) & 0xFFFFu;
-        const bool ok = seg_row<K, DENSE>(j, lane) < seg_rem;
-        uint32_t p = 0;
-        if (ok) {
-          p = atomicAdd(&s_cur[sl], 1u);
-          s_rec[p] = rec[jj];
-        }
-        pv[j] = static_cast<uint16_t>(p);
-      }
-      // pos is padded to whole tiles: rows >= n get don't-care values. (nullptr: build, no row map)
-      if (pos_out == nullptr) {
-      } else if constexpr (DENSE) {
-        constexpr int V = KeyTraits<K>::kVec;
-#pragma unroll
-        for (int c = 0; c < 8 / V; c++) {
-          const uint64_t row0 = base + static_cast<uint64_t>(c) * 64 * V + static_cast<uint64_t>(lane) * V;
-          if constexpr (V == 2) {
-            *reinterpret_cast<uint32_t*>(pos_out + row0) =
-                static_cast<uint32_t>(pv[c * 2]) | (static_cast<uint32_t>(pv[c * 2 + 1]) << 16);
-          } else {
-            *reinterpret_cast<uint64_t*>(pos_out + row0) =
-                static_cast<uint64_t>(pv[c * 4]) | (static_cast<uint64_t>(pv[c * 4 + 1]) << 16) |
-                (static_cast<uint64_t>(pv[c * 4 + 2]) << 32) | (static_cast<uint64_t>(pv[c * 4 + 3]) << 48);
-          }
-        }
-      } else {
-#pragma unroll
-        for (int c = 0; c < 8; c++) pos_out[base + c * 64 + lane] = pv[c];
-      }
-    }
-    __syncthreads();
-    // records of the tile (pad slots hold stale values: probed, never read back); the scatter left
-    // s_cur[i] = start_i + count_i
-    const uint32_t used = s_cur[slice_mask] - s_cnt[slice_mask] + pad_run(s_cnt[slice_mask]);
-    u32x4* dst = reinterpret_cast<u32x4*>(recs + tile * tile_cap);
-    const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
-    for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
-      runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i]) << 16) | s_cnt[i];  // start | true count
-    __syncthreads();
-  }
-}
-
-// runs_sm[slice][tile] = runs_tm[tile][slice], through 64 x 64 LDS tiles (both sides coalesced).
-__global__ __launch_bounds__(kBlockThreads) void runs_transpose_kernel(const uint32_t* __restrict__ runs_tm,
-                                                                      uint32_t n_slices, uint64_t n_tiles,
-                                                                      uint32_t* __restrict__ runs_sm) {
-  __shared__ uint32_t s_t[64][65];
-  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * 64;
-  const uint32_t s0 = blockIdx.y * 64;
-  const uint32_t c = threadIdx.x & 63, r0 = threadIdx.x >> 6;
-  for (uint32_t r = r0; r < 64; r += 4) {
-    const uint64_t t = t0 + r;
-    s_t[r][c] = (t < n_tiles && s0 + c < n_slices) ? runs_tm[t * n_slices + s0 + c] : 0u;
-  }
-  __syncthreads();
-  for (uint32_t r = r0; r < 64; r += 4) {
-    const uint64_t t = t0 + c;
-    if (t < n_tiles && s0 + r < n_slices) runs_sm[static_cast<uint64_t>(s0 + r) * n_tiles + t] = s_t[c][r];
-  }
-}
-
-// ---- partitioned probe, B: one workgroup per (slice, tile range) probes its records from LDS -------
-
-// The runs of 64 consecutive tiles are walked as ONE flattened record stream per wave: record k of
-// the stream belongs to the tile whose inclusive run-length prefix first exceeds k. Runs are padded
-// to kRunPad = 8 records, so each lane owns 8 consecutive, 32-byte aligned records of one run: two
-// 16-B loads and one byte of pass bits per lane, 512 records per wave step. The (uniform) tile cursor
-// lives in scalar registers; a step visits only the few tiles its 512 records overlap. Record offsets
-// are 32-bit relative to the batch's first tile (a uniform base pointer).
-// Which tiles and run-table row a slice workgroup walks. Plain partitioned: all n_tiles tiles, run row
-// = slice. Bucketed (bucket_tiles != nullptr): global slice g = bucket * kBucketSlices + local slice;
-// the bucket's tiles are [bucket_tiles[b], bucket_tiles[b+1]) and the run row is the local slice.
-struct SliceWork {
-  uint32_t slice, run_row;
-  uint64_t t_lo, t_hi;
-};
-__device__ __forceinline__ SliceWork slice_work(uint32_t item, uint32_t splits, uint64_t n_tiles,
-                                                const uint32_t* bucket_tiles) {
-  const uint32_t slice = item / splits, part = item % splits;
-  uint64_t lo = 0, cnt = n_tiles;
-  uint32_t row = slice;
-  if (bucket_tiles != nullptr) {
-    const uint32_t b = slice >> kBucketSliceLog;
-    lo = bucket_tiles[b];
-    cnt = bucket_tiles[b + 1] - lo;
-    row = slice & (kBucketSlices - 1);
-  }
-  return SliceWork{slice, row, lo + cnt * part / splits, lo + cnt * (part + 1) / splits};
-}
-
-// Probe the runs of tiles [sw.t_lo, sw.t_hi) of one slice held in LDS (see above).
-// Tiles per wave batch: 64 (one run per lane), or fewer so that all kSliceThreads/64 waves get work.
-__device__ __forceinline__ uint32_t batch_tiles(uint64_t n_t) {
-  constexpr uint64_t kWaves = kSliceThreads / 64;
-  return static_cast<uint32_t>(n_t >= 64 * kWaves ? 64 : (n_t + kWaves - 1) / kWaves);
-}
-
-__device__ __forceinline__ void probe_slice_runs(const uint64_t* s_slice, const uint64_t* s_rmasks, const SliceWork& sw,
-                                                 uint64_t n_tiles, const uint32_t* __restrict__ recs,
-                                                 const uint32_t* __restrict__ runs, uint8_t* __restrict__ passbits,
-                                                 uint32_t tile_cap) {
-  constexpr int kUnroll = RPT_SLICE_UNROLL;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr uint32_t kWaves = kSliceThreads / 64;
-  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
-  const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
-  // a wave walks batches of bt <= 64 consecutive tiles (one run per lane); few tiles per slice (the
-  // bucketed strategy) are spread over all waves in smaller batches
-  const uint32_t bt = batch_tiles(t_hi - t_lo);
-  const uint32_t my = lane < bt ? lane : ~0u >> 1;  // lanes >= bt hold no run
-  uint32_t info_next = (t_lo + wave * bt + my < t_hi) ? my_runs[t_lo + wave * bt + my] : 0u;
-  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
-    const uint32_t info = info_next;  // the next batch's runs are fetched while this one is probed
-    info_next = (tb + kWaves * bt + my < t_hi) ? my_runs[tb + kWaves * bt + my] : 0u;
-    const uint32_t cnt = pad_run(info & 0xFFFFu);  // padded run length (multiple of kRunPad)
-    const uint32_t start = lane * tile_cap + (info >> 16);
-    const uint32_t* brecs = recs + tb * tile_cap;  // uniform
-    uint8_t* bpass = passbits + tb * (tile_cap / kRunPad);
-    const uint32_t incl = wave_inclusive_sum(cnt);
-    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-    uint32_t j = 0;  // uniform: first tile of the batch whose inclusive prefix exceeds the step start
-    constexpr uint32_t kStep = 64 * kRunPad;  // records per wave step
-    for (uint32_t k0 = 0; k0 < total; k0 += kStep * kUnroll) {
-      uint32_t off[kUnroll];
-      u32x4 rec[kUnroll][2];
-#pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        const uint32_t kf = k0 + u * kStep;
-        const uint32_t k = kf + lane * kRunPad;
-        off[u] = ~0u;
-        if (kf < total) {
-          while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
-          const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
-          for (uint32_t jj = j;; jj++) {
-            const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
-            const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
-            const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(start), jj));
-            if (k >= inc - c && k < inc) off[u] = b + (k - (inc - c));
-            if (inc > kl) break;
-          }
-        }
-        rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
-        if (off[u] != ~0u) {
-          rec[u][0] = *reinterpret_cast<const u32x4*>(brecs + off[u]);
-          rec[u][1] = *reinterpret_cast<const u32x4*>(brecs + off[u] + 4);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        uint32_t bits = 0;
-#pragma unroll
-        for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
-        if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
-      }
-    }
-  }
-}
-
-// First work item >= item (stepping by gridDim.x) that has tiles; n_items if none.
-__device__ __forceinline__ uint32_t next_item(uint32_t item, uint32_t n_items, uint32_t splits, uint64_t n_tiles,
-                                              const uint32_t* bucket_tiles, SliceWork& sw) {
-  for (; item < n_items; item += gridDim.x) {
-    sw = slice_work(item, splits, n_tiles, bucket_tiles);
-    if (sw.t_lo < sw.t_hi) break;
-  }
-  return item;
-}
-
-// Work items (slice, split) are walked by a resident grid; when a workgroup has several (filters with
-// more slices than the chip has CUs: the bucketed strategy), the next item's slice is fetched into
-// registers (128 B per thread) while the current one is probed, then stored to LDS.
-__global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64_t* __restrict__ words,
-                                                                   uint32_t splits, uint64_t n_tiles,
-                                                                   const uint32_t* __restrict__ recs,
-                                                                   const uint32_t* __restrict__ runs,
-                                                                   uint8_t* __restrict__ passbits,
-                                                                   uint32_t tile_slices,
-                                                                   const uint32_t* __restrict__ bucket_tiles,
-                                                                   uint32_t n_items) {
-  // one LDS array, table first: the slice's base offset folds into the ds_read immediate
-  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
-  uint64_t* const s_rmasks = s_lds;
-  uint64_t* const s_slice = s_lds + kRotMasks;
-  u64x2* const s_slice2 = reinterpret_cast<u64x2*>(s_slice);
-  constexpr uint32_t kPre = kSliceWords / 2 / kSliceThreads;  // 16-B pieces of a slice per thread
-  SliceWork cur;
-  uint32_t item = next_item(blockIdx.x, n_items, splits, n_tiles, bucket_tiles, cur);
-  if (item >= n_items) return;  // uniform
-  {
-    const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(cur.slice) * kSliceWords);
-#pragma unroll
-    for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = src[threadIdx.x + i * kSliceThreads];
-  }
-  fill_rot_mask_table(s_rmasks);
-  const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(tile_slices));
-  while (true) {
-    __syncthreads();
-    SliceWork nxt;
-    const uint32_t nitem = next_item(item + gridDim.x, n_items, splits, n_tiles, bucket_tiles, nxt);
-    u64x2 pre[kPre];
-    if (nitem < n_items) {
-      const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(nxt.slice) * kSliceWords);
-#pragma unroll
-      for (uint32_t i = 0; i < kPre; i++) pre[i] = src[threadIdx.x + i * kSliceThreads];
-    }
-    probe_slice_runs(s_slice, s_rmasks, cur, n_tiles, recs, runs, passbits, tile_cap);
-    if (nitem >= n_items) break;
-    __syncthreads();  // every wave is done with this slice
-#pragma unroll
-    for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = pre[i];
-    item = nitem;
-    cur = nxt;
-  }
-}
-
-// ---- partitioned build: OR each slice's records into an LDS copy, then merge into the filter ----
-// Same flattened run walk as slice_probe_kernel. The slice starts from zero in LDS (ds_or_b64 per
-// record) and is merged into the filter with coalesced 64-bit device-scope atomic ORs of its non-zero
-// words, so concurrent inserts and several workgroups per slice compose (OR is idempotent).
-__global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* __restrict__ words, uint32_t splits,
-                                                                    uint64_t n_tiles,
-                                                                    const uint32_t* __restrict__ recs,
-                                                                    const uint32_t* __restrict__ runs,
-                                                                    uint32_t tile_slices,
-                                                                    const uint32_t* __restrict__ bucket_tiles) {
-  // one LDS array, table first: the slice's base offset folds into the ds_read immediate
-  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
-  uint64_t* const s_rmasks = s_lds;
-  uint64_t* const s_slice = s_lds + kRotMasks;
-  const SliceWork sw = slice_work(blockIdx.x, splits, n_tiles, bucket_tiles);
-  const uint32_t slice = sw.slice;
-  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
-  if (t_lo >= t_hi) return;  // no rows reach this slice (uniform)
-  for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) s_slice[i] = 0;
-  fill_rot_mask_table(s_rmasks);
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr uint32_t kWaves = kSliceThreads / 64;
-  const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
-  const uint64_t tile_cap = tile_cap_for(tile_slices);
-  const uint32_t bt = batch_tiles(t_hi - t_lo);  // as slice_probe_kernel
-  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
-    const uint32_t info = (lane < bt && tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
-    const uint32_t real = info & 0xFFFFu;      // records of the run
-    const uint32_t cnt = pad_run(real);          // padded length (k-space)
-    const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
-    const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
-    const uint32_t incl = wave_inclusive_sum(cnt);
-    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-    uint32_t j = 0;
-    constexpr uint32_t kStep = 64 * kRunPad;
-    for (uint32_t kf = 0; kf < total; kf += kStep) {
-      const uint32_t k = kf + lane * kRunPad;
-      while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
-      const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
-      uint64_t addr = ~0ULL;
-      uint32_t nreal = 0;  // how many of this lane's kRunPad slots are real records (pad slots are stale)
-      for (uint32_t jj = j;; jj++) {
-        const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
-        const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
-        const uint32_t rl = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(real), jj));
-        const uint64_t b =
-            static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_lo), jj))) |
-            (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_hi), jj))) << 32);
-        if (k >= inc - c && k < inc) {
-          const uint32_t off = k - (inc - c);
-          addr = b + off;
-          nreal = rl > off ? (rl - off < kRunPad ? rl - off : kRunPad) : 0;
-        }
-        if (inc > kl) break;
-      }
-      if (addr != ~0ULL) {
-        const u32x4 r0 = *reinterpret_cast<const u32x4*>(recs + addr);
-        const u32x4 r1 = *reinterpret_cast<const u32x4*>(recs + addr + 4);
-#pragma unroll
-        for (uint32_t e = 0; e < kRunPad; e++) {
-          if (e < nreal) {
-            const uint32_t rec = e < 4 ? r0[e] : r1[e - 4];
-            atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[rec_word(rec)]),
-                     static_cast<unsigned long long>(rec_mask(s_rmasks, rec)));
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
-  for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
-    const uint64_t v = s_slice[i];
-    if (v) __hip_atomic_fetch_or(dst + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// ---- partitioned probe, C: restore row order -> result bits + per-segment counts (P1's format) -----
-// One 256-thread workgroup per tile: the tile's pass bits (tile_cap / 8 bytes) are staged in LDS while
-// each wave's row positions are already in flight; a lane owns 8 consecutive rows of a segment (one
-// 16-B load of positions) and produces byte `lane` of the segment's 512-bit row-ordered result.
-constexpr int kUnpermuteThreads = 256;
-__global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
-                                                                     const uint8_t* __restrict__ passbits, uint64_t n,
-                                                                     uint64_t tile_cap,
-                                                                     uint64_t* __restrict__ out_bits,
-                                                                     uint32_t* __restrict__ seg_counts,
-                                                                     const uint32_t* __restrict__ dev_n_tiles) {
-  if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;  // bucketed: grid is an upper bound
-  extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
-  constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / (kUnpermuteThreads / 64);
-  const uint64_t tile = blockIdx.x;
-  const uint64_t seg0 = tile * (kTileRows / kSegRows) + wave * kSegsPerWave;
-  u32x4 pv[kSegsPerWave];  // 8 row positions (u16) per lane per segment
-#pragma unroll
-  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
-    pv[sg] = u32x4{0, 0, 0, 0};
-    if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos + (seg0 + sg) * kSegRows + lane * 8);
-  }
-  {
-    const u32x4* src = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / 8));
-    for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
-  }
-  __syncthreads();
-  uint8_t* out_bytes = reinterpret_cast<uint8_t*>(out_bits);
-#pragma unroll
-  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
-    const uint64_t seg = seg0 + sg;
-    if (seg >= n_segs) break;
-    uint32_t byte = 0;
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-      byte |= ((static_cast<uint32_t>(s_pass[p >> 3]) >> (p & 7)) & 1u) << e;
-    }
-    const uint64_t row0 = seg * kSegRows + lane * 8;  // rows >= n (last segment) carry don't-care positions
-    if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
-    out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);
-    if (seg_counts != nullptr) {
-      const uint32_t cnt = wave_sum(__popc(byte));
-      if (lane == 0) seg_counts[seg] = cnt;
-    }
-  }
-}
-
-// ---- bucketed strategy (filters of 2^22..2^31 blocks) ----------------------------------------------
-// Level 1 cuts the rows by 16 MiB filter region ("bucket": 128 slices) into one contiguous hash array
-// per bucket, each padded to whole 16 Ki-row tiles; level 2 is the partitioned pipeline above over
-// those arrays, every bucket against its own 128 slices. bucket = block id >> 21 = hash bits 37...
-__device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t bucket_mask) {
-  return static_cast<uint32_t>(h >> (kLogNumMasks + 6 + kSliceLog + kBucketSliceLog)) & bucket_mask;
-}
-
-// B1: rows per bucket of every 16 Ki-row level-1 tile -> counts_tm[tile][bucket] (+ the build's min/max).
-template <int K, bool DENSE, bool MM>
-__global__ __launch_bounds__(kTileThreads) void bucket_count_kernel(KeyArgs a, uint64_t n, uint32_t bucket_mask,
-                                                                    uint32_t* __restrict__ counts_tm,
-                                                                    int64_t* __restrict__ stats) {
-  __shared__ uint32_t s_cnt[kMaxBuckets];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t nb = bucket_mask + 1;
-  for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_cnt[i] = 0;
-  __syncthreads();
-  const uint64_t tile = blockIdx.x, tile_base = tile * kTileRows;
-  int64_t wmn = kMinInit, wmx = kMaxInit;
-#pragma unroll
-  for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-    const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
-    uint64_t hh[8];
-    bool oo[8];
-    int64_t mm[2] = {kMinInit, kMaxInit};
-    load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
-    if constexpr (MM && K != kKeyHash) {
-      wave_minmax(mm[0], mm[1]);
-      wmn = min(wmn, mm[0]);
-      wmx = max(wmx, mm[1]);
-    }
-#pragma unroll
-    for (int j = 0; j < 8; j++)
-      if (oo[j]) atomicAdd(&s_cnt[bucket_of(hh[j], bucket_mask)], 1u);
-  }
-  if constexpr (MM && K != kKeyHash) publish_minmax(wmn, wmx, stats);
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) counts_tm[tile * nb + i] = s_cnt[i];
-}
-
-// B2: in place, each bucket's row of counts_bm[bucket][tile] becomes its exclusive prefix over tiles
-// (where the tile's run starts inside the bucket's array); totals[bucket] = the bucket's rows.
-__global__ __launch_bounds__(1024) void bucket_scan_kernel(uint32_t* __restrict__ counts_bm, uint64_t n_tiles,
-                                                          uint32_t* __restrict__ totals) {
-  __shared__ uint32_t s_wave[16];
-  uint32_t* row = counts_bm + static_cast<uint64_t>(blockIdx.x) * n_tiles;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t carry = 0;
-  for (uint64_t c0 = 0; c0 < n_tiles; c0 += 1024) {
-    const uint64_t i = c0 + threadIdx.x;
-    const uint32_t v = i < n_tiles ? row[i] : 0u;
-    const uint32_t incl = wave_inclusive_sum(v);
-    if (lane == 63) s_wave[wave] = incl;
-    __syncthreads();
-    uint32_t off = carry, chunk = 0;
-    for (uint32_t w = 0; w < 16; w++) {
-      const uint32_t t = s_wave[w];
-      off += w < wave ? t : 0u;
-      chunk += t;
-    }
-    if (i < n_tiles) row[i] = off + incl - v;
-    carry += chunk;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
-}
-
-// B3: bucket bases in the level-2 array (each bucket padded to whole tiles) and its tile ranges:
-// base[b] (rows), bucket_tiles[b] = base[b] / kTileRows; base[nb], bucket_tiles[nb] = the totals.
-__global__ __launch_bounds__(1024) void bucket_base_kernel(const uint32_t* __restrict__ totals, uint32_t nb,
-                                                          uint64_t* __restrict__ base,
-                                                          uint32_t* __restrict__ bucket_tiles) {
-  __shared__ uint32_t s_wave[16];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t b = threadIdx.x;
-  const uint32_t tiles = b < nb ? static_cast<uint32_t>((totals[b] + kTileRows - 1) / kTileRows) : 0u;
-  const uint32_t incl = wave_inclusive_sum(tiles);
-  if (lane == 63) s_wave[wave] = incl;
-  __syncthreads();
-  uint32_t off = 0, all = 0;
-  for (uint32_t w = 0; w < 16; w++) {
-    off += w < wave ? s_wave[w] : 0u;
-    all += s_wave[w];
-  }
-  const uint32_t first = off + incl - tiles;
-  if (b < nb) {
-    bucket_tiles[b] = first;
-    base[b] = static_cast<uint64_t>(first) * kTileRows;
-  }
-  if (b == 0) {
-    bucket_tiles[nb] = all;
-    base[nb] = static_cast<uint64_t>(all) * kTileRows;
-  }
-}
-
-// B4: hash every row of a level-1 tile again, sort the tile's hashes by bucket in LDS and copy each
-// bucket's run to its place in that bucket's array: hashes[base[b] + pre_tm[tile][b] + i]. pos_out (u16,
-// probe only) records each row's position in the tile's bucket-sorted order.
-template <int K, bool DENSE>
-__global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a, uint64_t n, uint32_t bucket_mask,
-                                                                      const uint32_t* __restrict__ counts_tm,
-                                                                      const uint32_t* __restrict__ pre_tm,
-                                                                      const uint64_t* __restrict__ base,
-                                                                      uint64_t* __restrict__ hashes,
-                                                                      uint16_t* __restrict__ pos_out) {
-  extern __shared__ uint64_t s_h[];  // kTileRows hashes, bucket-sorted
-  __shared__ uint32_t s_start[kMaxBuckets], s_cur[kMaxBuckets];
-  __shared__ uint64_t s_dst[kMaxBuckets];  // where each bucket's run goes in the level-2 array
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t nb = bucket_mask + 1;
-  // Workgroups go round-robin to the 8 XCDs; give each XCD a contiguous range of tiles, so the runs of
-  // neighbouring tiles (adjacent in each bucket's array) are written through the same L2 and leave it
-  // as whole lines.
-  const uint32_t per_xcd = gridDim.x / 8, xcd = blockIdx.x % 8;
-  const uint64_t tile = blockIdx.x < per_xcd * 8 ? static_cast<uint64_t>(xcd) * per_xcd + blockIdx.x / 8 : blockIdx.x;
-  const uint64_t tile_base = tile * kTileRows;
-  const uint32_t* cnt = counts_tm + tile * nb;
-  for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_dst[i] = base[i] + pre_tm[tile * nb + i];
-  if (wave == 0) {  // exclusive scan of this tile's bucket counts, kMaxBuckets / 64 per lane
-    constexpr int kPer = kMaxBuckets / 64;
-    uint32_t c[kPer], t = 0;
-#pragma unroll
-    for (int i = 0; i < kPer; i++) {
-      const uint32_t idx = lane * kPer + i;
-      c[i] = idx < nb ? cnt[idx] : 0u;
-      t += c[i];
-    }
-    uint32_t off = wave_inclusive_sum(t) - t;
-#pragma unroll
-    for (int i = 0; i < kPer; i++) {
-      const uint32_t idx = lane * kPer + i;
-      if (idx < nb) s_start[idx] = s_cur[idx] = off;
-      off += c[i];
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-    const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
-    const uint64_t sbase = tile_base + seg_local;
-    uint64_t hh[8];
-    bool oo[8];
-    load_hashes<K, DENSE>(a, sbase, n, lane, hh, oo);
-    uint16_t pv[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      uint32_t p = 0;
-      if (oo[j]) {
-        p = atomicAdd(&s_cur[bucket_of(hh[j], bucket_mask)], 1u);
-        s_h[p] = hh[j];
-      }
-      pv[j] = static_cast<uint16_t>(p);
-    }
-    if (pos_out != nullptr) {  // padded to whole tiles: rows >= n get don't-care values
-#pragma unroll
-      for (int j = 0; j < 8; j++) pos_out[sbase + seg_row<K, DENSE>(j, lane)] = pv[j];
-    }
-  }
-  __syncthreads();
-  for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {  // LDS only: no global latency in the chain
-    const uint32_t c = s_cur[b] - s_start[b];
-    uint64_t* dst = hashes + s_dst[b];
-    const uint64_t* src = s_h + s_start[b];
-    for (uint32_t i = lane; i < c; i += 64) dst[i] = src[i];
-  }
-}
-
-// B5: pad each bucket's array to whole tiles with copies of its first hash (re-inserting or re-probing
-// a present hash changes nothing, and the pads' results are never read).
-__global__ __launch_bounds__(kBlockThreads) void bucket_pad_kernel(const uint32_t* __restrict__ totals,
-                                                                  const uint64_t* __restrict__ base,
-                                                                  uint64_t* __restrict__ hashes) {
-  const uint32_t b = blockIdx.x;
-  const uint64_t t = totals[b], b0 = base[b], end = base[b + 1];
-  if (t == 0) return;
-  const uint64_t v = hashes[b0];
-  for (uint64_t i = b0 + t + threadIdx.x; i < end; i += kBlockThreads) hashes[i] = v;
-}
-
-// B6: level-1 unpermute. Per level-1 tile: gather the pass bits of its bucket runs out of the level-2
-// result bits (bits2, level-2 array order) into LDS in the tile's bucket-sorted order, 64-bit pieces
-// per item (run, piece), then map every row through its position (pos1) -> result bits + counts.
-constexpr int kBucketUnpermuteThreads = 256;
-__global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kernel(
-    const uint16_t* __restrict__ pos1, const uint64_t* __restrict__ bits2, uint64_t n, uint32_t bucket_mask,
-    const uint32_t* __restrict__ counts_tm, const uint32_t* __restrict__ pre_tm, const uint64_t* __restrict__ base,
-    uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
-  __shared__ uint32_t s_bits[kTileRows / 32];
-  __shared__ uint32_t s_start[kMaxBuckets], s_item[kMaxBuckets + 1], s_cnt[kMaxBuckets];
-  __shared__ uint64_t s_g[kMaxBuckets];
-  __shared__ uint32_t s_wave[kBucketUnpermuteThreads / 64][2];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr uint32_t kWaves = kBucketUnpermuteThreads / 64;
-  const uint32_t nb = bucket_mask + 1;
-  const uint64_t tile = blockIdx.x;
-  const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
-  constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / kWaves;
-  const uint64_t seg0 = tile * (kTileRows / kSegRows) + wave * kSegsPerWave;
-  u32x4 pv[kSegsPerWave];  // row positions, in flight while the bits are staged
-#pragma unroll
-  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
-    pv[sg] = u32x4{0, 0, 0, 0};
-    if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos1 + (seg0 + sg) * kSegRows + lane * 8);
-  }
-  for (uint32_t i = threadIdx.x; i < kTileRows / 32; i += kBucketUnpermuteThreads) s_bits[i] = 0;
-  // per bucket: run length, start in the tile's sorted order, start in bits2, 64-bit pieces (scans by
-  // the whole workgroup, kMaxBuckets / 256 buckets per thread)
-  constexpr int kPer = kMaxBuckets / kBucketUnpermuteThreads;
-  uint32_t c[kPer], k[kPer], tc = 0, tk = 0;
-#pragma unroll
-  for (int i = 0; i < kPer; i++) {
-    const uint32_t b = threadIdx.x * kPer + i;
-    c[i] = b < nb ? counts_tm[tile * nb + b] : 0u;
-    k[i] = (c[i] + 63) / 64;
-    tc += c[i];
-    tk += k[i];
-    if (b < nb) {
-      s_cnt[b] = c[i];
-      s_g[b] = base[b] + pre_tm[tile * nb + b];
-    }
-  }
-  const uint32_t ic = wave_inclusive_sum(tc), ik = wave_inclusive_sum(tk);
-  if (lane == 63) {
-    s_wave[wave][0] = ic;
-    s_wave[wave][1] = ik;
-  }
-  __syncthreads();
-  uint32_t oc = ic - tc, ok_ = ik - tk, total_items = 0;
-  for (uint32_t w = 0; w < kWaves; w++) {
-    oc += w < wave ? s_wave[w][0] : 0u;
-    ok_ += w < wave ? s_wave[w][1] : 0u;
-    total_items += s_wave[w][1];
-  }
-#pragma unroll
-  for (int i = 0; i < kPer; i++) {
-    const uint32_t b = threadIdx.x * kPer + i;
-    if (b < nb) {
-      s_start[b] = oc;
-      s_item[b] = ok_;
-    }
-    oc += c[i];
-    ok_ += k[i];
-  }
-  if (threadIdx.x == 0) s_item[nb] = total_items;
-  __syncthreads();
-  for (uint32_t it = threadIdx.x; it < total_items; it += kBucketUnpermuteThreads) {
-    uint32_t lo = 0, hi = nb;  // last bucket whose first item <= it
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_item[mid] <= it) lo = mid;
-      else hi = mid;
-    }
-    const uint32_t b = lo, piece = it - s_item[b];
-    const uint32_t len = min(64u, s_cnt[b] - piece * 64);
-    const uint64_t q = s_g[b] + piece * 64ULL;
-    const uint32_t sh = static_cast<uint32_t>(q & 63);
-    const uint64_t w0 = bits2[q >> 6];
-    uint64_t v = w0 >> sh;
-    if (sh != 0 && sh + len > 64) v |= bits2[(q >> 6) + 1] << (64 - sh);
-    if (len < 64) v &= (1ULL << len) - 1;
-    const uint32_t d = s_start[b] + piece * 64;  // destination bit in the tile's sorted order
-    const uint32_t dw = d >> 5, ds = d & 31;
-    atomicOr(&s_bits[dw], static_cast<uint32_t>(v << ds));
-    if (len + ds > 32) atomicOr(&s_bits[dw + 1], static_cast<uint32_t>(v >> (32 - ds)));
-    if (len + ds > 64) atomicOr(&s_bits[dw + 2], static_cast<uint32_t>(v >> (64 - ds)));
-  }
-  __syncthreads();
-  uint8_t* out_bytes = reinterpret_cast<uint8_t*>(out_bits);
-#pragma unroll
-  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
-    const uint64_t seg = seg0 + sg;
-    if (seg >= n_segs) break;
-    uint32_t byte = 0;
-#pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-      byte |= ((s_bits[p >> 5] >> (p & 31)) & 1u) << e;
-    }
-    const uint64_t row0 = seg * kSegRows + lane * 8;
-    if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
-    out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);
-    const uint32_t cnt = wave_sum(__popc(byte));
-    if (lane == 0) seg_counts[seg] = cnt;
-  }
-}
-
-// ---- P2a: survivor count per group of 1024 segments --------------------------------------------
-__global__ __launch_bounds__(kBlockThreads) void group_sum_kernel(const uint32_t* __restrict__ seg_counts,
-                                                                 uint64_t n_segs, uint32_t* __restrict__ group_sums) {
-  static_assert(kGroupSegs == kBlockThreads, "one segment count per thread");
-  __shared__ uint32_t s_part[kWavesPerBlock];
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kGroupSegs + threadIdx.x;
-  uint32_t s = i < n_segs ? seg_counts[i] : 0u;
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) group_sums[blockIdx.x] = s_part[0] + s_part[1] + s_part[2] + s_part[3];
-}
-
-// ---- P2b: exclusive scan of the group sums (one 1024-thread workgroup; <= 8192 groups) ----------
-__global__ __launch_bounds__(1024) void group_scan_kernel(const uint32_t* __restrict__ group_sums, uint32_t n_groups,
-                                                         uint32_t* __restrict__ group_offs,
-                                                         uint64_t* __restrict__ out_count) {
-  __shared__ uint32_t s_wave[16];
-  const uint32_t per = (n_groups + 1023) / 1024;
-  const uint32_t first = threadIdx.x * per;
-  uint32_t local = 0;
-  for (uint32_t i = first; i < first + per && i < n_groups; i++) local += group_sums[i];
-  const uint32_t incl = wave_inclusive_sum(local);
-  const uint32_t wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 63) s_wave[wave] = incl;
-  __syncthreads();
-  uint32_t wave_off = 0;
-  for (uint32_t w = 0; w < wave; w++) wave_off += s_wave[w];
-  uint32_t run = wave_off + incl - local;
-  for (uint32_t i = first; i < first + per && i < n_groups; i++) {
-    group_offs[i] = run;
-    run += group_sums[i];
-  }
-  if (threadIdx.x == 1023) {
-    uint32_t total = 0;
-    for (int w = 0; w < 16; w++) total += s_wave[w];
-    *out_count = total;
-  }
-}
-
-// ---- P3: expand result bits into an ascending selection vector ----------------------------------
-__global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* __restrict__ bits,
-                                                               const uint32_t* __restrict__ seg_counts, uint64_t n_segs,
-                                                               const uint32_t* __restrict__ group_offs,
-                                                               const uint32_t* __restrict__ row_sel,
-                                                               uint32_t* __restrict__ out_sel) {
-  __shared__ uint32_t s_off[kGroupSegs];
-  __shared__ uint32_t s_wave[kWavesPerBlock];
-  __shared__ uint16_t s_stage[kWavesPerBlock][8 * kSegRows];  // one 4096-row step per wave (row offsets)
-  const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kGroupSegs;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint64_t sidx = g0 + threadIdx.x;
-  const uint32_t c = sidx < n_segs ? seg_counts[sidx] : 0u;
-  const uint32_t incl = wave_inclusive_sum(c);
-  if (lane == 63) s_wave[wave] = incl;
-  __syncthreads();
-  uint32_t off = group_offs[blockIdx.x] + incl - c;
-  for (uint32_t w = 0; w < wave; w++) off += s_wave[w];
-  s_off[threadIdx.x] = off;
-  __syncthreads();
-  const uint64_t n_words = n_segs * kWordsPerSeg;
-  // Each wave expands 8 segments (64 words = 4096 rows) per step: survivors are first written to the
-  // wave's LDS buffer in row order, then streamed out with coalesced stores.
-  uint16_t* buf = s_stage[wave];
-  constexpr uint32_t kSteps = kGroupSegs / 8 / kWavesPerBlock;
-  uint64_t words[kSteps];  // all of this wave's result words in flight at once
-#pragma unroll
-  for (uint32_t i = 0; i < kSteps; i++) {
-    const uint64_t wi = (g0 + (wave + i * kWavesPerBlock) * 8) * kWordsPerSeg + lane;
-    words[i] = wi < n_words ? bits[wi] : 0ULL;
-  }
-#pragma unroll
-  for (uint32_t i = 0; i < kSteps; i++) {
-    const uint32_t b = wave + i * kWavesPerBlock;
-    const uint64_t seg0 = g0 + b * 8;
-    if (seg0 >= n_segs) break;
-    uint64_t word = words[i];
-    const uint32_t pc = __popcll(word);
-    const uint32_t incl = wave_inclusive_sum(pc);
-    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-    uint32_t p = incl - pc;
-    while (word) {
-      buf[p++] = static_cast<uint16_t>(lane * 64 + __builtin_ctzll(word));
-      word &= word - 1;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    uint32_t* dst = out_sel + s_off[b * 8];
-    const uint32_t step_row = static_cast<uint32_t>(seg0 * kSegRows);
-    for (uint32_t q = lane; q < total; q += 64) {
-      const uint32_t row = step_row + buf[q];
-      dst[q] = row_sel ? row_sel[row] : row;
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// ---- k2: insert ----------------------------------------------------------------------------------
-template <int K, bool DENSE>
-__global__ __launch_bounds__(kBlockThreads) void insert_kernel(uint64_t* __restrict__ words, uint64_t block_mask,
-                                                              KeyArgs a, uint64_t n, uint64_t n_segs,
-                                                              int64_t* __restrict__ stats) {
-  constexpr bool MM = K != kKeyHash;
-  __shared__ uint64_t s_masks[kNumMasks];
-  fill_mask_table(s_masks);
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-  int64_t mm[2] = {kMinInit, kMaxInit};
-  for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6); seg < n_segs;
-       seg += total_waves) {
-    uint64_t h[8];
-    bool ok[8];
-    load_hashes<K, DENSE, MM>(a, seg * kSegRows, n, lane, h, ok, mm);
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      if (ok[j]) {
-        __hip_atomic_fetch_or(words + block_of(h[j], block_mask), mask_of(s_masks, h[j]), __ATOMIC_RELAXED,
-                              __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-  }
-  if constexpr (MM) {
-    wave_minmax(mm[0], mm[1]);
-    publish_minmax(mm[0], mm[1], stats);
-  }
-}
-
-// ---- hashing only (parity / debugging) ---------------------------------------------------------
-template <int K, bool COMBINE>
-__global__ __launch_bounds__(kBlockThreads) void hash_kernel(KeyArgs a, uint64_t n, uint64_t* __restrict__ out) {
-  using Tr = KeyTraits<K>;
-  const typename Tr::T* keys = static_cast<const typename Tr::T*>(a.keys);
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint64_t k = a.key_sel ? a.key_sel[i] : i;
-    uint64_t hv = Tr::hash(keys[k]);
-    if (K != kKeyHash && !valid_at(a.validity, k)) hv = kNullHash;
-    out[i] = COMBINE ? combine_hash(out[i], hv) : hv;
-  }
-}
-
-// ---- k4: OR merge --------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlockThreads) void or_slices_kernel(uint64_t* __restrict__ dst,
-                                                                 const uint64_t* __restrict__ srcs, uint32_t k,
-                                                                 uint64_t n_words, int accumulate) {
-  const uint64_t n_pairs = n_words / 2;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_pairs; i += stride) {
-    u64x2 acc = accumulate ? reinterpret_cast<const u64x2*>(dst)[i] : u64x2{0, 0};
-    for (uint32_t s = 0; s < k; s++) acc |= reinterpret_cast<const u64x2*>(srcs + s * n_words)[i];
-    reinterpret_cast<u64x2*>(dst)[i] = acc;
-  }
-  if ((n_words & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-    uint64_t acc = accumulate ? dst[n_words - 1] : 0ULL;
-    for (uint32_t s = 0; s < k; s++) acc |= srcs[s * n_words + n_words - 1];
-    dst[n_words - 1] = acc;
-  }
-}
-
-// ---- popcount ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlockThreads) void popcount_kernel(const uint64_t* __restrict__ w, uint64_t n_words,
-                                                                unsigned long long* __restrict__ out) {
-  __shared__ uint32_t s_part[kWavesPerBlock];
-  uint32_t s = 0;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_words;
-       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
-    s += __popcll(w[i]);
-  s = wave_sum(s);
-  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    atomicAdd(out, static_cast<unsigned long long>(s_part[0]) + s_part[1] + s_part[2] + s_part[3]);
-  }
-}
-
-// ---- synthetic workload (bench / tests) ----------------------------------------------
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-  return z ^ (z >> 31);
-}
-__device__ __forceinline__ uint64_t sm64(uint64_t seed, uint64_t i) { return mix64(seed + (i + 1) * 0x9e3779b97f4a7c15ULL); }
-
-__global__ __launch_bounds__(kBlockThreads) void synth_build_kernel(int64_t* __restrict__ out, uint64_t start,
-                                                                   uint64_t n) {
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
-    out[i] = static_cast<int64_t>(sm64(RPT_SYNTH_SEED_BUILD, start + i));
-}
-
-__global__ __launch_bounds__(kBlockThreads) void synth_probe_kernel(int64_t* __restrict__ out, uint64_t n_build,
-                                                                   uint32_t p_permille, uint64_t start, uint64_t n) {
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
-       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint64_t r = start + i;
-    const uint64_t u = sm64(RPT_SYNTH_SEED_PROBE_SEL, r);
-    out[i] = (n_build > 0 && (u % 1000) < p_permille)
-                 ? static_cast<int64_t>(sm64(RPT_SYNTH_SEED_BUILD, (u >> 20) % n_build))
-                 : static_cast<int64_t>(sm64(RPT_SYNTH_SEED_PROBE_MISS, r));
-  }
-}
-
-}  // namespace rpt
+#include "kernels/common.hpp"
+#include "kernels/probe_direct.hpp"
+#include "kernels/partitioned.hpp"
+#include "kernels/bucketed.hpp"
+#include "kernels/compaction.hpp"
+#include "kernels/misc.hpp"
 
 // =================================================================================================
 // Host side
