@@ -340,3 +340,24 @@ def test_full_size_probe_properties(rpt, n_probe, n_build, p, strategy):
     assert p / 1000 <= rate < p / 1000 + 0.05
     del probe, sel_t, bits, sel
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("strategy", ["partitioned", "gather"])
+def test_row_ids_beyond_int32(rpt, strategy):
+    """n > 2^31 rows (sel_t is uint32): ids past 2^31 stay exact, ascending, and match the oracle."""
+    n_build, n_probe = 10**7, (1 << 31) + (1 << 20) + 12345
+    build = rpt.synth_build_keys(n_build)
+    bf = with_strategy(rpt.BloomFilter(n_build), strategy)
+    bf.insert(build)
+    w = bf.export_words()
+    lnb = bf.log_num_blocks
+    probe = rpt.synth_probe_keys(n_probe, n_build, 100)
+    sel_t, cnt = bf.probe_async(probe)
+    count = int(cnt.item())
+    sel = sel_t[:count].cpu().numpy().view(np.uint32).astype(np.int64)
+    assert np.all(sel[1:] > sel[:-1]) and sel[-1] < n_probe and sel[-1] >= (1 << 31)
+    for lo, hi in [(0, 10**6), ((1 << 31) - 500_000, (1 << 31) + 500_000), (n_probe - 10**6, n_probe)]:
+        _window_check(bf, w, lnb, probe, sel, lo, hi)
+    assert 0.1 <= count / n_probe < 0.15
+    del probe, sel_t
+    torch.cuda.empty_cache()
