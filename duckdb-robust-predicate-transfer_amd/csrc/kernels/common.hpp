@@ -181,4 +181,47 @@ __device__ __forceinline__ void publish_minmax(int64_t mn, int64_t mx, int64_t* 
   }
 }
 constexpr int64_t kMinInit = INT64_MAX, kMaxInit = INT64_MIN;  // "no value yet"
+// The 8 pass flags a lane holds for a 512-row segment, in load_hashes<K, DENSE> order -> the segment's
+// row-ordered result words (8 x 64 bits, Arrow Find layout) and its survivor count.
+template <int K, bool DENSE>
+__device__ __forceinline__ void store_segment_bits(const bool (&pass)[8], uint32_t lane, uint64_t seg,
+                                                   uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
+  uint64_t word[8];
+  uint32_t cnt = 0;
+  if constexpr (DENSE) {
+    constexpr int V = KeyTraits<K>::kVec;
+    uint64_t b[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      b[j] = ballot64(pass[j]);
+      cnt += __popcll(b[j]);
+    }
+#pragma unroll
+    for (int c = 0; c < 8 / V; c++) {
+#pragma unroll
+      for (int q = 0; q < V; q++) {
+        uint64_t x = 0;
+        if constexpr (V == 2) {
+          x = spread2(b[c * 2 + 0] >> (32 * q)) | (spread2(b[c * 2 + 1] >> (32 * q)) << 1);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; e++) x |= spread4(b[c * 4 + e] >> (16 * q)) << e;
+        }
+        word[c * V + q] = x;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      word[j] = ballot64(pass[j]);
+      cnt += __popcll(word[j]);
+    }
+  }
+  uint64_t mine = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) mine = (lane == static_cast<uint32_t>(j)) ? word[j] : mine;
+  if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
+  if (seg_counts != nullptr && lane == 0) seg_counts[seg] = cnt;
+}
+
 }  // namespace rpt

@@ -37,42 +37,10 @@ __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_
         w[j] = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
       }
     }
-    uint64_t word[8];
-    uint32_t cnt = 0;
-    if constexpr (DENSE) {
-      constexpr int V = KeyTraits<K>::kVec;
-      uint64_t b[8];
+    bool pass[8];
 #pragma unroll
-      for (int j = 0; j < 8; j++) {
-        b[j] = ballot64(ok[j] && (w[j] & m[j]) == m[j]);
-        cnt += __popcll(b[j]);
-      }
-#pragma unroll
-      for (int c = 0; c < 8 / V; c++) {
-#pragma unroll
-        for (int q = 0; q < V; q++) {
-          uint64_t x = 0;
-          if constexpr (V == 2) {
-            x = spread2(b[c * 2 + 0] >> (32 * q)) | (spread2(b[c * 2 + 1] >> (32 * q)) << 1);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 4; e++) x |= spread4(b[c * 4 + e] >> (16 * q)) << e;
-          }
-          word[c * V + q] = x;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        word[j] = ballot64(ok[j] && (w[j] & m[j]) == m[j]);
-        cnt += __popcll(word[j]);
-      }
-    }
-    uint64_t mine = 0;
-#pragma unroll
-    for (int j = 0; j < 8; j++) mine = (lane == static_cast<uint32_t>(j)) ? word[j] : mine;
-    if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
-    if (seg_counts != nullptr && lane == 0) seg_counts[seg] = cnt;
+    for (int j = 0; j < 8; j++) pass[j] = ok[j] && (w[j] & m[j]) == m[j];
+    store_segment_bits<K, DENSE>(pass, lane, seg, out_bits, seg_counts);
   }
 }
 }  // namespace rpt
