@@ -4,9 +4,11 @@
 // CREATE_BF: 4 sink threads, 2048-row chunks (last one ragged), FLAT/CONSTANT/DICTIONARY vectors with
 // NULLs, an under-estimated cardinality so Finalize must ReinitializeAndRehash; then USE_BF with two
 // filters (chain = AND), the empty-build early exit, the not-finalized skip and passthrough; the
-// build's min/max dynamic filter; a composite (two-column) key filter.
+// build's min/max dynamic filter; a composite (two-column) key filter; a 256 MiB filter whose
+// batched insert and lookup take the bucketed strategy.
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <random>
 #include <thread>
@@ -309,6 +311,47 @@ int main() {
         const uint64_t ne = rpt_oracle_lookup_sel_hashes(wc.data(), lc, ph.data(), ch.count, exp.data());
         EXPECT(out == std::vector<uint32_t>(exp.begin(), exp.begin() + ne), "composite probe at row %zu", base);
         base += ch.count;
+      }
+    }
+    // ---------------- a 256 MiB filter: batched insert / lookup take the bucketed strategy ----------
+    {
+      const size_t nbig = 5000000;
+      std::vector<int64_t> keys(nbig);
+      std::mt19937_64 rng(9);
+      for (auto& k : keys) k = static_cast<int64_t>(rng());
+      std::vector<rpt::DataChunk> chunks;
+      for (size_t lo = 0; lo < nbig; lo += 500000) {
+        rpt::DataChunk ch;
+        ch.count = std::min<size_t>(500000, nbig - lo);
+        rpt::Vector v;
+        v.key_type = rpt::KeyType::I64;
+        v.data = keys.data() + lo;
+        ch.data.push_back(v);
+        chunks.push_back(ch);
+      }
+      std::vector<const rpt::DataChunk*> ptrs;
+      for (const auto& c : chunks) ptrs.push_back(&c);
+      rpt::PTBloomFilter fb;
+      fb.Initialize(dev, 1u << 28);  // 2^28 rows -> 2^25 blocks (256 MiB)
+      EXPECT(fb.LogNumBlocks() == 25, "big filter log blocks %d", fb.LogNumBlocks());
+      EXPECT(rpt_bf_insert_strategy_for(fb.native(), nbig) == RPT_INSERT_BUCKETED, "bucketed insert expected");
+      fb.InsertBatch(ctx, ptrs, {0});
+      std::vector<uint64_t> wb(1ULL << 25, 0);
+      rpt_oracle_insert_i64(wb.data(), 25, keys.data(), nullptr, nullptr, nbig);
+      EXPECT(fb.ExportWords() == wb, "bucketed insert words differ from the oracle");
+      int64_t mn = 0, mx = 0;
+      EXPECT(fb.MinMax(mn, mx) && mn == *std::min_element(keys.begin(), keys.end()) &&
+                 mx == *std::max_element(keys.begin(), keys.end()), "bucketed insert min/max");
+      // probe the same rows plus fresh ones, as one batch (bucketed) -- every build key must pass
+      for (size_t i = 0; i < nbig; i += 2) keys[i] = static_cast<int64_t>(rng());
+      EXPECT(rpt_bf_probe_strategy_for(fb.native(), nbig) == RPT_PROBE_BUCKETED, "bucketed probe expected");
+      std::vector<rpt::SelectionVector> sels;
+      fb.LookupSelBatch(ctx, ptrs, sels, {0});
+      std::vector<uint32_t> exp(500000);
+      for (size_t k = 0; k < chunks.size(); k++) {
+        const uint64_t ne = rpt_oracle_probe_i64(wb.data(), 25, keys.data() + k * 500000, nullptr, nullptr,
+                                                 chunks[k].count, exp.data());
+        EXPECT(sels[k] == std::vector<uint32_t>(exp.begin(), exp.begin() + ne), "bucketed probe chunk %zu", k);
       }
     }
   } catch (const std::exception& e) {
