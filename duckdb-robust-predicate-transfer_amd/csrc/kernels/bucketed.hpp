@@ -32,7 +32,7 @@ __global__ __launch_bounds__(kTileThreads) void bucket_count_kernel(KeyArgs a, u
     bool oo[8];
     int64_t mm[2] = {kMinInit, kMaxInit};
     load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
-    if constexpr (MM && K != kKeyHash) {
+    if constexpr (MM && KeyTraits<K>::kValues) {
       wave_minmax(mm[0], mm[1]);
       wmn = min(wmn, mm[0]);
       wmx = max(wmx, mm[1]);
@@ -41,7 +41,7 @@ __global__ __launch_bounds__(kTileThreads) void bucket_count_kernel(KeyArgs a, u
     for (int j = 0; j < 8; j++)
       if (oo[j]) atomicAdd(&s_cnt[bucket_of(hh[j], bucket_mask)], 1u);
   }
-  if constexpr (MM && K != kKeyHash) publish_minmax(wmn, wmx, stats);
+  if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) counts_tm[tile * nb + i] = s_cnt[i];
 }
@@ -102,16 +102,19 @@ __global__ __launch_bounds__(1024) void bucket_base_kernel(const uint32_t* __res
 }
 
 // B4: hash every row of a level-1 tile again, sort the tile's hashes by bucket in LDS and copy each
-// bucket's run to its place in that bucket's array: hashes[base[b] + pre_tm[tile][b] + i]. pos_out (u16,
-// probe only) records each row's position in the tile's bucket-sorted order.
+// bucket's run to its place in that bucket's array (index base[b] + pre_tm[tile][b] + i), as the
+// level-2 kKeySplit layout: hash bits 0..31 in hash_lo, bits 32..39 in hash_hi. pos_out (u16, probe
+// only) records each row's position in the tile's bucket-sorted order.
 template <int K, bool DENSE>
 __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a, uint64_t n, uint32_t bucket_mask,
                                                                       const uint32_t* __restrict__ counts_tm,
                                                                       const uint32_t* __restrict__ pre_tm,
                                                                       const uint64_t* __restrict__ base,
-                                                                      uint64_t* __restrict__ hashes,
+                                                                      uint32_t* __restrict__ hash_lo,
+                                                                      uint8_t* __restrict__ hash_hi,
                                                                       uint16_t* __restrict__ pos_out) {
-  extern __shared__ uint64_t s_h[];  // kTileRows hashes, bucket-sorted
+  extern __shared__ uint32_t s_lo[];  // kTileRows hash words (bits 0..31), bucket-sorted, then
+  uint8_t* s_hi = reinterpret_cast<uint8_t*>(s_lo + kTileRows);  // their bits 32..39
   __shared__ uint32_t s_start[kMaxBuckets], s_cur[kMaxBuckets];
   __shared__ uint64_t s_dst[kMaxBuckets];  // where each bucket's run goes in the level-2 array
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -155,7 +158,8 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
       uint32_t p = 0;
       if (oo[j]) {
         p = atomicAdd(&s_cur[bucket_of(hh[j], bucket_mask)], 1u);
-        s_h[p] = hh[j];
+        s_lo[p] = static_cast<uint32_t>(hh[j]);
+        s_hi[p] = static_cast<uint8_t>(hh[j] >> 32);
       }
       pv[j] = static_cast<uint16_t>(p);
     }
@@ -166,10 +170,12 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
   }
   __syncthreads();
   for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {  // LDS only: no global latency in the chain
-    const uint32_t c = s_cur[b] - s_start[b];
-    uint64_t* dst = hashes + s_dst[b];
-    const uint64_t* src = s_h + s_start[b];
-    for (uint32_t i = lane; i < c; i += 64) dst[i] = src[i];
+    const uint32_t c = s_cur[b] - s_start[b], s0 = s_start[b];
+    const uint64_t d = s_dst[b];
+    for (uint32_t i = lane; i < c; i += 64) {
+      hash_lo[d + i] = s_lo[s0 + i];
+      hash_hi[d + i] = s_hi[s0 + i];
+    }
   }
 }
 
@@ -177,12 +183,17 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
 // a present hash changes nothing, and the pads' results are never read).
 __global__ __launch_bounds__(kBlockThreads) void bucket_pad_kernel(const uint32_t* __restrict__ totals,
                                                                   const uint64_t* __restrict__ base,
-                                                                  uint64_t* __restrict__ hashes) {
+                                                                  uint32_t* __restrict__ hash_lo,
+                                                                  uint8_t* __restrict__ hash_hi) {
   const uint32_t b = blockIdx.x;
   const uint64_t t = totals[b], b0 = base[b], end = base[b + 1];
   if (t == 0) return;
-  const uint64_t v = hashes[b0];
-  for (uint64_t i = b0 + t + threadIdx.x; i < end; i += kBlockThreads) hashes[i] = v;
+  const uint32_t lo = hash_lo[b0];
+  const uint8_t hi = hash_hi[b0];
+  for (uint64_t i = b0 + t + threadIdx.x; i < end; i += kBlockThreads) {
+    hash_lo[i] = lo;
+    hash_hi[i] = hi;
+  }
 }
 
 // B6: level-1 unpermute. Per level-1 tile: gather the pass bits of its bucket runs out of the level-2

@@ -57,6 +57,7 @@ struct KeyArgs {
   const uint32_t* key_sel;
   const uint64_t* validity;
   const uint32_t* row_sel;
+  const uint8_t* hi8 = nullptr;  // kKeySplit only: hash bits 32..39 per row
 };
 
 __device__ __forceinline__ bool valid_at(const uint64_t* validity, uint64_t idx) {
@@ -101,14 +102,22 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
       }
       // validity bits of this lane's V rows, shifted down to bits 0..V-1 (V | 64: one word)
       uint32_t vbits = (1u << V) - 1;
-      if (K != kKeyHash && vb != nullptr && off < rem) vbits = static_cast<uint32_t>(vb[off >> 6] >> (off & 63));
+      if (Tr::kValues && vb != nullptr && off < rem) vbits = static_cast<uint32_t>(vb[off >> 6] >> (off & 63));
+      uint32_t hi4 = 0;  // kKeySplit: the V rows' hash bits 32..39
+      if constexpr (K == kKeySplit) {
+        const uint8_t* hb = a.hi8 + base;
+        if (off + V <= rem) hi4 = *reinterpret_cast<const uint32_t*>(hb + off);
+        else
+          for (int e = 0; e < V; e++) hi4 |= (off + e < rem ? static_cast<uint32_t>(hb[off + e]) : 0u) << (8 * e);
+      }
 #pragma unroll
       for (int e = 0; e < V; e++) {
         ok[c * V + e] = off + e < rem;
         uint64_t hv = Tr::hash(v[e]);
-        if (K != kKeyHash && !((vbits >> e) & 1u)) hv = kNullHash;
+        if constexpr (K == kKeySplit) hv |= static_cast<uint64_t>((hi4 >> (8 * e)) & 0xFFu) << 32;
+        if (Tr::kValues && !((vbits >> e) & 1u)) hv = kNullHash;
         h[c * V + e] = hv;
-        if constexpr (MM && K != kKeyHash) {
+        if constexpr (MM && Tr::kValues) {
           if (off + e < rem && ((vbits >> e) & 1u)) {
             mm[0] = min(mm[0], static_cast<int64_t>(v[e]));
             mm[1] = max(mm[1], static_cast<int64_t>(v[e]));
@@ -129,9 +138,10 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
         const uint64_t k = a.key_sel ? a.key_sel[r] : r;
         const T kv = keys[k];
         hv = Tr::hash(kv);
+        if constexpr (K == kKeySplit) hv |= static_cast<uint64_t>(a.hi8[k]) << 32;
         const bool valid = valid_at(a.validity, k);
-        if (K != kKeyHash && !valid) hv = kNullHash;
-        if constexpr (MM && K != kKeyHash) {
+        if (Tr::kValues && !valid) hv = kNullHash;
+        if constexpr (MM && Tr::kValues) {
           if (valid) {
             mm[0] = min(mm[0], static_cast<int64_t>(kv));
             mm[1] = max(mm[1], static_cast<int64_t>(kv));

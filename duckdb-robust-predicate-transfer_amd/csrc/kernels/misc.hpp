@@ -10,7 +10,7 @@ template <int K, bool DENSE>
 __global__ __launch_bounds__(kBlockThreads) void insert_kernel(uint64_t* __restrict__ words, uint64_t block_mask,
                                                               KeyArgs a, uint64_t n, uint64_t n_segs,
                                                               int64_t* __restrict__ stats) {
-  constexpr bool MM = K != kKeyHash;
+  constexpr bool MM = KeyTraits<K>::kValues;
   __shared__ uint64_t s_masks[kNumMasks];
   fill_mask_table(s_masks);
   __syncthreads();
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(kBlockThreads) void hash_kernel(KeyArgs a, uint64_t
        i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const uint64_t k = a.key_sel ? a.key_sel[i] : i;
     uint64_t hv = Tr::hash(keys[k]);
-    if (K != kKeyHash && !valid_at(a.validity, k)) hv = kNullHash;
+    if (KeyTraits<K>::kValues && !valid_at(a.validity, k)) hv = kNullHash;
     out[i] = COMBINE ? combine_hash(out[i], hv) : hv;
   }
 }

@@ -82,7 +82,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
       bool oo[8];
       int64_t mm[2] = {kMinInit, kMaxInit};
       load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
-      if constexpr (MM && K != kKeyHash) {
+      if constexpr (MM && KeyTraits<K>::kValues) {
         wave_minmax(mm[0], mm[1]);
         wmn = min(wmn, mm[0]);
         wmx = max(wmx, mm[1]);
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
         if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
       }
     }
-    if constexpr (MM && K != kKeyHash) publish_minmax(wmn, wmx, stats);
+    if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
     __syncthreads();
     if (wave == 0) {  // exclusive scan of the slice counts, each padded to 4 records: kMaxSliceCount/64 per lane
       constexpr int kPer = kMaxSliceCount / 64;

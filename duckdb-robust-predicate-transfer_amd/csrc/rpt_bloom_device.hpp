@@ -63,18 +63,22 @@ __device__ __forceinline__ uint64_t block_of(uint64_t h, uint64_t block_mask) {
   return (h >> (kLogNumMasks + 6)) & block_mask;
 }
 
-// Key types (rpt_key_type).
-enum KeyKind : int { kKeyI64 = 0, kKeyI32 = 1, kKeyHash = 2 };
+// Key types (rpt_key_type), plus kKeySplit: the bucketed strategy's level-2 input, the low 32 bits
+// of each row's hash (keys) with hash bits 32..39 in a parallel byte array (KeyArgs::hi8) -- the 37
+// bits a 16 MiB bucket's slices need, in 5 bytes instead of 8.
+enum KeyKind : int { kKeyI64 = 0, kKeyI32 = 1, kKeyHash = 2, kKeySplit = 3 };
 
 template <int K> struct KeyTraits;
 template <> struct KeyTraits<kKeyI64> {
   using T = int64_t;
-  static constexpr int kVec = 2;  // keys per 16-byte load
+  static constexpr int kVec = 2;         // keys per 16-byte load
+  static constexpr bool kValues = true;  // key values: validity (NULL_HASH) and min/max apply
   __device__ static __forceinline__ uint64_t hash(T v) { return murmur64(static_cast<uint64_t>(v)); }
 };
 template <> struct KeyTraits<kKeyI32> {
   using T = int32_t;
   static constexpr int kVec = 4;
+  static constexpr bool kValues = true;
   __device__ static __forceinline__ uint64_t hash(T v) {
     return murmur64(static_cast<uint64_t>(static_cast<uint32_t>(v)));
   }
@@ -82,7 +86,14 @@ template <> struct KeyTraits<kKeyI32> {
 template <> struct KeyTraits<kKeyHash> {
   using T = uint64_t;
   static constexpr int kVec = 2;
+  static constexpr bool kValues = false;
   __device__ static __forceinline__ uint64_t hash(T v) { return v; }
+};
+template <> struct KeyTraits<kKeySplit> {
+  using T = uint32_t;
+  static constexpr int kVec = 4;
+  static constexpr bool kValues = false;
+  __device__ static __forceinline__ uint64_t hash(T v) { return v; }  // | hi8 << 32, added by the loader
 };
 
 // Spread the low 32 bits of x so that bit i lands on bit 2i (wave-uniform: scalar ALU).

@@ -192,7 +192,8 @@ struct ProbeWorkspace {
   uint32_t* totals;        // [bucket] rows
   uint64_t* bbase;         // [bucket + 1] first row of the bucket in the level-2 array
   uint32_t* bucket_tiles;  // [bucket + 1] first level-2 tile of the bucket; [nb] = level-2 tile count
-  uint64_t* hashes;        // level-2 array: per bucket, its rows' hashes padded to whole tiles
+  uint32_t* hash_lo;       // level-2 array (kKeySplit): per bucket, its rows' hashes padded to whole
+  uint8_t* hash_hi;        // tiles -- bits 0..31 and bits 32..39
   uint16_t* pos1;          // row -> position in its level-1 tile's bucket-sorted order
   uint64_t* bits2;         // level-2 result bits (level-2 array order)
 };
@@ -269,9 +270,10 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     sz[12] = align256(nb * 4);
     sz[13] = align256((nb + 1) * 8);
     sz[14] = align256((nb + 1) * 4);
-    sz[15] = align256(t2 * T * 8);
+    sz[15] = align256(t2 * T * 4);
     sz[16] = align256(t1 * T * 2);
     sz[17] = align256(t2 * T / 8);
+    sz[18] = align256(t2 * T);
   }
   size_t off[kParts], total = 0;
   for (int i = 0; i < kParts; i++) {
@@ -296,9 +298,10 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     ws->totals = static_cast<uint32_t*>(at(12));
     ws->bbase = static_cast<uint64_t*>(at(13));
     ws->bucket_tiles = static_cast<uint32_t*>(at(14));
-    ws->hashes = static_cast<uint64_t*>(at(15));
+    ws->hash_lo = static_cast<uint32_t*>(at(15));
     ws->pos1 = static_cast<uint16_t*>(at(16));
     ws->bits2 = static_cast<uint64_t*>(at(17));
+    ws->hash_hi = static_cast<uint8_t*>(at(18));
   }
   return total;
 }
@@ -315,7 +318,8 @@ struct InsertWorkspace {
   uint32_t* totals;
   uint64_t* bbase;
   uint32_t* bucket_tiles;
-  uint64_t* hashes;
+  uint32_t* hash_lo;
+  uint8_t* hash_hi;
 };
 
 size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base, InsertWorkspace* ws) {
@@ -324,7 +328,7 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
   const uint64_t T = rpt::kTileRows;
   const uint64_t tiles = buck ? level2_tiles_max(n, log_num_blocks) : ceil_div(n, T);
   const uint32_t slices = buck ? rpt::kBucketSlices : slice_count(log_num_blocks);
-  constexpr int kParts = 10;
+  constexpr int kParts = 11;
   size_t sz[kParts] = {align256(tiles * rpt::tile_cap_for(slices) * 4), align256(static_cast<uint64_t>(slices) * tiles * 4),
                        align256(static_cast<uint64_t>(slices) * tiles * 4)};
   if (buck) {
@@ -333,7 +337,8 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
     sz[6] = align256(nb * 4);
     sz[7] = align256((nb + 1) * 8);
     sz[8] = align256((nb + 1) * 4);
-    sz[9] = align256(tiles * T * 8);
+    sz[9] = align256(tiles * T * 4);
+    sz[10] = align256(tiles * T);
   }
   size_t off[kParts], total = 0;
   for (int i = 0; i < kParts; i++) {
@@ -352,7 +357,8 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
     ws->totals = static_cast<uint32_t*>(at(6));
     ws->bbase = static_cast<uint64_t*>(at(7));
     ws->bucket_tiles = static_cast<uint32_t*>(at(8));
-    ws->hashes = static_cast<uint64_t*>(at(9));
+    ws->hash_lo = static_cast<uint32_t*>(at(9));
+    ws->hash_hi = static_cast<uint8_t*>(at(10));
   }
   return total;
 }
@@ -428,7 +434,7 @@ template <int K, bool D>
 void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
                         uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
                         const uint32_t* dev_n_tiles) {
-  if (K != rpt::kKeyHash && stats != nullptr)
+  if (rpt::KeyTraits<K>::kValues && stats != nullptr)
     launch_partition_mm<K, D, true>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
   else
     launch_partition_mm<K, D, false>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, nullptr, dev_n_tiles);
@@ -443,7 +449,7 @@ void launch_insert_t(unsigned grid, hipStream_t s, rpt_bf* bf, const rpt::KeyArg
 template <int K, bool D>
 void launch_bucket_count_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
                            uint32_t* counts_tm, int64_t* stats) {
-  if (K != rpt::kKeyHash && stats != nullptr)
+  if (rpt::KeyTraits<K>::kValues && stats != nullptr)
     hipLaunchKernelGGL((rpt::bucket_count_kernel<K, D, true>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n,
                        bucket_mask, counts_tm, stats);
   else
@@ -453,13 +459,13 @@ void launch_bucket_count_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, 
 
 template <int K, bool D>
 void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
-                             const uint32_t* counts_tm, const uint32_t* pre_tm, const uint64_t* bbase, uint64_t* hashes,
-                             uint16_t* pos1) {
-  const size_t lds = rpt::kTileRows * 8;
+                             const uint32_t* counts_tm, const uint32_t* pre_tm, const uint64_t* bbase, uint32_t* hash_lo,
+                             uint8_t* hash_hi, uint16_t* pos1) {
+  const size_t lds = rpt::kTileRows * 5;
   static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into (160 KiB minus the static part)
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D>)); });
   hipLaunchKernelGGL((rpt::bucket_scatter_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, bucket_mask,
-                     counts_tm, pre_tm, bbase, hashes, pos1);
+                     counts_tm, pre_tm, bbase, hash_lo, hash_hi, pos1);
 }
 
 #define RPT_DISPATCH_KD(fn, kt, dense, ...)                  \
@@ -496,7 +502,9 @@ int transpose_u32(hipStream_t s, const uint32_t* in, uint64_t rows, uint64_t col
 // tile's bucket-sorted order when pos1 != nullptr), each array padded to whole tiles.
 struct BucketLevel1 {
   uint32_t *counts_tm, *pre_bm, *pre_tm, *totals, *bucket_tiles;
-  uint64_t *bbase, *hashes;
+  uint64_t* bbase;
+  uint32_t* hash_lo;
+  uint8_t* hash_hi;
   uint16_t* pos1;
 };
 int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool dense, uint64_t n, int L,
@@ -523,8 +531,9 @@ int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool d
   {
     ProfScope prof_x("bucket_scatter_kernel", s);
     RPT_DISPATCH_KD(launch_bucket_scatter_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm,
-                    w.pre_tm, w.bbase, w.hashes, w.pos1);
-    hipLaunchKernelGGL(rpt::bucket_pad_kernel, dim3(nb), dim3(rpt::kBlockThreads), 0, s, w.totals, w.bbase, w.hashes);
+                    w.pre_tm, w.bbase, w.hash_lo, w.hash_hi, w.pos1);
+    hipLaunchKernelGGL(rpt::bucket_pad_kernel, dim3(nb), dim3(rpt::kBlockThreads), 0, s, w.totals, w.bbase, w.hash_lo,
+                       w.hash_hi);
     prof_x.end();
     RPT_LAUNCHED("bucket_scatter_kernel");
   }
@@ -851,14 +860,15 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   const uint32_t* dev_n_tiles = nullptr;
   uint32_t grid_slices = tile_slices;
   if (buck) {
-    const BucketLevel1 l1{ws.counts_tm, ws.pre_bm, ws.pre_tm, ws.totals, ws.bucket_tiles, ws.bbase, ws.hashes, nullptr};
+    const BucketLevel1 l1{ws.counts_tm, ws.pre_bm, ws.pre_tm, ws.totals, ws.bucket_tiles, ws.bbase, ws.hash_lo, ws.hash_hi,
+                          nullptr};
     st = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, bf->stats);
     if (st != RPT_OK) return st;
     tile_slices = rpt::kBucketSlices;
     n_tiles = level2_tiles_max(n, L);
     n_part = n_tiles * rpt::kTileRows;
-    pa = rpt::KeyArgs{ws.hashes, nullptr, nullptr, nullptr};
-    p_type = RPT_KEY_HASH;
+    pa = rpt::KeyArgs{ws.hash_lo, nullptr, nullptr, nullptr, ws.hash_hi};
+    p_type = rpt::kKeySplit;
     p_dense = true;
     p_stats = nullptr;  // min/max came from the key read of level 1
     bucket_tiles = ws.bucket_tiles;
@@ -866,8 +876,12 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
     grid_slices = bucket_count(L) * rpt::kBucketSlices;
   }
   ProfScope prof_p("partition_kernel", s);
-  RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
-                  n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, p_stats, dev_n_tiles);
+  if (p_type == rpt::kKeySplit)
+    launch_partition_t<rpt::kKeySplit, true>(static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1, n_tiles,
+                                             ws.recs, nullptr, ws.runs_tm, p_stats, dev_n_tiles);
+  else
+    RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
+                    n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, p_stats, dev_n_tiles);
   prof_p.end();
   RPT_LAUNCHED("partition_kernel");
   st = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
@@ -951,15 +965,16 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     uint64_t* part_bits = ws.bits;
     uint32_t* part_counts = ws.seg_counts;
     if (buck) {
-      const BucketLevel1 l1{ws.counts_tm, ws.pre_bm, ws.pre_tm, ws.totals, ws.bucket_tiles, ws.bbase, ws.hashes, ws.pos1};
+      const BucketLevel1 l1{ws.counts_tm, ws.pre_bm, ws.pre_tm, ws.totals, ws.bucket_tiles, ws.bbase, ws.hash_lo,
+                            ws.hash_hi, ws.pos1};
       int st1 = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, nullptr);
       if (st1 != RPT_OK) return st1;
       tile_slices = rpt::kBucketSlices;
       grid_slices = bucket_count(L) * rpt::kBucketSlices;
       n_tiles = level2_tiles_max(n, L);
       n_part = n_tiles * rpt::kTileRows;
-      pa = rpt::KeyArgs{ws.hashes, nullptr, nullptr, nullptr};
-      p_type = RPT_KEY_HASH;
+      pa = rpt::KeyArgs{ws.hash_lo, nullptr, nullptr, nullptr, ws.hash_hi};
+      p_type = rpt::kKeySplit;
       p_dense = true;
       bucket_tiles = ws.bucket_tiles;
       dev_n_tiles = ws.bucket_tiles + bucket_count(L);
@@ -968,8 +983,12 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     }
     const int cus = num_cus(bf->device);
     ProfScope prof5_("partition_kernel", s);
-    RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
-                    n_tiles, ws.recs, ws.pos, ws.runs_tm, static_cast<int64_t*>(nullptr), dev_n_tiles);
+    if (p_type == rpt::kKeySplit)
+      launch_partition_t<rpt::kKeySplit, true>(static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1, n_tiles,
+                                               ws.recs, ws.pos, ws.runs_tm, nullptr, dev_n_tiles);
+    else
+      RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
+                      n_tiles, ws.recs, ws.pos, ws.runs_tm, static_cast<int64_t*>(nullptr), dev_n_tiles);
     prof5_.end();
     RPT_LAUNCHED("partition_kernel");
     int st2 = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
