@@ -81,16 +81,21 @@ def allreduce_or_filter(bf, group=None) -> None:
         or_allreduce_words(host, group, or_slices=cpu_or_slices)
         buf.copy_(host)
     bf.copy_words_from(buf)
-    # has_data (OR) and the min/max dynamic filter (min / max) in ONE MIN all-reduce: the max and the
-    # flag are sent bit-complemented (~x = -x-1 reverses order without overflow).
-    mm = bf.minmax()
+    mm, has = allreduce_minmax_flag(bf.minmax(), not bf.is_empty(), group,
+                                    device=bf.device if on_device else torch.device("cpu"))
+    bf.set_minmax(mm)
+    bf.set_has_data(has)
+
+
+def allreduce_minmax_flag(mm: Optional[tuple], has_data: bool, group=None, device=None):
+    """Combine per-rank (min, max) (or None) and has_data flags across ranks in ONE MIN all-reduce:
+    the max and the flag are sent bit-complemented (~x = -x-1 reverses order without overflow).
+    Returns (global (min, max) or None, global has_data)."""
     mn, mx = mm if mm is not None else (INT64_MAX, INT64_MIN)
-    v = torch.tensor([mn, ~mx, ~int(not bf.is_empty())], dtype=torch.int64,
-                     device=bf.device if on_device else "cpu")
+    v = torch.tensor([mn, ~mx, ~int(bool(has_data))], dtype=torch.int64, device=device or "cpu")
     dist.all_reduce(v, op=dist.ReduceOp.MIN, group=group)
     g_mn, g_mx, g_has = int(v[0]), ~int(v[1]), ~int(v[2])
-    bf.set_minmax((g_mn, g_mx) if g_mn <= g_mx else None)
-    bf.set_has_data(bool(g_has))
+    return ((g_mn, g_mx) if g_mn <= g_mx else None), bool(g_has)
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:

@@ -85,3 +85,51 @@ def test_shard_range_partitions_rows():
             assert all(rs[i][1] == rs[i + 1][0] for i in range(w - 1))
             assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
     assert padded_words(1 << 21, 8) == 1 << 21 and padded_words(16, 3) == 18
+
+
+def _minmax_worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rpt_amd.distributed import allreduce_minmax_flag
+
+        i64 = np.iinfo(np.int64)
+        cases = [
+            # per-rank (min, max) or None, has_data
+            [((-5, 9), True), ((3, 12), True), (None, True), ((int(i64.min), -1), True)],
+            [(None, False), (None, True), (None, False), (None, False)],
+            [(None, False), (None, False), (None, False), (None, False)],
+            [((int(i64.max), int(i64.max)), True), (None, False), (None, False), (None, False)],
+        ]
+        out = []
+        for c in cases:
+            mm, has = c[rank]
+            out.append(allreduce_minmax_flag(mm, has))
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_minmax_and_flag_allreduce(world):
+    """The one-collective (min, max, has_data) reduce of the multi-GPU build (CreateBF Combine)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_minmax_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    i64 = np.iinfo(np.int64)
+    if world == 2:
+        expect = [((-5, 12), True), (None, True), (None, False), ((int(i64.max), int(i64.max)), True)]
+    else:
+        expect = [((int(i64.min), 12), True), (None, True), (None, False), ((int(i64.max), int(i64.max)), True)]
+    assert out == expect
