@@ -42,7 +42,8 @@ def parse():
                     help="size the filter for this many rows (default: --build-rows). C5 on one GPU = one "
                          "rank's share: --filter-rows 8e9 --build-rows 1e9")
     ap.add_argument("--p", type=float, default=0.10, help="fraction of probe rows drawn from the build keys")
-    ap.add_argument("--cpu-sample", type=float, default=1e8, help="probe rows in the CPU-baseline sample")
+    ap.add_argument("--cpu-sample", type=float, default=None,
+                    help="probe rows in the CPU-baseline sample (default: the whole per-GPU probe workload)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--strategy", default="auto", choices=["auto", "gather", "lds", "partitioned", "bucketed"],
@@ -100,7 +101,8 @@ def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int) -> di
         "unit": "keys/s",
         "cores": threads,
         "kind": "port",
-        "sample": (f"probe of the first {sample:.0e} rows of the same synthetic probe stream against the same "
+        "sample": (f"probe of the first {sample:.0e} rows (the GPU's whole per-step workload when equal to its "
+                   f"probe rows) of the same synthetic probe stream against the same "
                    f"{n_build:.0e}-key filter (2^{lnb} blocks), {threads} std::threads, 2048-row vectors, "
                    f"hash included; median of 5 after 1 warm-up; build of the filter {n_build / build_s:.3e} keys/s"),
         "cpu_model": _cpu_model(),
@@ -302,7 +304,8 @@ def main():
             },
         }
         if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(n_build, p_permille, int(args.cpu_sample), args.cpu_threads)
+            sample = int(args.cpu_sample) if args.cpu_sample else n_probe
+            line["cpu_baseline"] = cpu_baseline(n_build, p_permille, sample, args.cpu_threads)
         print(json.dumps(line), flush=True)
 
     if world > 1:
