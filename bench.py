@@ -305,7 +305,10 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             sample = int(args.cpu_sample) if args.cpu_sample else n_probe
-            line["cpu_baseline"] = cpu_baseline(n_build, p_permille, sample, args.cpu_threads)
+            cb = cpu_baseline(n_build, p_permille, sample, args.cpu_threads)
+            if sample == n_probe:  # same rows, same filter: a full-size cross-check of the survivor count
+                cb["survivors_match_gpu"] = cb["survivors"] == survivors
+            line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
 
     if world > 1:
