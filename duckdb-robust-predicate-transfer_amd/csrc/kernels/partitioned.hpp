@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
     }
     if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
     __syncthreads();
-    if (wave == 0) {  // exclusive scan of the slice counts, each padded to 4 records: kMaxSliceCount/64 per lane
+    if (wave == 0) {  // exclusive scan of the slice counts, each padded to kRunPad records: kMaxSliceCount/64 per lane
       constexpr int kPer = kMaxSliceCount / 64;
       uint32_t c[kPer], t = 0;
 #pragma unroll

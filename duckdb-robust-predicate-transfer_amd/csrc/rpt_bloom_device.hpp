@@ -45,7 +45,8 @@ __device__ __forceinline__ uint64_t rotl64(uint64_t x, uint32_t r) {
   return (x << r) | (x >> ((64u - r) & 63u));
 }
 
-// Expand the 1024 masks into an 8 KiB LDS table (one ds_read_b64 per key afterwards).
+// Expand the 1024 masks into an 8 KiB LDS table (one ds_read_b64 per key afterwards) -- the direct
+// probe and the atomic insert; the slice kernels use the 2048-entry rotated table (partitioned.hpp).
 // Must be followed by __syncthreads() before use.
 __device__ __forceinline__ void fill_mask_table(uint64_t* s_masks) {
   for (int id = threadIdx.x; id < kNumMasks; id += blockDim.x) {

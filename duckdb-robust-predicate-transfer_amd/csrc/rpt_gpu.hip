@@ -202,8 +202,7 @@ uint32_t slice_count(int log_num_blocks) {
   return log_num_blocks <= rpt::kSliceLog ? 1u : (1u << (log_num_blocks - rpt::kSliceLog));
 }
 
-// Strategy a probe of this filter will run: explicit choice, else by filter size
-// (<= 64 KiB: LDS-resident filter; <= 16 MiB: partitioned into LDS slices; larger: direct gather).
+// 16 MiB buckets of the bucketed strategy (1 for smaller filters).
 uint32_t bucket_count(int log_num_blocks) {
   return 1u << std::max(0, log_num_blocks - rpt::kSliceLog - rpt::kBucketSliceLog);
 }

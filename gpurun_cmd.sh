@@ -1,4 +1,9 @@
 mkdir -p gpurun_out; export TMPDIR=/tmp
-rm -rf gpurun_out/prof_c5
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_c5 -o c5 -- python3 bench.py --filter-rows 8e9 --build-rows 1e9 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_c5.log 2>&1 || { tail -5 gpurun_out/prof_c5.log; exit 1; }
-head -30 gpurun_out/prof_c5/c5_kernel_stats.csv | cut -d, -f1-4 | cut -c1-150
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc
+rm -rf gpurun_out/profile
+bash tools/profile_round.sh gpurun_out/profile r01 > gpurun_out/profile_round.log 2>&1 || { tail -5 gpurun_out/profile_round.log; exit 1; }
+cp gpurun_out/profile/pmc_summary.json profiles/pmc_latest.json
+timeout -k 10 300 python bench.py > gpurun_out/bench_final.log 2>&1 || exit 1
+grep '^{' gpurun_out/bench_final.log > gpurun_out/bench_final.json
+python3 -c "import json; d=json.load(open('gpurun_out/bench_final.json')); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline']['traffic'], d['cpu_baseline']['value'])"
