@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <thread>
 #include <utility>
 
 namespace rpt {
@@ -37,37 +38,62 @@ bool valid_bit(const uint64_t* validity, uint64_t idx) {
   return validity == nullptr || ((validity[idx >> 6] >> (idx & 63)) & 1ULL);
 }
 
+// OR `bits` (LSB = row g0) into the validity words at rows [g0, g0 + n), n <= 64. Words at a chunk's
+// edges may be shared with a neighbouring chunk that another thread flattens: those ORs are atomic.
+void or_bits(uint64_t* words, uint64_t g0, uint64_t bits, uint32_t n) {
+  if (n < 64) bits &= (1ULL << n) - 1;
+  if (!bits) return;
+  const uint64_t w = g0 >> 6, sh = g0 & 63;
+  __atomic_fetch_or(&words[w], bits << sh, __ATOMIC_RELAXED);
+  if (sh && sh + n > 64) __atomic_fetch_or(&words[w + 1], bits >> (64 - sh), __ATOMIC_RELAXED);
+}
+
+// Bits [r, r + n) (n <= 64) of a DuckDB validity mask (nullptr = all valid).
+uint64_t mask_bits(const uint64_t* validity, uint64_t r, uint32_t n) {
+  if (!validity) return n >= 64 ? ~0ULL : (1ULL << n) - 1;
+  const uint64_t w = r >> 6, sh = r & 63;
+  uint64_t b = validity[w] >> sh;
+  if (sh && sh + n > 64) b |= validity[w + 1] << (64 - sh);
+  return n >= 64 ? b : b & ((1ULL << n) - 1);
+}
+
 // Flatten one column of `chunk` (FLAT / CONSTANT / DICTIONARY) into `keys` (element size of the
-// column) and row validity bits appended at row offset `row0` of `valid_words`.
-// Returns true if any row was NULL.
+// column) and its row validity bits at row offset `row0` of `valid_words`, 64 rows per step for flat
+// and constant vectors. Returns true if any row was NULL.
 bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* valid_words, uint64_t row0) {
   const size_t es = key_size(v.key_type);
   bool any_null = false;
-  auto put_valid = [&](uint64_t r, bool ok) {
-    const uint64_t g = row0 + r;
-    if (ok) valid_words[g >> 6] |= 1ULL << (g & 63);
-    else any_null = true;
-  };
   switch (v.type) {
     case VectorType::FLAT:
       std::memcpy(keys, v.data, count * es);
-      for (uint64_t r = 0; r < count; r++) put_valid(r, valid_bit(v.validity, r));
+      for (uint64_t r = 0; r < count; r += 64) {
+        const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));
+        const uint64_t b = mask_bits(v.validity, r, n);
+        any_null |= b != (n == 64 ? ~0ULL : (1ULL << n) - 1);
+        or_bits(valid_words, row0 + r, b, n);
+      }
       break;
     case VectorType::CONSTANT: {
       const bool ok = valid_bit(v.validity, 0);
-      for (uint64_t r = 0; r < count; r++) {
-        std::memcpy(keys + r * es, v.data, es);
-        put_valid(r, ok);
-      }
+      for (uint64_t r = 0; r < count; r++) std::memcpy(keys + r * es, v.data, es);
+      any_null = !ok && count > 0;
+      if (ok)
+        for (uint64_t r = 0; r < count; r += 64) or_bits(valid_words, row0 + r, ~0ULL, static_cast<uint32_t>(std::min<uint64_t>(64, count - r)));
       break;
     }
     case VectorType::DICTIONARY: {
       const uint8_t* src = static_cast<const uint8_t*>(v.data);
-      for (uint64_t r = 0; r < count; r++) {
-        const uint32_t k = v.sel[r];
-        if (k >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
-        std::memcpy(keys + r * es, src + static_cast<uint64_t>(k) * es, es);
-        put_valid(r, valid_bit(v.validity, k));
+      for (uint64_t r = 0; r < count; r += 64) {
+        const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));
+        uint64_t b = 0;
+        for (uint32_t e = 0; e < n; e++) {
+          const uint32_t k = v.sel[r + e];
+          if (k >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
+          std::memcpy(keys + (r + e) * es, src + static_cast<uint64_t>(k) * es, es);
+          b |= static_cast<uint64_t>(valid_bit(v.validity, k)) << e;
+        }
+        any_null |= b != (n == 64 ? ~0ULL : (1ULL << n) - 1);
+        or_bits(valid_words, row0 + r, b, n);
       }
       break;
     }
@@ -84,13 +110,35 @@ rpt_key_column stage(DeviceContext& ctx, const std::vector<const DataChunk*>& ch
   auto* hkeys = static_cast<uint8_t*>(ctx.host(0, std::max<size_t>(total * es, 16)));
   auto* hvalid = static_cast<uint64_t*>(ctx.host(1, std::max<size_t>(nwords * 8, 8)));
   std::memset(hvalid, 0, nwords * 8);
+  std::vector<uint64_t> row0(chunks.size() + 1, 0);
+  for (size_t i = 0; i < chunks.size(); i++) {
+    if (chunks[i]->data.at(col).key_type != v0.key_type)
+      throw GpuError(RPT_ERR_INVALID_ARGUMENT, "mixed key types in one column");
+    row0[i + 1] = row0[i] + chunks[i]->count;
+  }
+  // Flattening into the pinned staging buffer is the host side's bottleneck for large batches (one
+  // thread copies ~10 GB/s); big batches are split over a few threads by chunk.
+  auto flatten_range = [&](size_t lo, size_t hi) {
+    bool nulls = false;
+    for (size_t i = lo; i < hi; i++)
+      nulls |= flatten_column(chunks[i]->data.at(col), chunks[i]->count, hkeys + row0[i] * es, hvalid, row0[i]);
+    return nulls;
+  };
   bool any_null = false;
-  uint64_t row = 0;
-  for (const DataChunk* c : chunks) {
-    const Vector& v = c->data.at(col);
-    if (v.key_type != v0.key_type) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "mixed key types in one column");
-    any_null |= flatten_column(v, c->count, hkeys + row * es, hvalid, row);
-    row += c->count;
+  const size_t n_threads = total >= (1u << 20) && chunks.size() >= 16
+                               ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()))
+                               : 1;
+  if (n_threads <= 1) {
+    any_null = flatten_range(0, chunks.size());
+  } else {
+    std::vector<std::thread> pool;
+    std::vector<char> nulls(n_threads, 0);
+    for (size_t t = 0; t < n_threads; t++) {
+      const size_t lo = chunks.size() * t / n_threads, hi = chunks.size() * (t + 1) / n_threads;
+      pool.emplace_back([&, t, lo, hi] { nulls[t] = flatten_range(lo, hi) ? 1 : 0; });
+    }
+    for (auto& th : pool) th.join();
+    for (char c : nulls) any_null |= c != 0;
   }
   void* dkeys = ctx.dev(0, std::max<size_t>(total * es, 16));
   void* dvalid = ctx.dev(1, std::max<size_t>(nwords * 8, 8));
