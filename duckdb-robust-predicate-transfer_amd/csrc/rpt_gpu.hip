@@ -220,19 +220,23 @@ int strategy_supported(int strategy, int log_num_blocks) {
   }
 }
 
-// The routed strategies (partitioned, bucketed) make one pass over the whole filter (every slice is
-// staged in LDS once), so they pay off only when the batch is large against the filter: n >= blocks/8
-// (measured break-even against the gather: ~0.1 x blocks).
-bool worth_routing(int log_num_blocks, uint64_t n) { return n >= ((1ULL << log_num_blocks) >> 3); }
-
-// AUTO: LDS for small filters; else a routed strategy for large batches; else the gather. n = ~0 is
-// "a batch of unknown, large size" (rpt_bf_probe_strategy).
+// AUTO, from measured crossovers (tools/strategy_crossover.py, profiles/r01/strategy_crossover.jsonl):
+//   <= 64 KiB   LDS: the whole filter in each workgroup's LDS;
+//   <= 256 KiB  GATHER: the filter stays resident in every XCD's L2 (~5 ps/key at any batch size);
+//   <= 128 MiB  PARTITIONED for batches of >= 4 Mi rows (>= 32 Mi below 8 MiB filters, where the L2
+//               still serves the gather well), else GATHER: routing has ~50 us of fixed cost;
+//   <= 16 GiB   BUCKETED for batches of >= max(blocks/8, 32 Mi) rows (it stages the whole filter in
+//               LDS once), else GATHER.
+// n = ~0 is "a batch of unknown, large size" (rpt_bf_probe_strategy).
 int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_PROBE_AUTO) return requested;
-  if (log_num_blocks <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
-  if (!worth_routing(log_num_blocks, n)) return RPT_PROBE_GATHER;
-  if (strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks)) return RPT_PROBE_PARTITIONED;
-  if (strategy_supported(RPT_PROBE_BUCKETED, log_num_blocks)) return RPT_PROBE_BUCKETED;
+  const int L = log_num_blocks;
+  if (L <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
+  if (L <= rpt::kLdsDirectMaxLog + 2) return RPT_PROBE_GATHER;
+  if (strategy_supported(RPT_PROBE_PARTITIONED, L))
+    return n >= (L >= 20 ? (1ULL << 22) : (1ULL << 25)) ? RPT_PROBE_PARTITIONED : RPT_PROBE_GATHER;
+  if (strategy_supported(RPT_PROBE_BUCKETED, L))
+    return n >= std::max<uint64_t>((1ULL << L) >> 3, 1ULL << 25) ? RPT_PROBE_BUCKETED : RPT_PROBE_GATHER;
   return RPT_PROBE_GATHER;
 }
 
@@ -368,7 +372,8 @@ int resolve_insert_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_INSERT_AUTO) return requested;
   if (n < kPartitionedInsertMinRows) return RPT_INSERT_ATOMIC;
   if (strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks)) return RPT_INSERT_PARTITIONED;
-  if (strategy_supported(RPT_PROBE_BUCKETED, log_num_blocks) && worth_routing(log_num_blocks, n))
+  if (strategy_supported(RPT_PROBE_BUCKETED, log_num_blocks) &&
+      n >= std::max<uint64_t>((1ULL << log_num_blocks) >> 3, 1ULL << 25))  // see resolve_strategy
     return RPT_INSERT_BUCKETED;
   return RPT_INSERT_ATOMIC;
 }

@@ -50,8 +50,9 @@ typedef enum rpt_key_type {
 
 /* How a probe reaches the filter blocks (rpt_bf_set_probe_strategy). All give identical results. */
 typedef enum rpt_probe_strategy {
-  RPT_PROBE_AUTO = 0,        /* LDS (<= 64 KiB); for n >= blocks/8: PARTITIONED (<= 128 MiB), BUCKETED
-                                (<= 16 GiB); otherwise GATHER */
+  RPT_PROBE_AUTO = 0,        /* by filter and batch size (measured crossovers): LDS (<= 64 KiB), GATHER
+                                (<= 256 KiB: L2-resident), PARTITIONED (<= 128 MiB, n >= 4 Mi), BUCKETED
+                                (<= 16 GiB, n >= max(blocks/8, 32 Mi)), otherwise GATHER */
   RPT_PROBE_GATHER = 1,      /* one random 8-byte gather per key from L2 / Infinity Cache / HBM */
   RPT_PROBE_LDS = 2,         /* whole filter staged in each workgroup's LDS (filters <= 64 KiB) */
   RPT_PROBE_PARTITIONED = 3, /* rows bucketed per 16 Ki-row tile by 128 KiB filter slice; each slice is
@@ -63,7 +64,7 @@ typedef enum rpt_probe_strategy {
 /* How an insert reaches the filter (rpt_bf_set_insert_strategy). All give identical filters. */
 typedef enum rpt_insert_strategy {
   RPT_INSERT_AUTO = 0,        /* for >= 2^20 rows: PARTITIONED when the filter supports it, BUCKETED for
-                                 larger filters when n >= blocks/8; otherwise ATOMIC */
+                                 larger filters when n >= max(blocks/8, 32 Mi); otherwise ATOMIC */
   RPT_INSERT_ATOMIC = 1,      /* one device-scope 64-bit atomic OR per key */
   RPT_INSERT_PARTITIONED = 2, /* rows bucketed by 128 KiB filter slice; each slice ORed in LDS, then
                                  merged with coalesced atomic ORs (filters 128 KiB..128 MiB) */

@@ -334,6 +334,9 @@ int main() {
       rpt::PTBloomFilter fb;
       fb.Initialize(dev, 1u << 28);  // 2^28 rows -> 2^25 blocks (256 MiB)
       EXPECT(fb.LogNumBlocks() == 25, "big filter log blocks %d", fb.LogNumBlocks());
+      // AUTO routes 256 MiB filters from 32 Mi rows per batch; this batch is pinned to the bucketed path
+      rpt_bf_set_insert_strategy(fb.native(), RPT_INSERT_BUCKETED);
+      rpt_bf_set_probe_strategy(fb.native(), RPT_PROBE_BUCKETED);
       EXPECT(rpt_bf_insert_strategy_for(fb.native(), nbig) == RPT_INSERT_BUCKETED, "bucketed insert expected");
       fb.InsertBatch(ctx, ptrs, {0});
       std::vector<uint64_t> wb(1ULL << 25, 0);

@@ -105,25 +105,31 @@ def test_bucketed_insert_vs_oracle(rpt, dtype, n):
 
 
 def test_auto_routes_large_filters(rpt):
-    """2^25 blocks (256 MiB): AUTO picks the bucketed insert / probe for large batches and the
-    atomic insert / gather for small ones; all give the oracle's bits and survivors."""
+    """2^25 blocks (256 MiB): AUTO picks the bucketed insert / probe for batches of >= 32 Mi rows and
+    the atomic insert / gather below; the chosen paths give the oracle's bits and survivors."""
     log_nb = 25
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    assert bf.insert_strategy_for(1 << 25) == INS_BUCKETED and bf.insert_strategy_for(5_000_000) == INS_ATOMIC
+    assert bf.probe_strategy_for(1 << 25) == BUCKETED and bf.probe_strategy_for(10**7) == GATHER
+    small = rpt.BloomFilter(log_num_blocks=14)  # 128 KiB: stays in L2, always the gather
+    assert small.probe_strategy_for(1 << 28) == GATHER
+    mid = rpt.BloomFilter(log_num_blocks=21)  # 16 MiB (C2): routed from 4 Mi rows
+    assert mid.probe_strategy_for(1 << 22) == PARTITIONED and mid.probe_strategy_for(1 << 21) == GATHER
     n_build = 5_000_000
     build = keys_of(np.int64, n_build, 11)
-    bf = rpt.BloomFilter(log_num_blocks=log_nb)
-    assert bf.insert_strategy_for(n_build) == INS_BUCKETED and bf.insert_strategy_for(1000) == INS_ATOMIC
-    assert bf.probe_strategy_for(10**7) == BUCKETED and bf.probe_strategy_for(10**5) == GATHER
-    bf.insert(dev(build))
+    bf.insert(dev(build))  # AUTO: atomic at this batch size
     w = oracle_filter(log_nb, build)
+    assert np.array_equal(bf.export_words(), w)
+    bf.insert(dev(build), strategy=INS_BUCKETED)  # re-inserting changes nothing
     assert np.array_equal(bf.export_words(), w)
     rng = np.random.default_rng(12)
     n_probe = 6_000_000
     probe = np.where(rng.random(n_probe) < 0.1, build[rng.integers(0, n_build, n_probe)], keys_of(np.int64, n_probe, 13))
     ref = orc.probe_keys(w, log_nb, probe)
-    sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
-    assert np.array_equal(sel, ref)
-    small = bf.lookup_sel(dev(probe[:100_000])).cpu().numpy().astype(np.uint32)
-    assert np.array_equal(small, ref[ref < 100_000])
+    for st in (0, BUCKETED):  # AUTO (gather here) and the bucketed path
+        bf.probe_strategy = st
+        sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
+        assert np.array_equal(sel, ref)
 
 
 def test_bucketed_skewed_keys(rpt):
