@@ -368,12 +368,18 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
 
 constexpr uint64_t kPartitionedInsertMinRows = 1ULL << 20;
 
+// AUTO insert, from the measured crossovers (profiles/r01/strategy_crossover.jsonl): memory-side
+// atomics cost ~37 ps/key at any filter size; the partitioned insert ~4-9 ps/key plus ~40 us (it
+// overtakes from ~1 Mi rows; ~4 Mi for single-slice filters, whose partition pass funnels every row
+// into one LDS counter); the bucketed insert ~9 ps/key plus a pass over the whole filter (~2 ms per
+// 8 GiB), so from ~blocks/16 rows.
 int resolve_insert_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_INSERT_AUTO) return requested;
-  if (n < kPartitionedInsertMinRows) return RPT_INSERT_ATOMIC;
-  if (strategy_supported(RPT_PROBE_PARTITIONED, log_num_blocks)) return RPT_INSERT_PARTITIONED;
-  if (strategy_supported(RPT_PROBE_BUCKETED, log_num_blocks) &&
-      n >= std::max<uint64_t>((1ULL << log_num_blocks) >> 3, 1ULL << 25))  // see resolve_strategy
+  const int L = log_num_blocks;
+  if (strategy_supported(RPT_PROBE_PARTITIONED, L))
+    return n >= (L <= rpt::kSliceLog + 1 ? (1ULL << 22) : kPartitionedInsertMinRows) ? RPT_INSERT_PARTITIONED
+                                                                                     : RPT_INSERT_ATOMIC;
+  if (strategy_supported(RPT_PROBE_BUCKETED, L) && n >= std::max<uint64_t>((1ULL << L) >> 4, 1ULL << 23))
     return RPT_INSERT_BUCKETED;
   return RPT_INSERT_ATOMIC;
 }

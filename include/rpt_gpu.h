@@ -63,8 +63,8 @@ typedef enum rpt_probe_strategy {
 
 /* How an insert reaches the filter (rpt_bf_set_insert_strategy). All give identical filters. */
 typedef enum rpt_insert_strategy {
-  RPT_INSERT_AUTO = 0,        /* for >= 2^20 rows: PARTITIONED when the filter supports it, BUCKETED for
-                                 larger filters when n >= max(blocks/8, 32 Mi); otherwise ATOMIC */
+  RPT_INSERT_AUTO = 0,        /* by filter and batch size (measured crossovers): PARTITIONED (<= 128 MiB,
+                                 n >= 1 Mi), BUCKETED (larger, n >= max(blocks/16, 8 Mi)), else ATOMIC */
   RPT_INSERT_ATOMIC = 1,      /* one device-scope 64-bit atomic OR per key */
   RPT_INSERT_PARTITIONED = 2, /* rows bucketed by 128 KiB filter slice; each slice ORed in LDS, then
                                  merged with coalesced atomic ORs (filters 128 KiB..128 MiB) */

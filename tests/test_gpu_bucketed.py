@@ -105,11 +105,11 @@ def test_bucketed_insert_vs_oracle(rpt, dtype, n):
 
 
 def test_auto_routes_large_filters(rpt):
-    """2^25 blocks (256 MiB): AUTO picks the bucketed insert / probe for batches of >= 32 Mi rows and
-    the atomic insert / gather below; the chosen paths give the oracle's bits and survivors."""
+    """2^25 blocks (256 MiB): AUTO picks the bucketed insert from 8 Mi rows and the bucketed probe from
+    32 Mi rows, the atomic insert / gather below; the chosen paths give the oracle's bits and survivors."""
     log_nb = 25
     bf = rpt.BloomFilter(log_num_blocks=log_nb)
-    assert bf.insert_strategy_for(1 << 25) == INS_BUCKETED and bf.insert_strategy_for(5_000_000) == INS_ATOMIC
+    assert bf.insert_strategy_for(1 << 23) == INS_BUCKETED and bf.insert_strategy_for(1 << 21) == INS_ATOMIC
     assert bf.probe_strategy_for(1 << 25) == BUCKETED and bf.probe_strategy_for(10**7) == GATHER
     small = rpt.BloomFilter(log_num_blocks=14)  # 128 KiB: stays in L2, always the gather
     assert small.probe_strategy_for(1 << 28) == GATHER

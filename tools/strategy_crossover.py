@@ -29,7 +29,38 @@ def time_probe(bf, keys, n, reps=5):
     return e0.elapsed_time(e1) / reps
 
 
+def time_insert(bf, keys, n, strategy, reps=3):
+    bf.insert(keys[:n], strategy=strategy)  # warm-up (workspace, code objects)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        bf.insert(keys[:n], strategy=strategy)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def insert_sweep():
+    lib = rpt_amd.load()
+    keys = rpt_amd.synth_build_keys(1 << 27)
+    for L in (12, 14, 16, 18, 21, 24, 27):
+        bf = rpt_amd.BloomFilter(log_num_blocks=L)
+        for lg in (16, 20, 22, 24, 26):
+            n = 1 << lg
+            row = {"op": "insert", "log_blocks": L, "n": n, "auto": bf.insert_strategy_for(n)}
+            for name, st in (("atomic", 1), ("partitioned", 2), ("bucketed", 3)):
+                if (st == 2 and not lib.rpt_probe_strategy_supported(3, L)) or (st == 3 and not lib.rpt_probe_strategy_supported(4, L)):
+                    continue
+                row[name] = round(time_insert(bf, keys, n, st), 4)
+            print(json.dumps(row), flush=True)
+        del bf
+        torch.cuda.empty_cache()
+
+
 def main():
+    if "--insert" in sys.argv:
+        return insert_sweep()
     lib = rpt_amd.load()
     n_max = 1 << 28
     for build in (10**5, 10**7, 10**8, 10**9):
