@@ -101,8 +101,15 @@ bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* va
   return any_null;
 }
 
-// Stage column `col` of `chunks` to the device as one flat key column (slots 0/1 of the context).
-rpt_key_column stage(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col, uint64_t total) {
+// Column `col` of `chunks` flattened into the context's pinned staging buffers (slots 0/1).
+struct Flattened {
+  KeyType key_type;
+  const uint8_t* keys;
+  const uint64_t* valid;
+  bool any_null;
+};
+
+Flattened flatten_pinned(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col, uint64_t total) {
   if (chunks.empty()) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "no chunks");
   const Vector& v0 = chunks[0]->data.at(col);
   const size_t es = key_size(v0.key_type);
@@ -140,17 +147,29 @@ rpt_key_column stage(DeviceContext& ctx, const std::vector<const DataChunk*>& ch
     for (auto& th : pool) th.join();
     for (char c : nulls) any_null |= c != 0;
   }
-  void* dkeys = ctx.dev(0, std::max<size_t>(total * es, 16));
-  void* dvalid = ctx.dev(1, std::max<size_t>(nwords * 8, 8));
+  return Flattened{v0.key_type, hkeys, hvalid, any_null};
+}
+
+// Copy a flattened column to device buffers (dvalid is only written when the batch had NULLs).
+rpt_key_column copy_flattened(DeviceContext& ctx, const Flattened& f, uint64_t total, void* dkeys, void* dvalid) {
   auto s = static_cast<hipStream_t>(ctx.stream());
-  check_hip(hipMemcpyAsync(dkeys, hkeys, total * es, hipMemcpyHostToDevice, s), "stage keys");
-  if (any_null) check_hip(hipMemcpyAsync(dvalid, hvalid, nwords * 8, hipMemcpyHostToDevice, s), "stage validity");
+  check_hip(hipMemcpyAsync(dkeys, f.keys, total * key_size(f.key_type), hipMemcpyHostToDevice, s), "stage keys");
+  if (f.any_null)
+    check_hip(hipMemcpyAsync(dvalid, f.valid, (total + 63) / 64 * 8, hipMemcpyHostToDevice, s), "stage validity");
   rpt_key_column kc;
-  kc.key_type = static_cast<int32_t>(v0.key_type);
+  kc.key_type = static_cast<int32_t>(f.key_type);
   kc.keys = dkeys;
   kc.key_sel = nullptr;
-  kc.validity = any_null ? static_cast<const uint64_t*>(dvalid) : nullptr;
+  kc.validity = f.any_null ? static_cast<const uint64_t*>(dvalid) : nullptr;
   return kc;
+}
+
+// Stage column `col` of `chunks` to the device as one flat key column (slots 0/1 of the context).
+rpt_key_column stage(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col, uint64_t total) {
+  const Flattened f = flatten_pinned(ctx, chunks, col, total);
+  void* dkeys = ctx.dev(0, std::max<size_t>(total * key_size(f.key_type), 16));
+  void* dvalid = ctx.dev(1, std::max<size_t>((total + 63) / 64 * 8, 8));
+  return copy_flattened(ctx, f, total, dkeys, dvalid);
 }
 
 uint64_t total_rows(const std::vector<const DataChunk*>& chunks) {
@@ -234,6 +253,64 @@ void* DeviceContext::dev(int slot, size_t bytes) {
   return b.p;
 }
 
+// ---- DeviceKeyColumn ---------------------------------------------------------------------------
+DeviceKeyColumn::~DeviceKeyColumn() { release(); }
+
+DeviceKeyColumn::DeviceKeyColumn(DeviceKeyColumn&& o) noexcept : device_(o.device_), segs_(std::move(o.segs_)) {
+  o.segs_.clear();
+}
+
+DeviceKeyColumn& DeviceKeyColumn::operator=(DeviceKeyColumn&& o) noexcept {
+  if (this != &o) {
+    release();
+    device_ = o.device_;
+    segs_ = std::move(o.segs_);
+    o.segs_.clear();
+  }
+  return *this;
+}
+
+void DeviceKeyColumn::release() {
+  if (segs_.empty()) return;
+  DeviceScope ds(device_);
+  for (auto& g : segs_) {
+    (void)hipFree(const_cast<void*>(g.col.keys));
+    if (g.col.validity) (void)hipFree(const_cast<uint64_t*>(g.col.validity));
+  }
+  segs_.clear();
+}
+
+const DeviceKeyColumn::Segment& DeviceKeyColumn::Append(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                                                        uint64_t col) {
+  const uint64_t total = total_rows(chunks);
+  if (total == 0) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "empty batch");
+  const Flattened f = flatten_pinned(ctx, chunks, col, total);
+  DeviceScope ds(device_);
+  void* dkeys = nullptr;
+  void* dvalid = nullptr;
+  check_hip(hipMalloc(&dkeys, total * key_size(f.key_type)), "hipMalloc key segment");
+  if (f.any_null) {
+    if (hipMalloc(&dvalid, (total + 63) / 64 * 8) != hipSuccess) {
+      (void)hipFree(dkeys);
+      throw GpuError(RPT_ERR_HIP, "hipMalloc validity segment");
+    }
+  }
+  segs_.push_back(Segment{copy_flattened(ctx, f, total, dkeys, dvalid), total});
+  return segs_.back();
+}
+
+void DeviceKeyColumn::Splice(DeviceKeyColumn&& other) {
+  if (other.device_ != device_) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "key columns on different devices");
+  for (auto& g : other.segs_) segs_.push_back(g);
+  other.segs_.clear();
+}
+
+uint64_t DeviceKeyColumn::rows() const {
+  uint64_t r = 0;
+  for (const auto& g : segs_) r += g.rows;
+  return r;
+}
+
 // ---- PTBloomFilter -------------------------------------------------------------------------------
 PTBloomFilter::~PTBloomFilter() {
   if (bf_) rpt_bf_destroy(bf_);
@@ -255,11 +332,15 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
                                 const std::vector<uint64_t>& cols) {
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:72-74
-  rpt_key_column kc = stage_key(ctx, chunks, cols, total);
+  InsertDevice(ctx, stage_key(ctx, chunks, cols, total), total);
+}
+
+void PTBloomFilter::InsertDevice(DeviceContext& ctx, const rpt_key_column& col, uint64_t n) {
+  if (n == 0) return;
   // large batches take the partitioned / bucketed insert (same filter bits)
-  const size_t ws_bytes = rpt_bf_insert_workspace_bytes(bf_, total);
-  if (ws_bytes) check(rpt_bf_insert_ws(bf_, &kc, total, ctx.dev(6, ws_bytes), ws_bytes, ctx.stream()));
-  else check(rpt_bf_insert(bf_, &kc, total, ctx.stream()));
+  const size_t ws_bytes = rpt_bf_insert_workspace_bytes(bf_, n);
+  if (ws_bytes) check(rpt_bf_insert_ws(bf_, &col, n, ctx.dev(6, ws_bytes), ws_bytes, ctx.stream()));
+  else check(rpt_bf_insert(bf_, &col, n, ctx.stream()));
   ctx.synchronize();  // the staging buffers are reused by the next call
 }
 
@@ -309,6 +390,11 @@ void PTBloomFilter::ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_ro
   if (!ptrs.empty()) InsertBatch(ctx, ptrs, cols);
 }
 
+void PTBloomFilter::ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const DeviceKeyColumn& keys) {
+  check(rpt_bf_reinitialize(bf_, actual_rows));
+  for (const auto& g : keys.segments()) InsertDevice(ctx, g.col, g.rows);
+}
+
 uint64_t PTBloomFilter::SizedForRows() const {
   rpt_bf_info i;
   check(rpt_bf_get_info(bf_, &i));
@@ -342,24 +428,31 @@ std::vector<uint64_t> PTBloomFilter::ExportWords() const {
 }
 
 // ---- CreateBF ------------------------------------------------------------------------------------
-CreateBF::CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices)
-    : device_(device), estimated_cardinality_(estimated_cardinality), cols_(std::move(bound_column_indices)) {
+CreateBF::CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices,
+                   uint64_t sink_flush_rows)
+    : device_(device),
+      estimated_cardinality_(estimated_cardinality),
+      cols_(std::move(bound_column_indices)),
+      sink_flush_rows_(std::max<uint64_t>(1, sink_flush_rows)) {
   for (size_t i = 0; i < cols_.size(); i++) {
     auto bf = std::make_shared<PTBloomFilter>();
     // CreateBFGlobalSinkState: Initialize(context, op.estimated_cardinality) -> uint32 (cpp:179-186)
     bf->Initialize(device_, static_cast<uint32_t>(estimated_cardinality_));
     filters_.push_back(std::move(bf));
     resized_.push_back(false);
+    all_keys_.emplace_back(device_);
   }
 }
 
 void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
-  // materialize the key columns (flattened, owned) for a possible rehash in Finalize
+  // materialize the chunk (every column, flattened, owned): the source re-emits it
+  // (physical_create_bf.cpp:211-218)
   DataChunk m;
   m.count = chunk.count;
   m.data.resize(chunk.data.size());
-  for (uint64_t col : cols_) {
-    const Vector& v = chunk.data.at(col);
+  for (size_t c = 0; c < chunk.data.size(); c++) {
+    const Vector& v = chunk.data[c];
+    if (v.data == nullptr) continue;  // a column this mirror does not carry
     const size_t es = key_size(v.key_type);
     std::vector<uint64_t> keys((chunk.count * es + 7) / 8 + 1, 0);
     std::vector<uint64_t> valid((chunk.count + 63) / 64 + 1, 0);
@@ -371,22 +464,42 @@ void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
     f.validity = any_null ? valid.data() : nullptr;
     local.storage.push_back(std::move(keys));
     local.storage.push_back(std::move(valid));
-    m.data[col] = f;
+    m.data[c] = f;
   }
   local.chunks.push_back(std::move(m));
-  // insert into one filter per build column (physical_create_bf.cpp:221-227)
-  for (size_t i = 0; i < cols_.size(); i++) filters_[i]->Insert(local.ctx, chunk, {cols_[i]});
+  local.pending_rows += chunk.count;
+  // insert into one filter per build column (physical_create_bf.cpp:221-227), a batch at a time
+  if (local.pending_rows >= sink_flush_rows_) Flush(local);
+}
+
+void CreateBF::Flush(LocalState& local) const {
+  if (local.pending_rows == 0) {
+    local.pending_from = local.chunks.size();
+    return;
+  }
+  std::vector<const DataChunk*> batch;
+  for (size_t k = local.pending_from; k < local.chunks.size(); k++)
+    if (local.chunks[k].count) batch.push_back(&local.chunks[k]);
+  for (size_t i = 0; i < cols_.size(); i++) {
+    const DeviceKeyColumn::Segment& g = local.keys[i].Append(local.ctx, batch, cols_[i]);
+    filters_[i]->InsertDevice(local.ctx, g.col, g.rows);
+  }
+  local.pending_from = local.chunks.size();
+  local.pending_rows = 0;
 }
 
 void CreateBF::Combine(LocalState& local) {
+  Flush(local);
   std::lock_guard<std::mutex> lk(lock_);
   for (auto& c : local.chunks) {
     total_rows_ += c.count;
     all_chunks_.push_back(std::move(c));
   }
   for (auto& s : local.storage) all_storage_.push_back(std::move(s));
+  for (size_t i = 0; i < cols_.size(); i++) all_keys_[i].Splice(std::move(local.keys[i]));
   local.chunks.clear();
   local.storage.clear();
+  local.pending_from = 0;
 }
 
 void CreateBF::Finalize() {
@@ -395,14 +508,45 @@ void CreateBF::Finalize() {
     DeviceContext ctx(device_);
     for (size_t i = 0; i < filters_.size(); i++) {
       auto& bf = *filters_[i];
-      // physical_create_bf.cpp:394-398: resize iff actual*8 > NextPow2(max(512, sized_for*12))
+      // physical_create_bf.cpp:394-398: resize iff actual*8 > NextPow2(max(512, sized_for*12)); the
+      // rehash reads the build column from HBM
       if (rpt_bf_needs_resize(bf.SizedForRows(), actual_rows)) {
-        bf.ReinitializeAndRehash(ctx, actual_rows, all_chunks_, {cols_[i]});
+        bf.ReinitializeAndRehash(ctx, actual_rows, all_keys_[i]);
         resized_[i] = true;
       }
     }
   }
   for (auto& bf : filters_) bf->finalized_ = true;  // physical_create_bf.cpp:409-413
+}
+
+std::unique_ptr<CreateBF::GlobalSourceState> CreateBF::GetGlobalSourceState(size_t num_threads) const {
+  auto g = std::make_unique<GlobalSourceState>();
+  const size_t chunk_count = all_chunks_.size();
+  num_threads = std::max<size_t>(1, num_threads);
+  const size_t per = std::max<size_t>((chunk_count + num_threads - 1) / num_threads, 1);
+  for (size_t t = 0, k = 0; t < num_threads && k < chunk_count; t++) {
+    const size_t to = std::min(k + per, chunk_count);
+    g->chunks_todo.emplace_back(k, to);
+    k = to;
+  }
+  return g;
+}
+
+bool CreateBF::GetData(GlobalSourceState& global, LocalSourceState& local, DataChunk& chunk) const {
+  if (local.initial) {
+    local.initial = false;
+    const size_t id = global.partition_id.fetch_add(1);
+    if (id >= global.chunks_todo.size()) {
+      local.current = local.chunk_to = 0;
+      return false;
+    }
+    local.chunk_from = global.chunks_todo[id].first;
+    local.chunk_to = global.chunks_todo[id].second;
+    local.current = local.chunk_from;
+  }
+  if (local.current >= local.chunk_to) return false;
+  chunk = all_chunks_[local.current++];
+  return true;
 }
 
 bool CreateBF::MinMax(size_t build_column, int64_t& min_value, int64_t& max_value) const {

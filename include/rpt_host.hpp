@@ -13,11 +13,13 @@
 // 2048-row chunks into one device call, which is how the shim amortises PCIe latency.
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "rpt_gpu.h"
@@ -82,6 +84,36 @@ class DeviceContext {
   Buf host_[8], dev_[8];
 };
 
+// One key column kept in HBM, one segment per staged batch: the device half of CREATE_BF's
+// materialization (physical_create_bf.cpp:211-218; the full rows stay in host memory). Finalize's
+// rehash (bloom_filter.cpp:34-58) re-inserts from these segments instead of re-staging every host
+// chunk over PCIe.
+class DeviceKeyColumn {
+ public:
+  struct Segment {
+    rpt_key_column col;  // device keys (+ validity words when the batch had NULLs)
+    uint64_t rows;
+  };
+  explicit DeviceKeyColumn(int device) : device_(device) {}
+  ~DeviceKeyColumn();
+  DeviceKeyColumn(DeviceKeyColumn&& o) noexcept;
+  DeviceKeyColumn& operator=(DeviceKeyColumn&& o) noexcept;
+  DeviceKeyColumn(const DeviceKeyColumn&) = delete;
+  DeviceKeyColumn& operator=(const DeviceKeyColumn&) = delete;
+
+  // Flatten column `col` of `chunks` (FLAT / CONSTANT / DICTIONARY) into a new device segment.
+  const Segment& Append(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col);
+  // Take over `other`'s segments (CREATE_BF Combine).
+  void Splice(DeviceKeyColumn&& other);
+  const std::vector<Segment>& segments() const { return segs_; }
+  uint64_t rows() const;
+
+ private:
+  void release();
+  int device_;
+  std::vector<Segment> segs_;
+};
+
 // PTBloomFilter (bloom_filter.hpp:22-57) with the filter on the device.
 class PTBloomFilter {
  public:
@@ -102,9 +134,13 @@ class PTBloomFilter {
   // many chunks in one device call; sels[i] holds chunk i's survivors (ids relative to chunk i)
   void LookupSelBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                       std::vector<SelectionVector>& sels, const std::vector<uint64_t>& cols) const;
+  // Insert a device-resident key column (large batches take the routed inserts; same bits).
+  void InsertDevice(DeviceContext& ctx, const rpt_key_column& col, uint64_t n);
   // bloom_filter.cpp:34-58: reallocate for actual_rows and re-insert the materialized chunks
   void ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const std::vector<DataChunk>& data,
                              const std::vector<uint64_t>& cols);
+  // ... or re-insert a key column already in HBM (no PCIe traffic)
+  void ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const DeviceKeyColumn& keys);
 
   uint64_t SizedForRows() const;
   bool IsEmpty() const;
@@ -122,38 +158,71 @@ class PTBloomFilter {
 
 // The hot-path part of PhysicalCreateBF: parallel Sink (materialize + insert), Combine, Finalize
 // (resize rule + rehash, finalized_), one filter per build column (bloom_filter_map,
-// physical_create_bf.hpp:73). Materialization keeps the build chunks' key columns (the reference
-// keeps full rows in a ColumnDataCollection, physical_create_bf.cpp:211-218).
+// physical_create_bf.hpp:73), and the parallel source that re-emits the materialized chunks
+// (physical_create_bf.cpp:441-557).
+//
+// Sink materializes every column of the chunk on the host (the reference's local
+// ColumnDataCollection, physical_create_bf.cpp:211-218) and stages the build columns to the device
+// in batches of `sink_flush_rows` rows (one PCIe transfer + one insert per batch instead of one per
+// 2048-row chunk; the filters are only read after Finalize, so deferring the inserts is unobservable).
+// The staged key columns stay in HBM (DeviceKeyColumn), so Finalize's rehash never re-reads the host.
 class CreateBF {
  public:
+  static constexpr uint64_t kDefaultSinkFlushRows = 1ULL << 22;
+
   struct LocalState {
-    explicit LocalState(int device) : ctx(device) {}
+    LocalState(int device, size_t n_cols) : ctx(device) {
+      for (size_t i = 0; i < n_cols; i++) keys.emplace_back(device);
+    }
     DeviceContext ctx;
-    std::vector<DataChunk> chunks;               // materialized key columns (views of owned storage)
+    std::vector<DataChunk> chunks;               // materialized chunks (views of owned storage)
     std::vector<std::vector<uint64_t>> storage;  // owned copies backing `chunks`
+    std::vector<DeviceKeyColumn> keys;           // build columns already staged to HBM
+    size_t pending_from = 0;                     // chunks[pending_from..] not yet inserted
+    uint64_t pending_rows = 0;
+  };
+  // CreateBFGlobalSourceState (physical_create_bf.cpp:441-485): chunk ranges, one per source thread
+  struct GlobalSourceState {
+    std::vector<std::pair<size_t, size_t>> chunks_todo;
+    std::atomic<size_t> partition_id{0};
+  };
+  struct LocalSourceState {
+    bool initial = true;
+    size_t chunk_from = 0, chunk_to = 0, current = 0;
   };
 
-  CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices);
-  std::unique_ptr<LocalState> MakeLocalState() const { return std::make_unique<LocalState>(device_); }
+  CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices,
+           uint64_t sink_flush_rows = kDefaultSinkFlushRows);
+  std::unique_ptr<LocalState> MakeLocalState() const { return std::make_unique<LocalState>(device_, cols_.size()); }
   void Sink(LocalState& local, const DataChunk& chunk) const;  // physical_create_bf.cpp:201-242
   void Combine(LocalState& local);                             // physical_create_bf.cpp:244-275
   void Finalize();                                             // physical_create_bf.cpp:352-419
   std::shared_ptr<PTBloomFilter> GetBloomFilter(size_t build_column) const { return filters_.at(build_column); }
   uint64_t MaterializedRows() const { return total_rows_; }
+  size_t ChunkCount() const { return all_chunks_.size(); }
   bool Resized(size_t build_column) const { return resized_.at(build_column); }
   // CreateBFGlobalSinkState::column_min_max[i] (physical_create_bf.cpp:229-272): min / max of the
   // valid keys of build column i, computed by the insert kernels; false when no valid key was seen.
   bool MinMax(size_t build_column, int64_t& min_value, int64_t& max_value) const;
+  // The parallel source (physical_create_bf.cpp:453-557): ceil(chunks / num_threads) chunks per
+  // range; each LocalSourceState claims one range and walks it. GetData returns false when its range
+  // is done (SourceResultType::FINISHED); `chunk` is a view of the materialized chunk.
+  std::unique_ptr<GlobalSourceState> GetGlobalSourceState(size_t num_threads) const;
+  bool GetData(GlobalSourceState& global, LocalSourceState& local, DataChunk& chunk) const;
 
  private:
+  void Flush(LocalState& local) const;  // stage + insert the pending chunks' build columns
+
   int device_;
   uint64_t estimated_cardinality_;
   std::vector<uint64_t> cols_;
+  uint64_t sink_flush_rows_;
   std::vector<std::shared_ptr<PTBloomFilter>> filters_;
   std::vector<bool> resized_;
   std::mutex lock_;
   std::vector<DataChunk> all_chunks_;
   std::vector<std::vector<uint64_t>> all_storage_;
+  std::vector<DeviceKeyColumn> all_keys_;
   uint64_t total_rows_ = 0;
 };
 

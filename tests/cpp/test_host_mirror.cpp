@@ -2,10 +2,12 @@
 // against the CPU restatement (oracle/librpt_oracle.so, test infrastructure).
 //
 // CREATE_BF: 4 sink threads, 2048-row chunks (last one ragged), FLAT/CONSTANT/DICTIONARY vectors with
-// NULLs, an under-estimated cardinality so Finalize must ReinitializeAndRehash; then USE_BF with two
-// filters (chain = AND), the empty-build early exit, the not-finalized skip and passthrough; the
-// build's min/max dynamic filter; a composite (two-column) key filter; a 256 MiB filter whose
+// NULLs, sink batches staged to HBM, an under-estimated cardinality so Finalize must
+// ReinitializeAndRehash (from the HBM key segments); the parallel source re-emitting the materialized
+// chunks; then USE_BF with two filters (chain = AND), the empty-build early exit, the not-finalized
+// skip and passthrough; the build's min/max dynamic filter; a composite (two-column) key filter; a 256 MiB filter whose
 // batched insert and lookup take the bucketed strategy.
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
@@ -181,7 +183,8 @@ int main() {
     Table bt = make_table(nb, 1, 97, 2048);
     ChunkStore bst;
     make_chunks(bt, nb, bst, true);
-    rpt::CreateBF create(dev, /*estimated_cardinality=*/1000, {0, 1});
+    // sink batches of >= 5000 rows: several device key segments per sink thread
+    rpt::CreateBF create(dev, /*estimated_cardinality=*/1000, {0, 1}, /*sink_flush_rows=*/5000);
     std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> locals;
     for (int t = 0; t < 4; t++) locals.push_back(create.MakeLocalState());
     std::vector<std::thread> ths;
@@ -217,6 +220,56 @@ int main() {
              (long long)mn, (long long)mx, (long long)e0[0], (long long)e0[1]);
       EXPECT(h1 && create.MinMax(1, mn, mx) && mn == e1[0] && mx == e1[1], "column 1 min/max %lld..%lld vs %lld..%lld",
              (long long)mn, (long long)mx, (long long)e1[0], (long long)e1[1]);
+    }
+
+    // ---------------- source: the materialized chunks re-emitted by thread range ---------------
+    {
+      const size_t cc = create.ChunkCount();
+      EXPECT(cc == bst.chunks.size(), "chunk count %zu", cc);
+      auto gs = create.GetGlobalSourceState(3);
+      const size_t per = (cc + 2) / 3;  // physical_create_bf.cpp:469-485
+      EXPECT(gs->chunks_todo.size() == 3 && gs->chunks_todo[0].first == 0 && gs->chunks_todo[0].second == per &&
+                 gs->chunks_todo[2].second == cc, "source ranges");
+      std::vector<std::vector<rpt::DataChunk>> got(4);
+      std::vector<std::thread> src;
+      for (int t = 0; t < 4; t++)
+        src.emplace_back([&, t] {
+          rpt::CreateBF::LocalSourceState ls;
+          rpt::DataChunk c;
+          while (create.GetData(*gs, ls, c)) got[t].push_back(c);
+        });
+      for (auto& th : src) th.join();
+      size_t empty_threads = 0;
+      std::vector<std::pair<int64_t, int64_t>> rows_out, rows_in;  // (c0 or NULL marker, c1 or NULL)
+      const int64_t kNull = INT64_MIN;
+      for (auto& g : got) {
+        empty_threads += g.empty();
+        for (const auto& c : g) {
+          EXPECT(c.data.size() == 3 && c.data[2].data == nullptr, "payload column shape");
+          auto* a = static_cast<const int64_t*>(c.data[0].data);
+          auto* b = static_cast<const int32_t*>(c.data[1].data);
+          for (size_t r = 0; r < c.count; r++) {
+            const bool va = !c.data[0].validity || ((c.data[0].validity[r / 64] >> (r % 64)) & 1);
+            const bool vb = !c.data[1].validity || ((c.data[1].validity[r / 64] >> (r % 64)) & 1);
+            rows_out.emplace_back(va ? a[r] : kNull, vb ? b[r] : kNull);
+          }
+        }
+      }
+      for (size_t i = 0; i < nb; i++) rows_in.emplace_back(bt.v0[i] ? bt.c0[i] : kNull, bt.v1[i] ? bt.c1[i] : kNull);
+      std::sort(rows_out.begin(), rows_out.end());
+      std::sort(rows_in.begin(), rows_in.end());
+      EXPECT(empty_threads == 1, "one of 4 source threads finds no range (%zu)", empty_threads);
+      EXPECT(rows_out == rows_in, "the source re-emits exactly the sunk rows (%zu vs %zu)", rows_out.size(), rows_in.size());
+    }
+    // default sink batching (all inserts at Combine), no resize: same filter as the oracle's
+    {
+      rpt::CreateBF c2(dev, /*estimated_cardinality=*/nb, {0});
+      auto l = c2.MakeLocalState();
+      for (const auto& ch : bst.chunks) c2.Sink(*l, ch);
+      c2.Combine(*l);
+      c2.Finalize();
+      EXPECT(!c2.Resized(0), "no resize at the right estimate");
+      EXPECT(c2.GetBloomFilter(0)->ExportWords() == w0, "batched-sink filter differs from the oracle");
     }
 
     // ---------------- probe -------------------------------------------------------------------

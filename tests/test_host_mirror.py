@@ -1,7 +1,8 @@
 """C++ host mirror (include/rpt_host.hpp) of PTBloomFilter / CREATE_BF / USE_BF, end to end.
 
 The GPU test runs tests/cpp/build/test_host_mirror (4 sink threads, FLAT/CONSTANT/DICTIONARY vectors
-with NULLs, resize + rehash in Finalize, a two-filter USE_BF chain, early exits) against the oracle.
+with NULLs, sink batches kept in HBM, resize + rehash from HBM in Finalize, the parallel source,
+a two-filter USE_BF chain, early exits) against the oracle.
 """
 import os
 import subprocess
@@ -26,7 +27,9 @@ def test_host_mirror_links():
     syms = subprocess.run(["nm", "-DC", os.path.join(REPO, "duckdb-robust-predicate-transfer_amd", "build",
                                                       "librpt_gpu.so")], capture_output=True, text=True).stdout
     for name in ["rpt::PTBloomFilter::Insert", "rpt::PTBloomFilter::LookupSel", "rpt::CreateBF::Finalize",
-                 "rpt::UseBF::Execute", "rpt::PTBloomFilter::ReinitializeAndRehash"]:
+                 "rpt::UseBF::Execute", "rpt::PTBloomFilter::ReinitializeAndRehash",
+                 "rpt::CreateBF::GetData", "rpt::CreateBF::GetGlobalSourceState", "rpt::DeviceKeyColumn::Append",
+                 "rpt::PTBloomFilter::InsertDevice"]:
         assert name in syms, name
 
 

@@ -1,10 +1,13 @@
 // host_bench.cpp — PCIe-inclusive throughput of the C++ host mirror (include/rpt_host.hpp): host-resident
 // 2048-row DuckDB-style chunks are staged to the device, probed, and their selection vectors copied
-// back, for batches of 1 .. 8192 chunks per device call (LookupSelBatch), plus the batched build.
+// back, for batches of 1 .. 8192 chunks per device call (LookupSelBatch), plus the batched build and
+// CREATE_BF end to end (parallel sink, Combine, Finalize's rehash from HBM vs from host chunks).
 // This is the rate a DuckDB shim calling the mirror would see; it is never the bench's `value`.
 #include <chrono>
 #include <cstdio>
+#include <memory>
 #include <random>
+#include <thread>
 #include <vector>
 
 #include "rpt_host.hpp"
@@ -70,6 +73,45 @@ int main() {
     printf("{\"op\": \"LookupSelBatch\", \"chunks_per_call\": %zu, \"rows\": %zu, \"calls\": %zu, \"us_per_call\": %.1f, "
            "\"rows_per_s\": %.4g, \"pass_fraction\": %.4f}\n",
            per_call, rows, calls, s / calls * 1e6, rows / s, static_cast<double>(survivors) / rows);
+  }
+  // CREATE_BF end to end: 8 sink threads over 2048-row chunks of the build (sink batches staged to HBM),
+  // Combine, then Finalize with an under-estimated cardinality so the filter is resized and rehashed
+  // -- from the HBM key segments, versus re-staging the materialized host chunks.
+  for (uint64_t flush : {uint64_t(1) << 20, rpt::CreateBF::kDefaultSinkFlushRows}) {
+    rpt::CreateBF create(dev, /*estimated_cardinality=*/1000, {0}, flush);
+    const int T = 8;
+    std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> locals;
+    for (int t = 0; t < T; t++) locals.push_back(create.MakeLocalState());
+    auto t0 = clk::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      th.emplace_back([&, t] {
+        for (size_t k = t; k < bchunks.size(); k += T) create.Sink(*locals[t], bchunks[k]);
+      });
+    for (auto& x : th) x.join();
+    for (auto& l : locals) create.Combine(*l);
+    const double sink_s = std::chrono::duration<double>(clk::now() - t0).count();
+    t0 = clk::now();
+    create.Finalize();
+    const double fin_s = std::chrono::duration<double>(clk::now() - t0).count();
+    // the same rehash from the host-materialized chunks (the reference's rescan, over PCIe)
+    auto bfh = create.GetBloomFilter(0);
+    std::vector<rpt::DataChunk> host_chunks;
+    {
+      auto gs = create.GetGlobalSourceState(1);
+      rpt::CreateBF::LocalSourceState ls;
+      rpt::DataChunk c;
+      while (create.GetData(*gs, ls, c)) host_chunks.push_back(c);
+    }
+    const auto words = bfh->ExportWords();
+    t0 = clk::now();
+    bfh->ReinitializeAndRehash(ctx, n_build, host_chunks, {0});
+    const double host_s = std::chrono::duration<double>(clk::now() - t0).count();
+    printf("{\"op\": \"CreateBF\", \"rows\": %zu, \"sink_threads\": %d, \"sink_flush_rows\": %llu, "
+           "\"sink_combine_rows_per_s\": %.4g, \"finalize_rehash_hbm_ms\": %.2f, \"rehash_from_host_ms\": %.2f, "
+           "\"resized\": %s, \"same_words\": %s}\n",
+           n_build, T, static_cast<unsigned long long>(flush), n_build / sink_s, fin_s * 1e3, host_s * 1e3,
+           create.Resized(0) ? "true" : "false", bfh->ExportWords() == words ? "true" : "false");
   }
   return 0;
 }
