@@ -45,9 +45,6 @@ constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: who
 #ifndef RPT_SLICE_UNROLL
 #define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
 #endif
-#ifndef RPT_SLICE_MASKSEQ
-#define RPT_SLICE_MASKSEQ 0                            // slice probe masks from the 18-word bit sequence
-#endif
 #ifndef RPT_PARTITION_MIN_WAVES
 #define RPT_PARTITION_MIN_WAVES 8                      // 2 partition workgroups per CU (64 VGPRs)
 #endif

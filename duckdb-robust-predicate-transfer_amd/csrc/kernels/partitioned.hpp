@@ -42,24 +42,6 @@ __device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_
   return ((~xl & static_cast<uint32_t>(e)) | (~xh & static_cast<uint32_t>(e >> 32))) == 0u;
 }
 
-#if RPT_SLICE_MASKSEQ
-// The mask from the 18-word bit sequence it is a window of (kMaskBits): the two words a record reads
-// lie in 36 distinct LDS banks, so the table read never conflicts (the 2048-entry table does).
-__device__ __forceinline__ uint64_t seq_entry(const uint64_t* s_seq, uint32_t rec) {
-  const uint32_t id = (rec >> 5) & (kNumMasks - 1), q = id >> 6, sh = id & 63;
-  const uint64_t lo = s_seq[q], hi = s_seq[q + 1];
-  const uint64_t m = ((lo >> sh) | ((hi << 1) << (63 - sh))) & kFullMask;
-  return (rec & 0x8000u) ? rotl64(m, 32) : m;
-}
-__device__ __forceinline__ bool probe_rec_seq(const uint64_t* s_slice, const uint64_t* s_seq, uint32_t rec) {
-  const uint64_t e = seq_entry(s_seq, rec);
-  const uint64_t w = s_slice[rec_word(rec)];
-  const uint32_t wl = static_cast<uint32_t>(w), wh = static_cast<uint32_t>(w >> 32);
-  const uint32_t xl = __builtin_amdgcn_alignbit(wh, wl, rec), xh = __builtin_amdgcn_alignbit(wl, wh, rec);
-  return ((~xl & static_cast<uint32_t>(e)) | (~xh & static_cast<uint32_t>(e >> 32))) == 0u;
-}
-#endif
-
 // ---- partitioned probe, A: bucket a 16 Ki-row tile by filter slice --------------------------------
 // Row r of the tile gets record slice_record(hash) stored at position pos(r) of the tile's
 // slice-sorted record array (runs padded to kRunPad records); pos(r) is
@@ -301,12 +283,7 @@ __device__ __forceinline__ void probe_slice_runs(const uint64_t* s_slice, const 
       for (int u = 0; u < kUnroll; u++) {
         uint32_t bits = 0;
 #pragma unroll
-        for (int e = 0; e < 8; e++)
-#if RPT_SLICE_MASKSEQ
-          bits |= static_cast<uint32_t>(probe_rec_seq(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
-#else
-          bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
-#endif
+        for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
         if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
       }
     }
@@ -335,14 +312,9 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
                                                                    const uint32_t* __restrict__ bucket_tiles,
                                                                    uint32_t n_items) {
   // one LDS array, table first: the slice's base offset folds into the ds_read immediate
-#if RPT_SLICE_MASKSEQ
-  constexpr uint32_t kTable = 18;
-#else
-  constexpr uint32_t kTable = kRotMasks;
-#endif
-  __shared__ uint64_t s_lds[kTable + kSliceWords];
+  __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
   uint64_t* const s_rmasks = s_lds;
-  uint64_t* const s_slice = s_lds + kTable;
+  uint64_t* const s_slice = s_lds + kRotMasks;
   u64x2* const s_slice2 = reinterpret_cast<u64x2*>(s_slice);
   constexpr uint32_t kPre = kSliceWords / 2 / kSliceThreads;  // 16-B pieces of a slice per thread
   SliceWork cur;
@@ -353,11 +325,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 #pragma unroll
     for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = src[threadIdx.x + i * kSliceThreads];
   }
-#if RPT_SLICE_MASKSEQ
-  if (threadIdx.x < kTable) s_rmasks[threadIdx.x] = kMaskBits[threadIdx.x];
-#else
   fill_rot_mask_table(s_rmasks);
-#endif
   const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(tile_slices));
   while (true) {
     __syncthreads();

@@ -392,7 +392,16 @@ void PTBloomFilter::ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_ro
 
 void PTBloomFilter::ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const DeviceKeyColumn& keys) {
   check(rpt_bf_reinitialize(bf_, actual_rows));
-  for (const auto& g : keys.segments()) InsertDevice(ctx, g.col, g.rows);
+  // one workspace sized for the largest segment; the inserts queue back to back on the stream
+  size_t ws_max = 0;
+  for (const auto& g : keys.segments()) ws_max = std::max(ws_max, rpt_bf_insert_workspace_bytes(bf_, g.rows));
+  void* ws = ws_max ? ctx.dev(6, ws_max) : nullptr;
+  for (const auto& g : keys.segments()) {
+    const size_t b = rpt_bf_insert_workspace_bytes(bf_, g.rows);
+    if (b) check(rpt_bf_insert_ws(bf_, &g.col, g.rows, ws, b, ctx.stream()));
+    else check(rpt_bf_insert(bf_, &g.col, g.rows, ctx.stream()));
+  }
+  ctx.synchronize();
 }
 
 uint64_t PTBloomFilter::SizedForRows() const {

@@ -201,6 +201,8 @@ class CreateBF {
   uint64_t MaterializedRows() const { return total_rows_; }
   size_t ChunkCount() const { return all_chunks_.size(); }
   bool Resized(size_t build_column) const { return resized_.at(build_column); }
+  // The build column's keys in HBM (after Combine): a device-side consumer can read them directly.
+  const DeviceKeyColumn& DeviceKeys(size_t build_column) const { return all_keys_.at(build_column); }
   // CreateBFGlobalSinkState::column_min_max[i] (physical_create_bf.cpp:229-272): min / max of the
   // valid keys of build column i, computed by the insert kernels; false when no valid key was seen.
   bool MinMax(size_t build_column, int64_t& min_value, int64_t& max_value) const;

@@ -74,44 +74,61 @@ int main() {
            "\"rows_per_s\": %.4g, \"pass_fraction\": %.4f}\n",
            per_call, rows, calls, s / calls * 1e6, rows / s, static_cast<double>(survivors) / rows);
   }
-  // CREATE_BF end to end: 8 sink threads over 2048-row chunks of the build (sink batches staged to HBM),
-  // Combine, then Finalize with an under-estimated cardinality so the filter is resized and rehashed
-  // -- from the HBM key segments, versus re-staging the materialized host chunks.
-  for (uint64_t flush : {uint64_t(1) << 20, rpt::CreateBF::kDefaultSinkFlushRows}) {
-    rpt::CreateBF create(dev, /*estimated_cardinality=*/1000, {0}, flush);
-    const int T = 8;
-    std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> locals;
-    for (int t = 0; t < T; t++) locals.push_back(create.MakeLocalState());
-    auto t0 = clk::now();
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; t++)
-      th.emplace_back([&, t] {
-        for (size_t k = t; k < bchunks.size(); k += T) create.Sink(*locals[t], bchunks[k]);
-      });
-    for (auto& x : th) x.join();
-    for (auto& l : locals) create.Combine(*l);
-    const double sink_s = std::chrono::duration<double>(clk::now() - t0).count();
-    t0 = clk::now();
-    create.Finalize();
-    const double fin_s = std::chrono::duration<double>(clk::now() - t0).count();
-    // the same rehash from the host-materialized chunks (the reference's rescan, over PCIe)
-    auto bfh = create.GetBloomFilter(0);
-    std::vector<rpt::DataChunk> host_chunks;
-    {
-      auto gs = create.GetGlobalSourceState(1);
-      rpt::CreateBF::LocalSourceState ls;
-      rpt::DataChunk c;
-      while (create.GetData(*gs, ls, c)) host_chunks.push_back(c);
+  // CREATE_BF end to end on a 1e8-row build: 8 sink threads over 2048-row chunks (sink batches staged
+  // to HBM), Combine, then Finalize with an under-estimated cardinality so the filter is resized and
+  // rehashed -- from the HBM key segments -- versus the same rehash re-staging the materialized host
+  // chunks over PCIe (each with a fresh DeviceContext, as Finalize has).
+  {
+    const size_t n_cb = 100000000;
+    std::vector<int64_t> cb(n_cb);
+    for (auto& k : cb) k = static_cast<int64_t>(rng() >> 1);
+    auto cchunks = chunks_of(cb);
+    for (uint64_t flush : {uint64_t(1) << 20, rpt::CreateBF::kDefaultSinkFlushRows, uint64_t(1) << 24}) {
+      rpt::CreateBF create(dev, /*estimated_cardinality=*/1000, {0}, flush);
+      const int T = 8;
+      std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> locals;
+      for (int t = 0; t < T; t++) locals.push_back(create.MakeLocalState());
+      auto t0 = clk::now();
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {  // each thread sinks its chunks, then combines (as DuckDB's pipeline does)
+          for (size_t k = t; k < cchunks.size(); k += T) create.Sink(*locals[t], cchunks[k]);
+          create.Combine(*locals[t]);
+        });
+      for (auto& x : th) x.join();
+      const double sink_s = std::chrono::duration<double>(clk::now() - t0).count();
+      t0 = clk::now();
+      create.Finalize();
+      const double fin_s = std::chrono::duration<double>(clk::now() - t0).count();
+      auto bfh = create.GetBloomFilter(0);
+      const auto words = bfh->ExportWords();
+      double hbm_s, host_s;
+      {
+        t0 = clk::now();
+        rpt::DeviceContext c2(dev);
+        bfh->ReinitializeAndRehash(c2, n_cb, create.DeviceKeys(0));
+        hbm_s = std::chrono::duration<double>(clk::now() - t0).count();
+      }
+      std::vector<rpt::DataChunk> host_chunks;
+      {
+        auto gs = create.GetGlobalSourceState(1);
+        rpt::CreateBF::LocalSourceState ls;
+        rpt::DataChunk c;
+        while (create.GetData(*gs, ls, c)) host_chunks.push_back(c);
+      }
+      {
+        t0 = clk::now();
+        rpt::DeviceContext c3(dev);
+        bfh->ReinitializeAndRehash(c3, n_cb, host_chunks, {0});
+        host_s = std::chrono::duration<double>(clk::now() - t0).count();
+      }
+      printf("{\"op\": \"CreateBF\", \"rows\": %zu, \"sink_threads\": %d, \"sink_flush_rows\": %llu, "
+             "\"segments\": %zu, \"sink_combine_rows_per_s\": %.4g, \"finalize_ms\": %.2f, "
+             "\"rehash_hbm_ms\": %.2f, \"rehash_from_host_ms\": %.2f, \"resized\": %s, \"same_words\": %s}\n",
+             n_cb, T, static_cast<unsigned long long>(flush), create.DeviceKeys(0).segments().size(), n_cb / sink_s,
+             fin_s * 1e3, hbm_s * 1e3, host_s * 1e3, create.Resized(0) ? "true" : "false",
+             bfh->ExportWords() == words ? "true" : "false");
     }
-    const auto words = bfh->ExportWords();
-    t0 = clk::now();
-    bfh->ReinitializeAndRehash(ctx, n_build, host_chunks, {0});
-    const double host_s = std::chrono::duration<double>(clk::now() - t0).count();
-    printf("{\"op\": \"CreateBF\", \"rows\": %zu, \"sink_threads\": %d, \"sink_flush_rows\": %llu, "
-           "\"sink_combine_rows_per_s\": %.4g, \"finalize_rehash_hbm_ms\": %.2f, \"rehash_from_host_ms\": %.2f, "
-           "\"resized\": %s, \"same_words\": %s}\n",
-           n_build, T, static_cast<unsigned long long>(flush), n_build / sink_s, fin_s * 1e3, host_s * 1e3,
-           create.Resized(0) ? "true" : "false", bfh->ExportWords() == words ? "true" : "false");
   }
   return 0;
 }
