@@ -38,14 +38,15 @@ bool valid_bit(const uint64_t* validity, uint64_t idx) {
   return validity == nullptr || ((validity[idx >> 6] >> (idx & 63)) & 1ULL);
 }
 
-// OR `bits` (LSB = row g0) into the validity words at rows [g0, g0 + n), n <= 64. Words at a chunk's
-// edges may be shared with a neighbouring chunk that another thread flattens: those ORs are atomic.
-void or_bits(uint64_t* words, uint64_t g0, uint64_t bits, uint32_t n) {
-  if (n < 64) bits &= (1ULL << n) - 1;
-  if (!bits) return;
+// Clear the validity bits of the NULL rows in `nulls` (LSB = row g0) at rows [g0, g0 + n), n <= 64, in
+// words preset to all-valid. Words at a chunk's edges may be shared with a neighbouring chunk that
+// another thread flattens: those ANDs are atomic.
+void clear_bits(uint64_t* words, uint64_t g0, uint64_t nulls, uint32_t n) {
+  if (n < 64) nulls &= (1ULL << n) - 1;
+  if (!nulls) return;
   const uint64_t w = g0 >> 6, sh = g0 & 63;
-  __atomic_fetch_or(&words[w], bits << sh, __ATOMIC_RELAXED);
-  if (sh && sh + n > 64) __atomic_fetch_or(&words[w + 1], bits >> (64 - sh), __ATOMIC_RELAXED);
+  __atomic_fetch_and(&words[w], ~(nulls << sh), __ATOMIC_RELAXED);
+  if (sh && sh + n > 64) __atomic_fetch_and(&words[w + 1], ~(nulls >> (64 - sh)), __ATOMIC_RELAXED);
 }
 
 // Bits [r, r + n) (n <= 64) of a DuckDB validity mask (nullptr = all valid).
@@ -58,42 +59,45 @@ uint64_t mask_bits(const uint64_t* validity, uint64_t r, uint32_t n) {
 }
 
 // Flatten one column of `chunk` (FLAT / CONSTANT / DICTIONARY) into `keys` (element size of the
-// column) and its row validity bits at row offset `row0` of `valid_words`, 64 rows per step for flat
-// and constant vectors. Returns true if any row was NULL.
+// column) and clear the bits of its NULL rows at row offset `row0` of `valid_words` (preset to
+// all-valid: a chunk without NULLs touches no validity word), 64 rows per step. Returns true if any
+// row was NULL.
 bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* valid_words, uint64_t row0) {
   const size_t es = key_size(v.key_type);
   bool any_null = false;
   switch (v.type) {
     case VectorType::FLAT:
       std::memcpy(keys, v.data, count * es);
-      for (uint64_t r = 0; r < count; r += 64) {
-        const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));
-        const uint64_t b = mask_bits(v.validity, r, n);
-        any_null |= b != (n == 64 ? ~0ULL : (1ULL << n) - 1);
-        or_bits(valid_words, row0 + r, b, n);
+      if (v.validity) {
+        for (uint64_t r = 0; r < count; r += 64) {
+          const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));
+          const uint64_t nulls = ~mask_bits(v.validity, r, n) & (n == 64 ? ~0ULL : (1ULL << n) - 1);
+          any_null |= nulls != 0;
+          clear_bits(valid_words, row0 + r, nulls, n);
+        }
       }
       break;
     case VectorType::CONSTANT: {
-      const bool ok = valid_bit(v.validity, 0);
       for (uint64_t r = 0; r < count; r++) std::memcpy(keys + r * es, v.data, es);
-      any_null = !ok && count > 0;
-      if (ok)
-        for (uint64_t r = 0; r < count; r += 64) or_bits(valid_words, row0 + r, ~0ULL, static_cast<uint32_t>(std::min<uint64_t>(64, count - r)));
+      if (!valid_bit(v.validity, 0) && count > 0) {
+        any_null = true;
+        for (uint64_t r = 0; r < count; r += 64) clear_bits(valid_words, row0 + r, ~0ULL, static_cast<uint32_t>(std::min<uint64_t>(64, count - r)));
+      }
       break;
     }
     case VectorType::DICTIONARY: {
       const uint8_t* src = static_cast<const uint8_t*>(v.data);
       for (uint64_t r = 0; r < count; r += 64) {
         const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));
-        uint64_t b = 0;
+        uint64_t nulls = 0;
         for (uint32_t e = 0; e < n; e++) {
           const uint32_t k = v.sel[r + e];
           if (k >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
           std::memcpy(keys + (r + e) * es, src + static_cast<uint64_t>(k) * es, es);
-          b |= static_cast<uint64_t>(valid_bit(v.validity, k)) << e;
+          nulls |= static_cast<uint64_t>(!valid_bit(v.validity, k)) << e;
         }
-        any_null |= b != (n == 64 ? ~0ULL : (1ULL << n) - 1);
-        or_bits(valid_words, row0 + r, b, n);
+        any_null |= nulls != 0;
+        clear_bits(valid_words, row0 + r, nulls, n);
       }
       break;
     }
@@ -109,22 +113,25 @@ struct Flattened {
   bool any_null;
 };
 
-Flattened flatten_pinned(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col, uint64_t total) {
-  if (chunks.empty()) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "no chunks");
+// Column `col` of chunks[0 .. n_chunks) (total rows) into pinned slots `slot` (keys) and `slot + 1`
+// (validity words).
+Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, size_t n_chunks, uint64_t col,
+                         uint64_t total, int slot) {
+  if (n_chunks == 0) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "no chunks");
   const Vector& v0 = chunks[0]->data.at(col);
   const size_t es = key_size(v0.key_type);
   const uint64_t nwords = (total + 63) / 64;
-  auto* hkeys = static_cast<uint8_t*>(ctx.host(0, std::max<size_t>(total * es, 16)));
-  auto* hvalid = static_cast<uint64_t*>(ctx.host(1, std::max<size_t>(nwords * 8, 8)));
-  std::memset(hvalid, 0, nwords * 8);
-  std::vector<uint64_t> row0(chunks.size() + 1, 0);
-  for (size_t i = 0; i < chunks.size(); i++) {
+  auto* hkeys = static_cast<uint8_t*>(ctx.host(slot, std::max<size_t>(total * es, 16)));
+  auto* hvalid = static_cast<uint64_t*>(ctx.host(slot + 1, std::max<size_t>(nwords * 8, 8)));
+  std::memset(hvalid, 0xFF, nwords * 8);  // all valid; flatten_column clears the NULL rows
+  std::vector<uint64_t> row0(n_chunks + 1, 0);
+  for (size_t i = 0; i < n_chunks; i++) {
     if (chunks[i]->data.at(col).key_type != v0.key_type)
       throw GpuError(RPT_ERR_INVALID_ARGUMENT, "mixed key types in one column");
     row0[i + 1] = row0[i] + chunks[i]->count;
   }
-  // Flattening into the pinned staging buffer is the host side's bottleneck for large batches (one
-  // thread copies ~10 GB/s); big batches are split over a few threads by chunk.
+  // Flattening into the pinned staging buffer is the host side's bottleneck for large batches; big
+  // batches are split over ctx.flatten_threads threads by chunk.
   auto flatten_range = [&](size_t lo, size_t hi) {
     bool nulls = false;
     for (size_t i = lo; i < hi; i++)
@@ -132,16 +139,17 @@ Flattened flatten_pinned(DeviceContext& ctx, const std::vector<const DataChunk*>
     return nulls;
   };
   bool any_null = false;
-  const size_t n_threads = total >= (1u << 20) && chunks.size() >= 16
-                               ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency()))
+  const size_t n_threads = total >= (1u << 20) && n_chunks >= 16
+                               ? std::min<size_t>(std::max<size_t>(ctx.flatten_threads, 1),
+                                                  std::max(1u, std::thread::hardware_concurrency()))
                                : 1;
   if (n_threads <= 1) {
-    any_null = flatten_range(0, chunks.size());
+    any_null = flatten_range(0, n_chunks);
   } else {
     std::vector<std::thread> pool;
     std::vector<char> nulls(n_threads, 0);
     for (size_t t = 0; t < n_threads; t++) {
-      const size_t lo = chunks.size() * t / n_threads, hi = chunks.size() * (t + 1) / n_threads;
+      const size_t lo = n_chunks * t / n_threads, hi = n_chunks * (t + 1) / n_threads;
       pool.emplace_back([&, t, lo, hi] { nulls[t] = flatten_range(lo, hi) ? 1 : 0; });
     }
     for (auto& th : pool) th.join();
@@ -166,7 +174,7 @@ rpt_key_column copy_flattened(DeviceContext& ctx, const Flattened& f, uint64_t t
 
 // Stage column `col` of `chunks` to the device as one flat key column (slots 0/1 of the context).
 rpt_key_column stage(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col, uint64_t total) {
-  const Flattened f = flatten_pinned(ctx, chunks, col, total);
+  const Flattened f = flatten_pinned(ctx, chunks.data(), chunks.size(), col, total, 0);
   void* dkeys = ctx.dev(0, std::max<size_t>(total * key_size(f.key_type), 16));
   void* dvalid = ctx.dev(1, std::max<size_t>((total + 63) / 64 * 8, 8));
   return copy_flattened(ctx, f, total, dkeys, dvalid);
@@ -201,6 +209,70 @@ rpt_key_column stage_key(DeviceContext& ctx, const std::vector<const DataChunk*>
   return hc;
 }
 
+
+// Whole-chunk stages of about `target` rows for the pipelined batch paths (a short tail joins the
+// previous stage). Every chunk's key column must have the same key type.
+struct StageRange {
+  size_t c_lo, c_hi;
+  uint64_t rows;
+};
+std::vector<StageRange> pipeline_stages(const std::vector<const DataChunk*>& chunks, uint64_t col, uint64_t target) {
+  std::vector<StageRange> st;
+  StageRange cur{0, 0, 0};
+  const KeyType kt = chunks.at(0)->data.at(col).key_type;
+  for (size_t i = 0; i < chunks.size(); i++) {
+    if (chunks[i]->data.at(col).key_type != kt) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "mixed key types in one column");
+    cur.rows += chunks[i]->count;
+    cur.c_hi = i + 1;
+    if (cur.rows >= target) {
+      st.push_back(cur);
+      cur = StageRange{i + 1, i + 1, 0};
+    }
+  }
+  if (cur.rows > 0) {
+    if (!st.empty() && cur.rows < target / 2) {
+      st.back().c_hi = cur.c_hi;
+      st.back().rows += cur.rows;
+    } else {
+      st.push_back(cur);
+    }
+  }
+  return st;
+}
+
+}  // namespace
+
+// Double-buffered staging of the pipelined batch paths, sized once for the largest stage (a slot that
+// grows synchronizes both streams, which must not happen mid-pipeline).
+struct PTBloomFilter::PipelineBuffers {
+  static constexpr int kHostKeys = 8;  // host slots 8..11: keys / validity of buffers 0 and 1
+  void* d_keys[2];
+  void* d_valid[2];
+  uint32_t* d_sel[2];
+  uint64_t* d_cnt[2];
+  uint32_t* h_sel[2];
+  uint64_t* h_cnt[2];
+  DeviceContext& ctx;
+  PipelineBuffers(DeviceContext& c, uint64_t max_rows, size_t key_bytes) : ctx(c) {
+    const size_t words = (max_rows + 63) / 64 * 8;
+    for (int b = 0; b < 2; b++) {
+      (void)ctx.host(kHostKeys + 2 * b, std::max<size_t>(max_rows * key_bytes, 16));
+      (void)ctx.host(kHostKeys + 2 * b + 1, std::max<size_t>(words, 8));
+      h_cnt[b] = static_cast<uint64_t*>(ctx.host(12 + b, 8));
+      h_sel[b] = static_cast<uint32_t*>(ctx.host(14 + b, std::max<size_t>(max_rows * 4, 4)));
+      d_keys[b] = ctx.dev(8 + 2 * b, std::max<size_t>(max_rows * key_bytes, 16));
+      d_valid[b] = ctx.dev(9 + 2 * b, std::max<size_t>(words, 8));
+      d_sel[b] = static_cast<uint32_t*>(ctx.dev(12 + b, std::max<size_t>(max_rows * 4, 4)));
+      d_cnt[b] = static_cast<uint64_t*>(ctx.dev(14 + b, 8));
+    }
+  }
+  // stage of buffer b copied to the device / probed (count on its way back) / sel back on the host
+  hipEvent_t staged(int b) { return static_cast<hipEvent_t>(ctx.event(b)); }
+  hipEvent_t probed(int b) { return static_cast<hipEvent_t>(ctx.event(2 + b)); }
+  hipEvent_t returned(int b) { return static_cast<hipEvent_t>(ctx.event(4 + b)); }
+};
+
+namespace {
 }  // namespace
 
 // ---- DeviceContext -----------------------------------------------------------------------------
@@ -214,16 +286,42 @@ DeviceContext::DeviceContext(int device) : device_(device) {
 DeviceContext::~DeviceContext() {
   DeviceScope ds(device_);
   if (stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
+  if (copy_stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(copy_stream_));
   for (auto& b : host_)
     if (b.p) (void)hipHostFree(b.p);
   for (auto& b : dev_)
     if (b.p) (void)hipFree(b.p);
+  for (void* e : events_)
+    if (e) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
+  if (copy_stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(copy_stream_));
   if (stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
 }
 
 void DeviceContext::synchronize() {
   DeviceScope ds(device_);
   check_hip(hipStreamSynchronize(static_cast<hipStream_t>(stream_)), "hipStreamSynchronize");
+  if (copy_stream_) check_hip(hipStreamSynchronize(static_cast<hipStream_t>(copy_stream_)), "hipStreamSynchronize");
+}
+
+void* DeviceContext::copy_stream() {
+  if (!copy_stream_) {
+    DeviceScope ds(device_);
+    hipStream_t s;
+    check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    copy_stream_ = s;
+  }
+  return copy_stream_;
+}
+
+void* DeviceContext::event(int i) {
+  void*& e = events_[i];
+  if (!e) {
+    DeviceScope ds(device_);
+    hipEvent_t ev;
+    check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+    e = ev;
+  }
+  return e;
 }
 
 void* DeviceContext::host(int slot, size_t bytes) {
@@ -284,7 +382,7 @@ const DeviceKeyColumn::Segment& DeviceKeyColumn::Append(DeviceContext& ctx, cons
                                                         uint64_t col) {
   const uint64_t total = total_rows(chunks);
   if (total == 0) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "empty batch");
-  const Flattened f = flatten_pinned(ctx, chunks, col, total);
+  const Flattened f = flatten_pinned(ctx, chunks.data(), chunks.size(), col, total, 0);
   DeviceScope ds(device_);
   void* dkeys = nullptr;
   void* dvalid = nullptr;
@@ -332,7 +430,43 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
                                 const std::vector<uint64_t>& cols) {
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:72-74
+  if (cols.size() == 1 && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
+    InsertPipelined(ctx, chunks, cols[0]);
+    return;
+  }
   InsertDevice(ctx, stage_key(ctx, chunks, cols, total), total);
+}
+
+// Stage by stage: flatten stage i into pinned buffer i % 2 while stage i-1 is copied and inserted
+// (stream order keeps the inserts serial; a pinned buffer is refilled once its copy has finished).
+void PTBloomFilter::InsertPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col) {
+  const std::vector<StageRange> st = pipeline_stages(chunks, col, ctx.pipeline_rows);
+  uint64_t max_rows = 0;
+  size_t ws_bytes = 0;
+  for (const StageRange& r : st) {
+    max_rows = std::max(max_rows, r.rows);
+    ws_bytes = std::max(ws_bytes, rpt_bf_insert_workspace_bytes(bf_, r.rows));
+  }
+  const size_t es = key_size(chunks[st[0].c_lo]->data.at(col).key_type);
+  PipelineBuffers pb(ctx, max_rows, es);
+  void* ws = ws_bytes ? ctx.dev(6, ws_bytes) : nullptr;
+  auto s = static_cast<hipStream_t>(ctx.stream());
+  try {
+    for (size_t i = 0; i < st.size(); i++) {
+      const int b = static_cast<int>(i & 1);
+      if (i >= 2) check_hip(hipEventSynchronize(pb.staged(b)), "hipEventSynchronize");
+      const Flattened f = flatten_pinned(ctx, chunks.data() + st[i].c_lo, st[i].c_hi - st[i].c_lo, col, st[i].rows,
+                                         PipelineBuffers::kHostKeys + 2 * b);
+      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b]);
+      check_hip(hipEventRecord(pb.staged(b), s), "hipEventRecord");
+      if (rpt_bf_insert_workspace_bytes(bf_, st[i].rows)) check(rpt_bf_insert_ws(bf_, &kc, st[i].rows, ws, ws_bytes, s));
+      else check(rpt_bf_insert(bf_, &kc, st[i].rows, s));
+    }
+  } catch (...) {
+    (void)hipStreamSynchronize(s);  // nothing may still read the staging buffers
+    throw;
+  }
+  ctx.synchronize();
 }
 
 void PTBloomFilter::InsertDevice(DeviceContext& ctx, const rpt_key_column& col, uint64_t n) {
@@ -357,6 +491,10 @@ void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const D
   sels.assign(chunks.size(), SelectionVector());
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:63-65
+  if (cols.size() == 1 && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
+    LookupSelPipelined(ctx, chunks, sels, cols[0]);
+    return;
+  }
   rpt_key_column kc = stage_key(ctx, chunks, cols, total);
   const size_t ws_bytes = rpt_bf_probe_workspace_bytes(bf_, total);  // for the strategy this batch runs
   void* ws = ctx.dev(2, ws_bytes);
@@ -378,6 +516,73 @@ void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const D
     SelectionVector& out = sels[i];
     while (k < cnt && h_sel[k] < end) out.push_back(static_cast<uint32_t>(h_sel[k++] - start));
     start = end;
+  }
+}
+
+// Three stages in flight: while the host flattens stage i into pinned buffer i % 2, the compute stream
+// copies and probes stage i-1 (then copies its count back), and the copy stream brings stage i-2's
+// selection vector back (its exact length is known once that stage's count has arrived). A stage's
+// device sel buffer is reused once its copy back has finished (the compute stream waits on it).
+void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                                       std::vector<SelectionVector>& sels, uint64_t col) const {
+  const std::vector<StageRange> st = pipeline_stages(chunks, col, ctx.pipeline_rows);
+  uint64_t max_rows = 0;
+  size_t ws_bytes = 16;
+  for (const StageRange& r : st) {
+    max_rows = std::max(max_rows, r.rows);
+    ws_bytes = std::max(ws_bytes, rpt_bf_probe_workspace_bytes(bf_, r.rows));
+  }
+  const size_t es = key_size(chunks[st[0].c_lo]->data.at(col).key_type);
+  PipelineBuffers pb(ctx, max_rows, es);
+  void* ws = ctx.dev(2, ws_bytes);
+  auto s = static_cast<hipStream_t>(ctx.stream());
+  auto d = static_cast<hipStream_t>(ctx.copy_stream());
+  uint64_t counts[2] = {0, 0};
+  auto count_arrived = [&](size_t j) {  // stage j's count is on the host: copy its sel back exactly
+    const int b = static_cast<int>(j & 1);
+    check_hip(hipEventSynchronize(pb.probed(b)), "hipEventSynchronize");
+    counts[b] = *pb.h_cnt[b];
+    if (counts[b]) {
+      check_hip(hipStreamWaitEvent(d, pb.probed(b), 0), "hipStreamWaitEvent");
+      check_hip(hipMemcpyAsync(pb.h_sel[b], pb.d_sel[b], counts[b] * 4, hipMemcpyDeviceToHost, d), "copy sel");
+    }
+    check_hip(hipEventRecord(pb.returned(b), d), "hipEventRecord");
+  };
+  auto split = [&](size_t j) {  // stage j's ascending sel -> per-chunk sels (ids relative to each chunk)
+    const int b = static_cast<int>(j & 1);
+    check_hip(hipEventSynchronize(pb.returned(b)), "hipEventSynchronize");
+    const uint32_t* h_sel = pb.h_sel[b];
+    uint64_t k = 0, start = 0;
+    for (size_t c = st[j].c_lo; c < st[j].c_hi; c++) {
+      const uint64_t end = start + chunks[c]->count;
+      SelectionVector& out = sels[c];
+      while (k < counts[b] && h_sel[k] < end) out.push_back(static_cast<uint32_t>(h_sel[k++] - start));
+      start = end;
+    }
+  };
+  try {
+    for (size_t i = 0; i < st.size(); i++) {
+      const int b = static_cast<int>(i & 1);
+      if (i >= 2) check_hip(hipEventSynchronize(pb.staged(b)), "hipEventSynchronize");
+      const Flattened f = flatten_pinned(ctx, chunks.data() + st[i].c_lo, st[i].c_hi - st[i].c_lo, col, st[i].rows,
+                                         PipelineBuffers::kHostKeys + 2 * b);
+      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b]);
+      check_hip(hipEventRecord(pb.staged(b), s), "hipEventRecord");
+      if (i >= 2) check_hip(hipStreamWaitEvent(s, pb.returned(b), 0), "hipStreamWaitEvent");
+      check(rpt_bf_probe(bf_, &kc, nullptr, st[i].rows, pb.d_sel[b], pb.d_cnt[b], ws, ws_bytes, s));
+      check_hip(hipMemcpyAsync(pb.h_cnt[b], pb.d_cnt[b], 8, hipMemcpyDeviceToHost, s), "copy count");
+      check_hip(hipEventRecord(pb.probed(b), s), "hipEventRecord");
+      if (i >= 1) count_arrived(i - 1);
+      if (i >= 2) split(i - 2);
+    }
+    const size_t n = st.size();
+    count_arrived(n - 1);
+    if (n >= 2) split(n - 2);
+    split(n - 1);
+  } catch (...) {
+    (void)hipStreamSynchronize(s);  // nothing may still read or write the staging buffers
+    (void)hipStreamSynchronize(d);
+    throw;
   }
 }
 
@@ -464,7 +669,7 @@ void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
     if (v.data == nullptr) continue;  // a column this mirror does not carry
     const size_t es = key_size(v.key_type);
     std::vector<uint64_t> keys((chunk.count * es + 7) / 8 + 1, 0);
-    std::vector<uint64_t> valid((chunk.count + 63) / 64 + 1, 0);
+    std::vector<uint64_t> valid((chunk.count + 63) / 64 + 1, ~0ULL);  // all valid; NULL rows cleared
     const bool any_null = flatten_column(v, chunk.count, reinterpret_cast<uint8_t*>(keys.data()), valid.data(), 0);
     Vector f;
     f.type = VectorType::FLAT;

@@ -68,20 +68,33 @@ class DeviceContext {
   DeviceContext& operator=(const DeviceContext&) = delete;
   int device() const { return device_; }
   void* stream() const { return stream_; }
-  void synchronize();
+  void synchronize();  // both streams
 
   // internal: grow-on-demand buffers
+  static constexpr int kSlots = 16;
   void* host(int slot, size_t bytes);
   void* dev(int slot, size_t bytes);
+  // internal: the device-to-host stream of pipelined batches (created on first use) and its events
+  void* copy_stream();
+  void* event(int i);
+
+  // Single-column batches of at least 2 * pipeline_rows rows are staged in stages of about this many
+  // rows (whole chunks): flattening stage i+1 on the host overlaps the copy and probe / insert of
+  // stage i and the copy back of stage i-1's selection vector.
+  uint64_t pipeline_rows = 1ULL << 22;
+  // Host threads that flatten a batch (or stage) of >= 1 Mi rows into pinned memory.
+  unsigned flatten_threads = 8;
 
  private:
   int device_;
   void* stream_ = nullptr;
+  void* copy_stream_ = nullptr;
   struct Buf {
     void* p = nullptr;
     size_t cap = 0;
   };
-  Buf host_[8], dev_[8];
+  Buf host_[kSlots], dev_[kSlots];
+  void* events_[8] = {};
 };
 
 // One key column kept in HBM, one segment per staged batch: the device half of CREATE_BF's
@@ -131,7 +144,8 @@ class PTBloomFilter {
   // bloom_filter.cpp:60-68: ascending surviving row ids; returns the count
   uint64_t LookupSel(DeviceContext& ctx, const DataChunk& chunk, SelectionVector& sel,
                      const std::vector<uint64_t>& cols) const;
-  // many chunks in one device call; sels[i] holds chunk i's survivors (ids relative to chunk i)
+  // many chunks in one device call (pipelined in stages for large single-column batches, see
+  // DeviceContext::pipeline_rows); sels[i] holds chunk i's survivors (ids relative to chunk i)
   void LookupSelBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                       std::vector<SelectionVector>& sels, const std::vector<uint64_t>& cols) const;
   // Insert a device-resident key column (large batches take the routed inserts; same bits).
@@ -153,6 +167,10 @@ class PTBloomFilter {
   bool finalized_ = false;
 
  private:
+  struct PipelineBuffers;
+  void InsertPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col);
+  void LookupSelPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                          std::vector<SelectionVector>& sels, uint64_t col) const;
   rpt_bf* bf_ = nullptr;
 };
 

@@ -314,6 +314,32 @@ int main() {
         EXPECT(sels[k] == one, "batch lookup differs at chunk %zu", k);
       }
     }
+    // pipelined batches: stages of >= 3000 rows (FLAT / CONSTANT / DICTIONARY chunks, NULLs), both key
+    // types, lookups == per-chunk lookups and inserts == the oracle's words
+    {
+      rpt::DeviceContext pctx(dev);
+      pctx.pipeline_rows = 3000;
+      std::vector<const rpt::DataChunk*> ptrs;
+      for (const auto& ch : pst.chunks) ptrs.push_back(&ch);
+      for (int c = 0; c < 2; c++) {
+        const auto& f = c == 0 ? f0 : f1;
+        std::vector<rpt::SelectionVector> sels;
+        f->LookupSelBatch(pctx, ptrs, sels, {static_cast<uint64_t>(c)});
+        for (size_t k = 0; k < ptrs.size(); k++) {
+          rpt::SelectionVector one;
+          f->LookupSel(ctx, *ptrs[k], one, {static_cast<uint64_t>(c)});
+          EXPECT(sels[k] == one, "pipelined lookup (column %d) differs at chunk %zu", c, k);
+        }
+      }
+      std::vector<const rpt::DataChunk*> bptrs;
+      for (const auto& ch : bst.chunks) bptrs.push_back(&ch);
+      for (int c = 0; c < 2; c++) {
+        rpt::PTBloomFilter fp;
+        fp.Initialize(dev, static_cast<uint32_t>(nb));
+        fp.InsertBatch(pctx, bptrs, {static_cast<uint64_t>(c)});
+        EXPECT(fp.ExportWords() == (c == 0 ? w0 : w1), "pipelined insert (column %d) differs from the oracle", c);
+      }
+    }
     // ---------------- early exits / skips ---------------------------------------------------
     {
       rpt::CreateBF empty(dev, 100, {0});

@@ -1,6 +1,7 @@
 // host_bench.cpp — PCIe-inclusive throughput of the C++ host mirror (include/rpt_host.hpp): host-resident
 // 2048-row DuckDB-style chunks are staged to the device, probed, and their selection vectors copied
-// back, for batches of 1 .. 8192 chunks per device call (LookupSelBatch), plus the batched build and
+// back, for batches of 1 .. 16384 chunks per device call (LookupSelBatch, unpipelined and pipelined in
+// stages of 0.5-4 Mi rows), plus the batched build and
 // CREATE_BF end to end (parallel sink, Combine, Finalize's rehash from HBM vs from host chunks).
 // This is the rate a DuckDB shim calling the mirror would see; it is never the bench's `value`.
 #include <chrono>
@@ -40,15 +41,30 @@ int main() {
   {
     std::vector<const rpt::DataChunk*> all;
     for (auto& c : bchunks) all.push_back(&c);
-    bf.InsertBatch(ctx, all, {0});  // warm-up
-    auto t0 = clk::now();
-    bf.InsertBatch(ctx, all, {0});
-    const double s = std::chrono::duration<double>(clk::now() - t0).count();
-    printf("{\"op\": \"InsertBatch\", \"rows\": %zu, \"chunks_per_call\": %zu, \"rows_per_s\": %.4g}\n", n_build,
-           all.size(), n_build / s);
+    for (uint64_t pr : {uint64_t(~0ULL), uint64_t(1) << 20, uint64_t(1) << 21}) {
+      ctx.pipeline_rows = pr;
+      bf.InsertBatch(ctx, all, {0});  // warm-up
+      auto t0 = clk::now();
+      bf.InsertBatch(ctx, all, {0});
+      const double s = std::chrono::duration<double>(clk::now() - t0).count();
+      printf("{\"op\": \"InsertBatch\", \"rows\": %zu, \"chunks_per_call\": %zu, \"pipeline_rows\": %lld, \"rows_per_s\": %.4g}\n",
+             n_build, all.size(), pr == ~0ULL ? -1LL : static_cast<long long>(pr), n_build / s);
+    }
   }
   bf.finalized_ = true;
-  for (size_t per_call : {1, 16, 128, 1024, 8192}) {
+  struct Case {
+    size_t per_call;
+    uint64_t pipeline_rows;  // ~0: one staged copy per call (no pipeline)
+    unsigned threads = 8;    // flatten threads
+  };
+  std::vector<Case> cases = {{1, ~0ULL}, {16, ~0ULL}, {128, ~0ULL}, {1024, ~0ULL}, {8192, ~0ULL}, {16384, ~0ULL}};
+  for (size_t per_call : {8192, 16384})
+    for (uint64_t pr : {uint64_t(1) << 20, uint64_t(1) << 21, uint64_t(1) << 22}) cases.push_back({per_call, pr});
+  for (unsigned th : {4u, 12u, 16u}) cases.push_back({16384, uint64_t(1) << 22, th});
+  for (const Case& cs : cases) {
+    const size_t per_call = cs.per_call;
+    ctx.pipeline_rows = cs.pipeline_rows;
+    ctx.flatten_threads = cs.threads;
     std::vector<rpt::SelectionVector> sels;
     size_t rows = 0, calls = 0, survivors = 0;
     const size_t max_calls = per_call == 1 ? 2000 : pchunks.size() / per_call;
@@ -70,9 +86,10 @@ int main() {
       calls++;
     }
     const double s = std::chrono::duration<double>(clk::now() - t0).count();
-    printf("{\"op\": \"LookupSelBatch\", \"chunks_per_call\": %zu, \"rows\": %zu, \"calls\": %zu, \"us_per_call\": %.1f, "
-           "\"rows_per_s\": %.4g, \"pass_fraction\": %.4f}\n",
-           per_call, rows, calls, s / calls * 1e6, rows / s, static_cast<double>(survivors) / rows);
+    printf("{\"op\": \"LookupSelBatch\", \"chunks_per_call\": %zu, \"pipeline_rows\": %lld, \"flatten_threads\": %u, \"rows\": %zu, "
+           "\"calls\": %zu, \"us_per_call\": %.1f, \"rows_per_s\": %.4g, \"pass_fraction\": %.4f}\n",
+           per_call, cs.pipeline_rows == ~0ULL ? -1LL : static_cast<long long>(cs.pipeline_rows), cs.threads, rows, calls,
+           s / calls * 1e6, rows / s, static_cast<double>(survivors) / rows);
   }
   // CREATE_BF end to end on a 1e8-row build: 8 sink threads over 2048-row chunks (sink batches staged
   // to HBM), Combine, then Finalize with an under-estimated cardinality so the filter is resized and
