@@ -249,6 +249,14 @@ def main():
         dom_bytes = algorithmic_bytes(dom_name, n_probe, survivors)
         achieved = dom_bytes / (dom_ms * 1e-3)
         traffic = pmc_traffic(dom_name)
+        # whole-step HBM traffic: every kernel of the step at its PMC bytes per launch
+        step_traffic, unprofiled = 0.0, []
+        for name, (calls, _total) in ktimes.items():
+            t = pmc_traffic(name)
+            if t is None:
+                unprofiled.append(name)
+            else:
+                step_traffic += t["bytes_per_launch"] * calls / args.steps
         line = {
             "metric": "bloom probe keys/sec (whole node)",
             "value": value,
@@ -294,6 +302,10 @@ def main():
                 "algorithmic_bytes": probe_bytes,
                 "achieved_GBps": probe_bytes / (probe_ms * 1e-3) / 1e9,
                 "frac": probe_bytes / (probe_ms * 1e-3) / HBM_PEAK_BPS,
+                # HBM bytes the whole step moves (PMC, every kernel) and their rate over the step
+                "traffic": step_traffic if not unprofiled else None,
+                "traffic_GBps": step_traffic / (probe_ms * 1e-3) / 1e9 if not unprofiled else None,
+                "traffic_unprofiled_kernels": unprofiled,
             },
             "build": {
                 "rows": n_build,
