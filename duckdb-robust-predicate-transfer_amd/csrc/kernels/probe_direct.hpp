@@ -43,4 +43,59 @@ __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_
     store_segment_bits<K, DENSE>(pass, lane, seg, out_bits, seg_counts);
   }
 }
+
+// ---- small batches: probe + compaction in ONE workgroup ----------------------------------------
+// A DuckDB-sized call (one to eight 2048-row vectors) is dominated by launch and copy latency, not by
+// bytes: probe_bits + group_sum + group_scan + compact become one launch of one workgroup. Each wave
+// probes whole 512-row segments (gathers from the L2-resident filter) into row-ordered result words
+// in LDS, then the segments' counts are scanned and every wave expands its segments' words into the
+// ascending selection vector. n <= kSmallRows.
+constexpr int kSmallThreads = 1024;
+constexpr uint64_t kSmallRows = RPT_SMALL_PROBE_ROWS;
+template <int K, bool DENSE>
+__global__ __launch_bounds__(kSmallThreads) void probe_small_kernel(const uint64_t* __restrict__ words,
+                                                                   uint64_t block_mask, KeyArgs a, uint64_t n,
+                                                                   const uint32_t* __restrict__ row_sel,
+                                                                   uint32_t* __restrict__ out_sel,
+                                                                   uint64_t* __restrict__ out_count) {
+  constexpr uint32_t kSegs = kSmallRows / kSegRows;
+  constexpr uint32_t kWaves = kSmallThreads / 64;
+  __shared__ uint64_t s_masks[kNumMasks];
+  __shared__ uint64_t s_words[kSegs * kWordsPerSeg];
+  __shared__ uint32_t s_cnt[kSegs];
+  fill_mask_table(s_masks);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t n_segs = static_cast<uint32_t>((n + kSegRows - 1) / kSegRows);
+  for (uint32_t seg = wave; seg < n_segs; seg += kWaves) {
+    uint64_t h[8];
+    bool ok[8], pass[8];
+    load_hashes<K, DENSE>(a, static_cast<uint64_t>(seg) * kSegRows, n, lane, h, ok);
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint64_t m = mask_of(s_masks, h[j]);
+      const uint64_t w = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
+      pass[j] = ok[j] && (w & m) == m;
+    }
+    store_segment_bits<K, DENSE>(pass, lane, seg, s_words, s_cnt);
+  }
+  __syncthreads();
+  // every wave scans the (<= 32) segment counts itself: lane i holds segment i's
+  const uint32_t c = lane < n_segs ? s_cnt[lane] : 0u;
+  const uint32_t incl = wave_inclusive_sum(c);
+  if (threadIdx.x == 0) *out_count = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+  for (uint32_t seg = wave; seg < n_segs; seg += kWaves) {
+    // lanes 0..7 own the segment's 8 result words (64 rows each); pc = their survivors
+    uint64_t word = lane < kWordsPerSeg ? s_words[seg * kWordsPerSeg + lane] : 0ULL;
+    const uint32_t pc = __popcll(word);
+    uint32_t p = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl - c), static_cast<int>(seg))) +
+                 wave_inclusive_sum(pc) - pc;
+    const uint32_t row0 = seg * static_cast<uint32_t>(kSegRows) + lane * 64;
+    while (word) {
+      const uint32_t row = row0 + __builtin_ctzll(word);
+      out_sel[p++] = row_sel ? row_sel[row] : row;
+      word &= word - 1;
+    }
+  }
+}
 }  // namespace rpt

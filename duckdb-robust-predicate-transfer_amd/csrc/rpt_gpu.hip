@@ -409,6 +409,13 @@ void launch_probe_bits_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const r
                      (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
 }
 
+template <int K, bool D>
+void launch_probe_small_t(hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n, const uint32_t* row_sel,
+                          uint32_t* out_sel, uint64_t* out_count) {
+  hipLaunchKernelGGL((rpt::probe_small_kernel<K, D>), dim3(1), dim3(rpt::kSmallThreads), 0, s, bf->words,
+                     (1ULL << bf->log_num_blocks) - 1, a, n, row_sel, out_sel, out_count);
+}
+
 // Whole filter in LDS (dynamic LDS = filter bytes); as many workgroups per CU as LDS allows.
 template <int K, bool D>
 void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
@@ -1072,11 +1079,30 @@ int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, u
   return RPT_OK;
 }
 
+int rpt_bf_probe_is_fused(const rpt_bf* bf, uint64_t n_rows) {
+  if (!bf) return -fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  return n_rows > 0 && n_rows <= rpt::kSmallRows && bf->probe_strategy.load() == RPT_PROBE_AUTO;
+}
+
 int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
                  uint32_t* out_sel, uint64_t* out_count_dev, void* workspace, size_t workspace_bytes,
                  rpt_stream_t stream) {
   if (!bf || !out_count_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
   RPT_ON_DEVICE(bf->device);
+  if (rpt_bf_probe_is_fused(bf, n) == 1) {
+    // small batch: one fused launch, no workspace
+    int st = check_col(col);
+    if (st != RPT_OK) return st;
+    if (!out_sel) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_sel");
+    hipStream_t s = as_stream(stream);
+    const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, row_sel};
+    ProfScope prof_("probe_small_kernel", s);
+    RPT_DISPATCH_KD(launch_probe_small_t, col->key_type, dense_ok(col, row_sel), s, bf, a, n, row_sel, out_sel,
+                    out_count_dev);
+    prof_.end();
+    RPT_LAUNCHED("probe_small_kernel");
+    return RPT_OK;
+  }
   int st = rpt_bf_probe_phase1(bf, col, row_sel, n, workspace, workspace_bytes, stream);
   if (st != RPT_OK) return st;
   return rpt_bf_probe_phase2(bf, row_sel, n, out_sel, out_count_dev, workspace, workspace_bytes, stream);

@@ -210,6 +210,9 @@ rpt_key_column stage_key(DeviceContext& ctx, const std::vector<const DataChunk*>
 }
 
 
+// Batches up to this many rows copy the count and the whole sel capacity back in one copy.
+constexpr uint64_t kSingleCopyRows = RPT_SMALL_PROBE_ROWS;
+
 // Whole-chunk stages of about `target` rows for the pipelined batch paths (a short tail joins the
 // previous stage). Every chunk's key column must have the same key type.
 struct StageRange {
@@ -495,21 +498,64 @@ void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const D
     LookupSelPipelined(ctx, chunks, sels, cols[0]);
     return;
   }
+  if (cols.size() == 1 && rpt_bf_probe_is_fused(bf_, total) == 1) {
+    LookupSelMapped(ctx, chunks, sels, cols[0], total);
+    return;
+  }
   rpt_key_column kc = stage_key(ctx, chunks, cols, total);
   const size_t ws_bytes = rpt_bf_probe_workspace_bytes(bf_, total);  // for the strategy this batch runs
   void* ws = ctx.dev(2, ws_bytes);
-  auto* d_sel = static_cast<uint32_t*>(ctx.dev(3, total * 4));
-  auto* d_cnt = static_cast<uint64_t*>(ctx.dev(4, 8));
+  // [count (8 B) | sel]: small batches bring both back in ONE copy (one sync per call); larger ones
+  // copy the count first and then exactly `count` ids
+  auto* d_out = static_cast<uint8_t*>(ctx.dev(3, 8 + total * 4));
+  auto* d_cnt = reinterpret_cast<uint64_t*>(d_out);
+  auto* d_sel = reinterpret_cast<uint32_t*>(d_out + 8);
   check(rpt_bf_probe(bf_, &kc, nullptr, total, d_sel, d_cnt, ws, ws_bytes, ctx.stream()));
-  auto* h_cnt = static_cast<uint64_t*>(ctx.host(2, 8));
   auto s = static_cast<hipStream_t>(ctx.stream());
-  check_hip(hipMemcpyAsync(h_cnt, d_cnt, 8, hipMemcpyDeviceToHost, s), "copy count");
+  const bool one_copy = total <= kSingleCopyRows;
+  auto* h_out = static_cast<uint8_t*>(ctx.host(2, one_copy ? 8 + total * 4 : 8));
+  check_hip(hipMemcpyAsync(h_out, d_out, one_copy ? 8 + total * 4 : 8, hipMemcpyDeviceToHost, s), "copy count");
   ctx.synchronize();
-  const uint64_t cnt = *h_cnt;
-  auto* h_sel = static_cast<uint32_t*>(ctx.host(3, std::max<uint64_t>(cnt, 1) * 4));
-  if (cnt) check_hip(hipMemcpyAsync(h_sel, d_sel, cnt * 4, hipMemcpyDeviceToHost, s), "copy sel");
-  ctx.synchronize();
+  const uint64_t cnt = *reinterpret_cast<const uint64_t*>(h_out);
+  const uint32_t* h_sel = reinterpret_cast<const uint32_t*>(h_out + 8);
+  if (!one_copy) {
+    auto* hs = static_cast<uint32_t*>(ctx.host(3, std::max<uint64_t>(cnt, 1) * 4));
+    if (cnt) check_hip(hipMemcpyAsync(hs, d_sel, cnt * 4, hipMemcpyDeviceToHost, s), "copy sel");
+    ctx.synchronize();
+    h_sel = hs;
+  }
   // split the batch-wide ascending sel into per-chunk sels
+  uint64_t k = 0, start = 0;
+  for (size_t i = 0; i < chunks.size(); i++) {
+    const uint64_t end = start + chunks[i]->count;
+    SelectionVector& out = sels[i];
+    while (k < cnt && h_sel[k] < end) out.push_back(static_cast<uint32_t>(h_sel[k++] - start));
+    start = end;
+  }
+}
+
+// Per-vector calls (one fused kernel): the kernel reads the flattened keys straight from the pinned
+// staging buffer and writes [count | sel] straight into pinned memory through device-mapped pointers,
+// so a call is one launch and one sync with no copies.
+void PTBloomFilter::LookupSelMapped(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                                    std::vector<SelectionVector>& sels, uint64_t col, uint64_t total) const {
+  const Flattened f = flatten_pinned(ctx, chunks.data(), chunks.size(), col, total, 0);
+  auto* h_out = static_cast<uint8_t*>(ctx.host(2, 8 + total * 4));
+  void *d_keys = nullptr, *d_valid = nullptr, *d_out = nullptr;
+  check_hip(hipHostGetDevicePointer(&d_keys, const_cast<uint8_t*>(f.keys), 0), "hipHostGetDevicePointer");
+  check_hip(hipHostGetDevicePointer(&d_out, h_out, 0), "hipHostGetDevicePointer");
+  if (f.any_null) check_hip(hipHostGetDevicePointer(&d_valid, const_cast<uint64_t*>(f.valid), 0), "hipHostGetDevicePointer");
+  rpt_key_column kc;
+  kc.key_type = static_cast<int32_t>(f.key_type);
+  kc.keys = d_keys;
+  kc.key_sel = nullptr;
+  kc.validity = static_cast<const uint64_t*>(d_valid);
+  auto* d_cnt = static_cast<uint64_t*>(d_out);
+  auto* d_sel = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_out) + 8);
+  check(rpt_bf_probe(bf_, &kc, nullptr, total, d_sel, d_cnt, nullptr, 0, ctx.stream()));
+  ctx.synchronize();
+  const uint64_t cnt = *reinterpret_cast<const volatile uint64_t*>(h_out);
+  const uint32_t* h_sel = reinterpret_cast<const uint32_t*>(h_out + 8);
   uint64_t k = 0, start = 0;
   for (size_t i = 0; i < chunks.size(); i++) {
     const uint64_t end = start + chunks[i]->count;

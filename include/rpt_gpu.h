@@ -176,7 +176,15 @@ int rpt_bf_set_minmax(rpt_bf* bf, int64_t min_value, int64_t max_value, int has_
  * already-sliced chunk of PhysicalUseBF's multi-filter loop, physical_use_bf.cpp:137-183); the
  * written ids are then the row_sel values. n must be < 2^32 (sel_t is uint32). out_sel capacity n.
  * workspace: device memory of rpt_probe_workspace_bytes(n, log_num_blocks) bytes, exclusively owned by this call
- * until it completes on `stream`. */
+ * until it completes on `stream`. Batches of at most RPT_SMALL_PROBE_ROWS rows under the AUTO strategy
+ * run one fused single-workgroup kernel (probe + compaction: one launch instead of four) and leave
+ * the workspace untouched. */
+#define RPT_SMALL_PROBE_ROWS 16384
+/* 1 if rpt_bf_probe of n_rows rows runs the fused small-batch kernel now (AUTO strategy, 1 <= n_rows <=
+ * RPT_SMALL_PROBE_ROWS), else 0; negative rpt_status on error. Its key, validity, row_sel and output
+ * buffers may then be device-mapped pinned host memory (hipHostGetDevicePointer): one launch and no
+ * copies per call. */
+int rpt_bf_probe_is_fused(const rpt_bf* bf, uint64_t n_rows);
 int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
                  uint32_t* out_sel, uint64_t* out_count_dev, void* workspace, size_t workspace_bytes,
                  rpt_stream_t stream);

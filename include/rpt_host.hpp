@@ -171,6 +171,8 @@ class PTBloomFilter {
   void InsertPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col);
   void LookupSelPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                           std::vector<SelectionVector>& sels, uint64_t col) const;
+  void LookupSelMapped(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
+                       std::vector<SelectionVector>& sels, uint64_t col, uint64_t total) const;
   rpt_bf* bf_ = nullptr;
 };
 

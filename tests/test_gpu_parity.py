@@ -361,3 +361,79 @@ def test_row_ids_beyond_int32(rpt, strategy):
     assert 0.1 <= count / n_probe < 0.15
     del probe, sel_t
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("log_nb", [17, 21, 24])
+def test_partitioned_skewed_and_all_null(rpt, log_nb):
+    """Adversarial runs for the partitioned probe and insert: every row of a tile in ONE slice (a run
+    of 16384 records, the tile's whole capacity), 2 distinct keys, and an all-NULL column (every row
+    hashes to NULL_HASH)."""
+    rng = np.random.default_rng(log_nb + 100)
+    base = rng.integers(-2**40, 2**40, size=4096, dtype=np.int64)
+    h = orc.hash_keys(base)
+    slice_of = (h >> np.uint64(16 + 14)) & np.uint64((1 << max(log_nb - 14, 0)) - 1)
+    one = base[slice_of == slice_of[0]][:3]  # keys of one 128 KiB slice
+    n = 3 * 16384 + 501
+    cases = {
+        "one_slice": one[rng.integers(0, one.size, n)],
+        "two_keys": np.where(rng.random(n) < 0.5, base[0], base[1]),
+    }
+    for name, keys in cases.items():
+        w = orc.new_words(log_nb)
+        orc.insert_keys(w, log_nb, keys)
+        bf = rpt.BloomFilter(log_num_blocks=log_nb)
+        bf.insert(dev(keys), strategy=rpt.RPT_INSERT_PARTITIONED)
+        assert np.array_equal(bf.export_words(), w), name
+        probe = np.concatenate([keys, base])
+        bf.probe_strategy = STRATEGIES["partitioned"]
+        sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
+        assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe)), name
+    # all-NULL: inserted NULL rows set the NULL_HASH bits, probed NULL rows test them
+    keys = base[:1].repeat(n)
+    vw = gu.validity_words(np.zeros(n, dtype=bool))
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, keys, validity=vw)
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.insert(dev(keys), validity=dev(vw), strategy=rpt.RPT_INSERT_PARTITIONED)
+    assert np.array_equal(bf.export_words(), w)
+    bf.probe_strategy = STRATEGIES["partitioned"]
+    sel = bf.lookup_sel(dev(keys), validity=dev(vw)).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, log_nb, keys, validity=vw))
+
+
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+@pytest.mark.parametrize("n", [1, 63, 513, 2048, 5000, 16383, 16384, 16385])
+def test_small_batch_fused_probe(rpt, dtype, n):
+    """AUTO batches of <= RPT_SMALL_PROBE_ROWS rows take the fused one-workgroup probe (probe +
+    compaction in one launch): == the oracle and == the forced four-kernel gather path, for flat,
+    unaligned and dictionary vectors with NULLs and a row selection."""
+    rng = np.random.default_rng(n * 3 + (dtype == np.int32))
+    dict_vals = rng.integers(-2**40, 2**40, size=4000, dtype=np.int64).astype(dtype)
+    build_sel = rng.integers(0, dict_vals.size, size=1500).astype(np.uint32)
+    valid = rng.random(dict_vals.size) > 0.05
+    vw = gu.validity_words(valid)
+    bf = rpt.BloomFilter(1500)
+    lnb = bf.log_num_blocks
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, dict_vals, key_sel=build_sel, validity=vw)
+    bf.insert(dev(dict_vals), key_sel=dev(build_sel), validity=dev(vw))
+    assert np.array_equal(bf.export_words(), w)
+    key_sel = rng.integers(0, dict_vals.size, size=n).astype(np.uint32)
+    flat = dict_vals[key_sel]
+    row_sel = np.sort(rng.choice(n, size=max(n // 2, 1), replace=False)).astype(np.uint32)
+    ref_dict = orc.probe_keys(w, lnb, dict_vals, key_sel=key_sel, validity=vw)
+    exp_rowsel = np.intersect1d(row_sel, ref_dict).astype(np.uint32)
+    padded = np.concatenate([flat[:1], flat])  # the same keys one element off 16-B alignment
+    cases = {
+        "flat": (dict(keys=dev(flat)), orc.probe_keys(w, lnb, flat)),
+        "unaligned": (dict(keys=dev(padded)[1:]), orc.probe_keys(w, lnb, flat)),
+        "dict_nulls": (dict(keys=dev(dict_vals), key_sel=dev(key_sel), validity=dev(vw)), ref_dict),
+        "dict_rowsel": (dict(keys=dev(dict_vals), key_sel=dev(key_sel), validity=dev(vw), row_sel=dev(row_sel)),
+                        exp_rowsel),
+    }
+    for name, (kw, exp) in cases.items():
+        keys = kw.pop("keys")
+        for strategy in (rpt.RPT_PROBE_AUTO, rpt.RPT_PROBE_GATHER):
+            bf.probe_strategy = strategy
+            got = bf.lookup_sel(keys, **kw).cpu().numpy().view(np.uint32)
+            assert np.array_equal(got, exp), (name, strategy)
