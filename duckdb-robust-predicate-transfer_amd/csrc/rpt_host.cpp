@@ -437,6 +437,22 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
     InsertPipelined(ctx, chunks, cols[0]);
     return;
   }
+  if (cols.size() == 1 && total <= kSingleCopyRows && rpt_bf_insert_workspace_bytes(bf_, total) == 0) {
+    // small batch, atomic insert: the kernel reads the flattened keys from the pinned staging buffer
+    // through device-mapped pointers (no copy)
+    const Flattened f = flatten_pinned(ctx, chunks.data(), chunks.size(), cols[0], total, 0);
+    void *d_keys = nullptr, *d_valid = nullptr;
+    check_hip(hipHostGetDevicePointer(&d_keys, const_cast<uint8_t*>(f.keys), 0), "hipHostGetDevicePointer");
+    if (f.any_null) check_hip(hipHostGetDevicePointer(&d_valid, const_cast<uint64_t*>(f.valid), 0), "hipHostGetDevicePointer");
+    rpt_key_column kc;
+    kc.key_type = static_cast<int32_t>(f.key_type);
+    kc.keys = d_keys;
+    kc.key_sel = nullptr;
+    kc.validity = static_cast<const uint64_t*>(d_valid);
+    check(rpt_bf_insert(bf_, &kc, total, ctx.stream()));
+    ctx.synchronize();  // the staging buffer is reused by the next call
+    return;
+  }
   InsertDevice(ctx, stage_key(ctx, chunks, cols, total), total);
 }
 

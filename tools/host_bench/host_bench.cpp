@@ -51,6 +51,16 @@ int main() {
              n_build, all.size(), pr == ~0ULL ? -1LL : static_cast<long long>(pr), n_build / s);
     }
   }
+  {  // per-vector Insert (an unbatched Sink): 2000 single 2048-row chunks
+    rpt::PTBloomFilter one;
+    one.Initialize(dev, static_cast<uint32_t>(n_build));
+    one.Insert(ctx, bchunks[0], {0});  // warm-up
+    auto t0 = clk::now();
+    for (size_t c = 0; c < 2000; c++) one.Insert(ctx, bchunks[c], {0});
+    const double s = std::chrono::duration<double>(clk::now() - t0).count();
+    printf("{\"op\": \"Insert\", \"chunks_per_call\": 1, \"calls\": 2000, \"us_per_call\": %.1f, \"rows_per_s\": %.4g}\n",
+           s / 2000 * 1e6, 2000 * 2048 / s);
+  }
   bf.finalized_ = true;
   struct Case {
     size_t per_call;
