@@ -23,11 +23,11 @@ __global__ __launch_bounds__(kTileThreads) void bucket_count_kernel(KeyArgs a, u
   const uint32_t nb = bucket_mask + 1;
   for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_cnt[i] = 0;
   __syncthreads();
-  const uint64_t tile = blockIdx.x, tile_base = tile * kTileRows;
+  const uint64_t tile = blockIdx.x, tile_base = tile * kL1TileRows;
   int64_t wmn = kMinInit, wmx = kMaxInit;
 #pragma unroll
-  for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-    const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+  for (int sg = 0; sg < kL1SegsPerWave; sg++) {
+    const uint32_t seg_local = wave * (kL1SegsPerWave * kSegRows) + sg * kSegRows;
     uint64_t hh[8];
     bool oo[8];
     int64_t mm[2] = {kMinInit, kMaxInit};
@@ -113,8 +113,8 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
                                                                       uint32_t* __restrict__ hash_lo,
                                                                       uint8_t* __restrict__ hash_hi,
                                                                       uint16_t* __restrict__ pos_out) {
-  extern __shared__ uint32_t s_lo[];  // kTileRows hash words (bits 0..31), bucket-sorted, then
-  uint8_t* s_hi = reinterpret_cast<uint8_t*>(s_lo + kTileRows);  // their bits 32..39
+  extern __shared__ uint32_t s_lo[];  // kL1TileRows hash words (bits 0..31), bucket-sorted, then
+  uint8_t* s_hi = reinterpret_cast<uint8_t*>(s_lo + kL1TileRows);  // their bits 32..39
   __shared__ uint32_t s_start[kMaxBuckets], s_cur[kMaxBuckets];
   __shared__ uint64_t s_dst[kMaxBuckets];  // where each bucket's run goes in the level-2 array
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
   // as whole lines.
   const uint32_t per_xcd = gridDim.x / 8, xcd = blockIdx.x % 8;
   const uint64_t tile = blockIdx.x < per_xcd * 8 ? static_cast<uint64_t>(xcd) * per_xcd + blockIdx.x / 8 : blockIdx.x;
-  const uint64_t tile_base = tile * kTileRows;
+  const uint64_t tile_base = tile * kL1TileRows;
   const uint32_t* cnt = counts_tm + tile * nb;
   for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_dst[i] = base[i] + pre_tm[tile * nb + i];
   if (wave == 0) {  // exclusive scan of this tile's bucket counts, kMaxBuckets / 64 per lane
@@ -146,8 +146,8 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
   }
   __syncthreads();
 #pragma unroll
-  for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-    const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+  for (int sg = 0; sg < kL1SegsPerWave; sg++) {
+    const uint32_t seg_local = wave * (kL1SegsPerWave * kSegRows) + sg * kSegRows;
     const uint64_t sbase = tile_base + seg_local;
     uint64_t hh[8];
     bool oo[8];
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
     const uint16_t* __restrict__ pos1, const uint64_t* __restrict__ bits2, uint64_t n, uint32_t bucket_mask,
     const uint32_t* __restrict__ counts_tm, const uint32_t* __restrict__ pre_tm, const uint64_t* __restrict__ base,
     uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
-  __shared__ uint32_t s_bits[kTileRows / 32];
+  __shared__ uint32_t s_bits[kL1TileRows / 32];
   __shared__ uint32_t s_start[kMaxBuckets], s_item[kMaxBuckets + 1], s_cnt[kMaxBuckets];
   __shared__ uint64_t s_g[kMaxBuckets];
   __shared__ uint32_t s_wave[kBucketUnpermuteThreads / 64][2];
@@ -213,15 +213,15 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
   const uint32_t nb = bucket_mask + 1;
   const uint64_t tile = blockIdx.x;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
-  constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / kWaves;
-  const uint64_t seg0 = tile * (kTileRows / kSegRows) + wave * kSegsPerWave;
+  constexpr uint32_t kSegsPerWave = (kL1TileRows / kSegRows) / kWaves;
+  const uint64_t seg0 = tile * (kL1TileRows / kSegRows) + wave * kSegsPerWave;
   u32x4 pv[kSegsPerWave];  // row positions, in flight while the bits are staged
 #pragma unroll
   for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
     pv[sg] = u32x4{0, 0, 0, 0};
     if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos1 + (seg0 + sg) * kSegRows + lane * 8);
   }
-  for (uint32_t i = threadIdx.x; i < kTileRows / 32; i += kBucketUnpermuteThreads) s_bits[i] = 0;
+  for (uint32_t i = threadIdx.x; i < kL1TileRows / 32; i += kBucketUnpermuteThreads) s_bits[i] = 0;
   // per bucket: run length, start in the tile's sorted order, start in bits2, 64-bit pieces (scans by
   // the whole workgroup, kMaxBuckets / 256 buckets per thread)
   constexpr int kPer = kMaxBuckets / kBucketUnpermuteThreads;

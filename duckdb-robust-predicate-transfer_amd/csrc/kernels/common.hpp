@@ -13,40 +13,47 @@ constexpr uint64_t kGroupSegs = 256;               // segments per scan group (o
 constexpr int kBlocksPerCU = 8;
 
 // Partitioned ("routed") probe: the filter is cut into 128 KiB slices that fit in LDS; probe rows are
-// bucketed by slice per 16 Ki-row tile so that every filter access is an LDS read.
+// bucketed by slice per 16 Ki- (or 32 Ki-) row tile so that every filter access is an LDS read.
 #ifndef RPT_SLICE_LOG
 #define RPT_SLICE_LOG 14
 #endif
 constexpr int kSliceLog = RPT_SLICE_LOG;               // 2^13 blocks = 64 KiB (or 2^14 = 128 KiB) per slice
 constexpr uint64_t kSliceWords = 1ULL << kSliceLog;
 constexpr int kMaxSliceCount = 1024;                   // P <= 1024 slices (filters <= 128 MiB at 128 KiB slices)
-#ifndef RPT_TILE_ROWS
-#define RPT_TILE_ROWS 16384
-#endif
-constexpr uint64_t kTileRows = RPT_TILE_ROWS;          // rows per partition tile (8 or 16 per thread)
+constexpr uint64_t kTileRows = 16384;                  // rows per partition tile (x tile_mult for large P)
 // Runs are padded to kRunPad records so a lane owns kRunPad aligned records of one run and its pass
 // results form one byte of bits. Tile capacity is a multiple of 128 so the tile's pass bits are
 // whole 16-byte vectors.
 constexpr uint32_t kRunPad = 8;
 __host__ __device__ constexpr uint32_t pad_run(uint32_t c) { return (c + kRunPad - 1) & ~(kRunPad - 1); }
-__host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices) {
-  return (kTileRows + static_cast<uint64_t>(kRunPad) * n_slices + 127) & ~127ULL;
+// Tiles of tm * kTileRows rows (tm = 1 or 2).
+__host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices, uint32_t tm = 1) {
+  return (kTileRows * tm + static_cast<uint64_t>(kRunPad) * n_slices + 127) & ~127ULL;
 }
+// The plain partitioned strategy doubles its tiles above 512 slices (filters > 64 MiB): a tile's run
+// per slice would otherwise average under 16 records (64 B), and the slice probe's reads fragment
+// (C3, 1024 slices: slice probe 2.67 -> 1.73 ms, partition 2.78 -> 2.66 ms with 32 Ki-row tiles;
+// at 128 slices 32 Ki-row tiles lose: one workgroup per CU, partition 2.31 -> 2.59 ms). The
+// bucketed strategy's level 2 (128 slices per bucket) keeps tm = 1.
+__host__ __device__ constexpr uint32_t tile_mult(uint32_t n_slices) { return n_slices > 512 ? 2u : 1u; }
 // Bucketed strategy (filters > 128 MiB): 16 MiB buckets of 128 slices, at most 1024 buckets (16 GiB).
 constexpr int kBucketSliceLog = 7;
 constexpr uint32_t kBucketSlices = 1u << kBucketSliceLog;
 constexpr uint32_t kMaxBuckets = 1024;
 constexpr int kTileThreads = 1024;                     // 16 waves
 constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
-constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave in the partition kernel
-static_assert(kRowsPerThread == 8 || kRowsPerThread == 16 || kRowsPerThread == 32, "tile = 8, 16 or 32 Ki rows");
+constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave (bucketed level 2 / build)
+// Level-1 tiles of the bucketed strategy (bucket_count / bucket_scatter / bucket_unpermute): 16 Ki rows,
+// independent of the partition tile (the scatter stages 5 B per row in LDS).
+constexpr uint64_t kL1TileRows = 16384;
+constexpr int kL1SegsPerWave = static_cast<int>(kL1TileRows / kTileThreads / 8);
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
 constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
 #ifndef RPT_SLICE_UNROLL
 #define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
 #endif
 #ifndef RPT_PARTITION_MIN_WAVES
-#define RPT_PARTITION_MIN_WAVES 8                      // 2 partition workgroups per CU (64 VGPRs)
+#define RPT_PARTITION_MIN_WAVES 8                      // 2 partition workgroups per CU (64 VGPRs) at tm = 1
 #endif
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));

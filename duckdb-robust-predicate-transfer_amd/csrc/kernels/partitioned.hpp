@@ -42,42 +42,57 @@ __device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_
   return ((~xl & static_cast<uint32_t>(e)) | (~xh & static_cast<uint32_t>(e >> 32))) == 0u;
 }
 
-// ---- partitioned probe, A: bucket a 16 Ki-row tile by filter slice --------------------------------
+// ---- partitioned probe, A: bucket a tile of kTileRows rows by filter slice ------------------------
 // Row r of the tile gets record slice_record(hash) stored at position pos(r) of the tile's
-// slice-sorted record array (runs padded to kRunPad records); pos(r) is
-// written per row (u16) so the unpermute step can restore row order. Per tile the padded runs
-// (start << 16 | length) are written tile-major (one coalesced 4*P-byte row); runs_transpose_kernel
-// turns them slice-major for the slice kernel. Two passes over the rows held in registers: count per
-// slice (LDS atomics), scan, then claim positions with an LDS cursor per slice and scatter.
-// Dynamic LDS: tile_cap record slots, then the per-slice count and cursor arrays.
-template <int K, bool DENSE, bool MM>
-__global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partition_kernel(
+// slice-sorted record array (runs padded to kRunPad records); pos(r) is written per row (u16) so
+// the unpermute step can restore row order. Per tile the padded runs (start << 16 | length) are
+// written tile-major (one coalesced 4*P-byte row); runs_transpose_kernel turns them slice-major for
+// the slice kernel. Two passes over the rows held in registers: count per slice (LDS atomics), scan,
+// then claim positions with an LDS cursor per slice and scatter.
+// TM = 1 (16 Ki rows): the LDS copy of the tile has the padded layout of the output (tile_cap records)
+// and leaves as one contiguous 16-B stream. TM = 2 (32 Ki rows, P > 512, where the padded copy would
+// not fit in 160 KiB): the LDS copy is UNPADDED (kTileRows records) and the padding exists only in global
+// memory. A record at unpadded LDS position q of slice s goes to padded position q + s_delta[s]; the
+// copy-out walks the padded layout in 16-B pieces (a piece never straddles two runs: runs start at
+// multiples of kRunPad) and finds each piece's slice in s_gslice (one u16 per kRunPad-record group).
+// Dynamic LDS (partition_lds_bytes): records, then count / cursor [/ delta] per slice [, s_gslice].
+__host__ __device__ constexpr uint64_t partition_lds_bytes(uint32_t n_slices, uint32_t tm) {
+  return tm == 1 ? tile_cap_for(n_slices, 1) * 4 + 2ULL * n_slices * 4
+                 : kTileRows * tm * 4 + 3ULL * n_slices * 4 + (tile_cap_for(n_slices, tm) / kRunPad) * 2;
+}
+template <int K, bool DENSE, bool MM, int TM>
+__global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4) void partition_kernel(
     KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
     uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm, int64_t* __restrict__ stats,
     const uint32_t* __restrict__ dev_n_tiles) {
   // dev_n_tiles (bucketed strategy): the tile count is only known on the device; the grid is an upper
   // bound and surplus workgroups leave (their run-table rows are never read).
   if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;
+  constexpr bool PAD = TM == 1;
+  constexpr uint64_t kTR = kTileRows * TM;               // rows of this tile
+  constexpr int kRPT = static_cast<int>(kTR / kTileThreads), kSPW = kRPT / 8;
   extern __shared__ uint32_t s_dyn[];
-  const uint64_t tile_cap = tile_cap_for(slice_mask + 1);
-  uint32_t* s_rec = s_dyn;
-  uint32_t* s_cnt = s_dyn + tile_cap;                  // rows per slice in this tile
-  uint32_t* s_cur = s_dyn + tile_cap + slice_mask + 1;  // run start, then scatter cursor (start + count)
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t n_slices = slice_mask + 1;
+  const uint64_t tile_cap = tile_cap_for(n_slices, TM);
+  uint32_t* s_rec = s_dyn;
+  uint32_t* s_cnt = s_dyn + (PAD ? tile_cap : kTR);  // rows per slice in this tile
+  uint32_t* s_cur = s_cnt + n_slices;        // run start (padded if PAD), then scatter cursor (start + count)
+  uint32_t* s_delta = s_cur + n_slices;      // !PAD: padded start - unpadded start
+  uint16_t* s_gslice = reinterpret_cast<uint16_t*>(s_delta + n_slices);  // slice of each kRunPad group
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   {  // one tile per workgroup (no persistent loop: keeps per-lane invariants out of registers)
     const uint64_t tile = blockIdx.x;
     for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads) s_cnt[i] = 0;
     __syncthreads();
-    const uint64_t tile_base = tile * kTileRows;
+    const uint64_t tile_base = tile * kTR;
     // pass 1: hash, stage the record at its row position in LDS, count rows per slice; only the 16-bit
     // slice ids stay in registers (2 per word).
     static_assert(kMaxSliceCount <= 65536, "slice ids are packed as 16 bits");
-    uint32_t sl2[kRowsPerThread / 2] = {};
+    uint32_t sl2[kRPT / 2] = {};
     int64_t wmn = kMinInit, wmx = kMaxInit;  // wave-uniform: the key min/max stays out of VGPRs
 #pragma unroll
-    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-      const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+    for (int sg = 0; sg < kSPW; sg++) {
+      const uint32_t seg_local = wave * (kSPW * kSegRows) + sg * kSegRows;
       uint64_t hh[8];
       bool oo[8];
       int64_t mm[2] = {kMinInit, kMaxInit};
@@ -97,35 +112,45 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
     }
     if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
     __syncthreads();
-    if (wave == 0) {  // exclusive scan of the slice counts, each padded to kRunPad records: kMaxSliceCount/64 per lane
+    if (wave == 0) {  // exclusive scans of the slice counts, unpadded and padded to kRunPad: kMaxSliceCount/64 per lane
       constexpr int kPer = kMaxSliceCount / 64;
-      uint32_t c[kPer], t = 0;
+      uint32_t c[kPer], t = 0, tp = 0;
 #pragma unroll
       for (int i = 0; i < kPer; i++) {
         const uint32_t idx = lane * kPer + i;
-        c[i] = idx < n_slices ? pad_run(s_cnt[idx]) : 0u;
+        c[i] = idx < n_slices ? s_cnt[idx] : 0u;
         t += c[i];
+        tp += pad_run(c[i]);
       }
-      uint32_t off = wave_inclusive_sum(t) - t;
+      uint32_t off = wave_inclusive_sum(t) - t, poff = wave_inclusive_sum(tp) - tp;
 #pragma unroll
       for (int i = 0; i < kPer; i++) {
-        if (lane * kPer + i < n_slices) s_cur[lane * kPer + i] = off;
+        const uint32_t idx = lane * kPer + i;
+        if (idx < n_slices) {
+          if constexpr (PAD) {
+            s_cur[idx] = poff;
+          } else {
+            s_cur[idx] = off;
+            s_delta[idx] = poff - off;
+          }
+        }
         off += c[i];
+        poff += pad_run(c[i]);
       }
     }
     // pass 2: pull this thread's records back out of the row-ordered staging ...
-    uint32_t rec[kRowsPerThread];
+    uint32_t rec[kRPT];
 #pragma unroll
-    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-      const uint32_t seg_local = wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+    for (int sg = 0; sg < kSPW; sg++) {
+      const uint32_t seg_local = wave * (kSPW * kSegRows) + sg * kSegRows;
 #pragma unroll
       for (int j = 0; j < 8; j++) rec[sg * 8 + j] = s_rec[seg_local + seg_row<K, DENSE>(j, lane)];
     }
     __syncthreads();
-    // ... and scatter them to their slice-sorted positions
+    // ... and scatter them to their slice-sorted (unpadded) LDS positions; the row map gets the padded one
 #pragma unroll
-    for (int sg = 0; sg < kSegsPerWaveA; sg++) {
-      const uint64_t base = tile_base + wave * (kSegsPerWaveA * kSegRows) + sg * kSegRows;
+    for (int sg = 0; sg < kSPW; sg++) {
+      const uint64_t base = tile_base + wave * (kSPW * kSegRows) + sg * kSegRows;
       const uint32_t seg_rem = n > base ? static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows) : 0u;
       uint16_t pv[8];
 #pragma unroll
@@ -135,8 +160,9 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
         const bool ok = seg_row<K, DENSE>(j, lane) < seg_rem;
         uint32_t p = 0;
         if (ok) {
-          p = atomicAdd(&s_cur[sl], 1u);
-          s_rec[p] = rec[jj];
+          const uint32_t q = atomicAdd(&s_cur[sl], 1u);
+          s_rec[q] = rec[jj];
+          p = PAD ? q : q + s_delta[sl];
         }
         pv[j] = static_cast<uint16_t>(p);
       }
@@ -162,14 +188,33 @@ __global__ __launch_bounds__(kTileThreads, RPT_PARTITION_MIN_WAVES) void partiti
       }
     }
     __syncthreads();
-    // records of the tile (pad slots hold stale values: probed, never read back); the scatter left
-    // s_cur[i] = start_i + count_i
-    const uint32_t used = s_cur[slice_mask] - s_cnt[slice_mask] + pad_run(s_cnt[slice_mask]);
+    // records of the tile in the padded layout, 16 B per thread and step (pad slots hold stale values:
+    // probed, never read back); the scatter left s_cur[i] = start_i + count_i
     u32x4* dst = reinterpret_cast<u32x4*>(recs + tile * tile_cap);
-    const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
-    for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
-    for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
-      runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i]) << 16) | s_cnt[i];  // start | true count
+    if constexpr (PAD) {
+      const uint32_t used = s_cur[slice_mask] - s_cnt[slice_mask] + pad_run(s_cnt[slice_mask]);
+      const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
+      for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
+      for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
+        runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i]) << 16) | s_cnt[i];  // padded start | true count
+    } else {
+      // each slice owns the kRunPad-record groups of its padded run
+      for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads) {
+        const uint32_t c = s_cnt[i], pst = s_cur[i] - c + s_delta[i];
+        for (uint32_t g = pst / kRunPad; g < (pst + pad_run(c)) / kRunPad; g++) s_gslice[g] = static_cast<uint16_t>(i);
+      }
+      __syncthreads();
+      const uint32_t used = s_cur[slice_mask] + s_delta[slice_mask] - s_cnt[slice_mask] + pad_run(s_cnt[slice_mask]);
+      for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) {
+        const uint32_t q = 4 * i - s_delta[s_gslice[(4 * i) / kRunPad]];  // unpadded position of the piece
+        u32x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = s_rec[min(q + e, static_cast<uint32_t>(kTR) - 1)];
+        dst[i] = v;
+      }
+      for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
+        runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i] + s_delta[i]) << 16) | s_cnt[i];  // padded start | true count
+    }
     __syncthreads();
   }
 }
@@ -308,7 +353,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
                                                                    const uint32_t* __restrict__ recs,
                                                                    const uint32_t* __restrict__ runs,
                                                                    uint8_t* __restrict__ passbits,
-                                                                   uint32_t tile_slices,
+                                                                   uint32_t tile_cap,
                                                                    const uint32_t* __restrict__ bucket_tiles,
                                                                    uint32_t n_items) {
   // one LDS array, table first: the slice's base offset folds into the ds_read immediate
@@ -326,7 +371,6 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
     for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = src[threadIdx.x + i * kSliceThreads];
   }
   fill_rot_mask_table(s_rmasks);
-  const uint32_t tile_cap = static_cast<uint32_t>(tile_cap_for(tile_slices));
   while (true) {
     __syncthreads();
     SliceWork nxt;
@@ -354,7 +398,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
                                                                     uint64_t n_tiles,
                                                                     const uint32_t* __restrict__ recs,
                                                                     const uint32_t* __restrict__ runs,
-                                                                    uint32_t tile_slices,
+                                                                    uint32_t tile_cap,
                                                                     const uint32_t* __restrict__ bucket_tiles) {
   // one LDS array, table first: the slice's base offset folds into the ds_read immediate
   __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
@@ -370,7 +414,6 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
-  const uint64_t tile_cap = tile_cap_for(tile_slices);
   const uint32_t bt = batch_tiles(t_hi - t_lo);  // as slice_probe_kernel
   for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
     const uint32_t info = (lane < bt && tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
@@ -429,6 +472,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
 // each wave's row positions are already in flight; a lane owns 8 consecutive rows of a segment (one
 // 16-B load of positions) and produces byte `lane` of the segment's 512-bit row-ordered result.
 constexpr int kUnpermuteThreads = 256;
+template <int TM>
 __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint16_t* __restrict__ pos,
                                                                      const uint8_t* __restrict__ passbits, uint64_t n,
                                                                      uint64_t tile_cap,
@@ -439,9 +483,9 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint
   extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
-  constexpr uint32_t kSegsPerWave = (kTileRows / kSegRows) / (kUnpermuteThreads / 64);
+  constexpr uint32_t kSegsPerWave = (kTileRows * TM / kSegRows) / (kUnpermuteThreads / 64);
   const uint64_t tile = blockIdx.x;
-  const uint64_t seg0 = tile * (kTileRows / kSegRows) + wave * kSegsPerWave;
+  const uint64_t seg0 = tile * (kTileRows * TM / kSegRows) + wave * kSegsPerWave;
   u32x4 pv[kSegsPerWave];  // 8 row positions (u16) per lane per segment
 #pragma unroll
   for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {

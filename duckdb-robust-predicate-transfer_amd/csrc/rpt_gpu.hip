@@ -257,24 +257,25 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
                        align256(n_groups * 4), align256(n_groups * 4)};
   const bool part = strategy == RPT_PROBE_PARTITIONED, buck = strategy == RPT_PROBE_BUCKETED;
   if (part || buck) {
-    const uint64_t tiles = part ? ceil_div(n, T) : level2_tiles_max(n, log_num_blocks);
     const uint32_t slices = part ? slice_count(log_num_blocks) : rpt::kBucketSlices;
-    const uint64_t cap = rpt::tile_cap_for(slices);
+    const uint32_t tm = part ? rpt::tile_mult(slices) : 1u;
+    const uint64_t tiles = part ? ceil_div(n, T * tm) : level2_tiles_max(n, log_num_blocks);
+    const uint64_t cap = rpt::tile_cap_for(slices, tm);
     sz[4] = align256(tiles * cap * 4);
-    sz[5] = align256(tiles * T * 2);
+    sz[5] = align256(tiles * T * tm * 2);
     sz[6] = align256(tiles * cap / 8);
     sz[7] = align256(static_cast<uint64_t>(slices) * tiles * 4);
     sz[8] = sz[7];
   }
   if (buck) {
-    const uint64_t t1 = ceil_div(n, T), t2 = level2_tiles_max(n, log_num_blocks);
+    const uint64_t t1 = ceil_div(n, rpt::kL1TileRows), t2 = level2_tiles_max(n, log_num_blocks);
     const uint64_t nb = bucket_count(log_num_blocks);
     sz[9] = sz[10] = sz[11] = align256(t1 * nb * 4);
     sz[12] = align256(nb * 4);
     sz[13] = align256((nb + 1) * 8);
     sz[14] = align256((nb + 1) * 4);
     sz[15] = align256(t2 * T * 4);
-    sz[16] = align256(t1 * T * 2);
+    sz[16] = align256(t1 * rpt::kL1TileRows * 2);
     sz[17] = align256(t2 * T / 8);
     sz[18] = align256(t2 * T);
   }
@@ -329,13 +330,14 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
   const bool buck = strategy == RPT_INSERT_BUCKETED;
   if (strategy != RPT_INSERT_PARTITIONED && !buck) return 0;
   const uint64_t T = rpt::kTileRows;
-  const uint64_t tiles = buck ? level2_tiles_max(n, log_num_blocks) : ceil_div(n, T);
   const uint32_t slices = buck ? rpt::kBucketSlices : slice_count(log_num_blocks);
+  const uint32_t tm = buck ? 1u : rpt::tile_mult(slices);
+  const uint64_t tiles = buck ? level2_tiles_max(n, log_num_blocks) : ceil_div(n, T * tm);
   constexpr int kParts = 11;
-  size_t sz[kParts] = {align256(tiles * rpt::tile_cap_for(slices) * 4), align256(static_cast<uint64_t>(slices) * tiles * 4),
+  size_t sz[kParts] = {align256(tiles * rpt::tile_cap_for(slices, tm) * 4), align256(static_cast<uint64_t>(slices) * tiles * 4),
                        align256(static_cast<uint64_t>(slices) * tiles * 4)};
   if (buck) {
-    const uint64_t t1 = ceil_div(n, T), nb = bucket_count(log_num_blocks);
+    const uint64_t t1 = ceil_div(n, rpt::kL1TileRows), nb = bucket_count(log_num_blocks);
     sz[3] = sz[4] = sz[5] = align256(t1 * nb * 4);
     sz[6] = align256(nb * 4);
     sz[7] = align256((nb + 1) * 8);
@@ -434,27 +436,37 @@ void allow_dynamic_lds(const void* fn) {
   (void)hipGetLastError();
 }
 
+template <int K, bool D, bool MM, int TM>
+void launch_partition_tm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
+                         uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
+                         const uint32_t* dev_n_tiles) {
+  const size_t lds = rpt::partition_lds_bytes(slice_mask + 1, TM);
+  static std::once_flag once;  // per instantiation; > 64 KiB of dynamic LDS must be opted into
+  std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM, TM>)); });
+  hipLaunchKernelGGL((rpt::partition_kernel<K, D, MM, TM>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n,
+                     slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+}
+
+// Tiles of tm * kTileRows rows (rpt::tile_mult; the bucketed level 2 always passes tm = 1).
 template <int K, bool D, bool MM>
 void launch_partition_mm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
                          uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
-                         const uint32_t* dev_n_tiles = nullptr) {
-  const uint32_t slices = slice_mask + 1;
-  const size_t lds = rpt::tile_cap_for(slices) * 4 + 2ULL * slices * 4;
-  static std::once_flag once;  // per instantiation; > 64 KiB of dynamic LDS must be opted into
-  std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM>)); });
-  hipLaunchKernelGGL((rpt::partition_kernel<K, D, MM>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, slice_mask,
-                     n_tiles, recs, pos, runs, stats, dev_n_tiles);
+                         const uint32_t* dev_n_tiles, uint32_t tm) {
+  if (tm == 2)
+    launch_partition_tm<K, D, MM, 2>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+  else
+    launch_partition_tm<K, D, MM, 1>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
 }
 
 // stats == nullptr: probe (no min/max); otherwise the build's key min/max is folded into stats.
 template <int K, bool D>
 void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
                         uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
-                        const uint32_t* dev_n_tiles) {
+                        const uint32_t* dev_n_tiles, uint32_t tm) {
   if (rpt::KeyTraits<K>::kValues && stats != nullptr)
-    launch_partition_mm<K, D, true>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+    launch_partition_mm<K, D, true>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles, tm);
   else
-    launch_partition_mm<K, D, false>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, nullptr, dev_n_tiles);
+    launch_partition_mm<K, D, false>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, nullptr, dev_n_tiles, tm);
 }
 
 template <int K, bool D>
@@ -478,7 +490,7 @@ template <int K, bool D>
 void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
                              const uint32_t* counts_tm, const uint32_t* pre_tm, const uint64_t* bbase, uint32_t* hash_lo,
                              uint8_t* hash_hi, uint16_t* pos1) {
-  const size_t lds = rpt::kTileRows * 5;
+  const size_t lds = rpt::kL1TileRows * 5;
   static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into (160 KiB minus the static part)
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D>)); });
   hipLaunchKernelGGL((rpt::bucket_scatter_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, bucket_mask,
@@ -527,7 +539,7 @@ struct BucketLevel1 {
 int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool dense, uint64_t n, int L,
                       const BucketLevel1& w, int64_t* stats) {
   const uint32_t nb = bucket_count(L);
-  const uint64_t t1 = ceil_div(n, rpt::kTileRows);
+  const uint64_t t1 = ceil_div(n, rpt::kL1TileRows);
   {
     ProfScope prof_c("bucket_count_kernel", s);
     RPT_DISPATCH_KD(launch_bucket_count_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm, stats);
@@ -867,8 +879,8 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
   const bool dense = dense_ok(col, nullptr);
   // the partition input: the key column itself, or (bucketed) the level-2 hash array
-  uint32_t tile_slices = slice_count(L);
-  uint64_t n_tiles = ceil_div(n, rpt::kTileRows), n_part = n;
+  uint32_t tile_slices = slice_count(L), tm = rpt::tile_mult(tile_slices);
+  uint64_t n_tiles = ceil_div(n, rpt::kTileRows * tm), n_part = n;
   rpt::KeyArgs pa = a;
   int p_type = col->key_type;
   bool p_dense = dense;
@@ -882,6 +894,7 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
     st = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, bf->stats);
     if (st != RPT_OK) return st;
     tile_slices = rpt::kBucketSlices;
+    tm = 1;
     n_tiles = level2_tiles_max(n, L);
     n_part = n_tiles * rpt::kTileRows;
     pa = rpt::KeyArgs{ws.hash_lo, nullptr, nullptr, nullptr, ws.hash_hi};
@@ -895,10 +908,10 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   ProfScope prof_p("partition_kernel", s);
   if (p_type == rpt::kKeySplit)
     launch_partition_t<rpt::kKeySplit, true>(static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1, n_tiles,
-                                             ws.recs, nullptr, ws.runs_tm, p_stats, dev_n_tiles);
+                                             ws.recs, nullptr, ws.runs_tm, p_stats, dev_n_tiles, 1u);
   else
     RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
-                    n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, p_stats, dev_n_tiles);
+                    n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, p_stats, dev_n_tiles, tm);
   prof_p.end();
   RPT_LAUNCHED("partition_kernel");
   st = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
@@ -907,7 +920,7 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
       std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) / grid_slices)));
   ProfScope prof_i("slice_insert_kernel", s);
   hipLaunchKernelGGL(rpt::slice_insert_kernel, dim3(grid_slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words, splits,
-                     n_tiles, ws.recs, ws.runs, tile_slices, bucket_tiles);
+                     n_tiles, ws.recs, ws.runs, static_cast<uint32_t>(rpt::tile_cap_for(tile_slices, tm)), bucket_tiles);
   prof_i.end();
   RPT_LAUNCHED("slice_insert_kernel");
   return RPT_OK;
@@ -972,8 +985,8 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     // same pipeline over the level-2 hash array (tiles of 128 slices, bucket by bucket), then level 1's
     // unpermute.
     const bool buck = strategy == RPT_PROBE_BUCKETED;
-    uint32_t tile_slices = slice_count(L), grid_slices = tile_slices;
-    uint64_t n_tiles = ceil_div(n, rpt::kTileRows), n_part = n;
+    uint32_t tile_slices = slice_count(L), grid_slices = tile_slices, tm = rpt::tile_mult(tile_slices);
+    uint64_t n_tiles = ceil_div(n, rpt::kTileRows * tm), n_part = n;
     rpt::KeyArgs pa = a;
     int p_type = col->key_type;
     bool p_dense = dense;
@@ -987,6 +1000,7 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
       int st1 = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, nullptr);
       if (st1 != RPT_OK) return st1;
       tile_slices = rpt::kBucketSlices;
+      tm = 1;
       grid_slices = bucket_count(L) * rpt::kBucketSlices;
       n_tiles = level2_tiles_max(n, L);
       n_part = n_tiles * rpt::kTileRows;
@@ -1002,10 +1016,10 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     ProfScope prof5_("partition_kernel", s);
     if (p_type == rpt::kKeySplit)
       launch_partition_t<rpt::kKeySplit, true>(static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1, n_tiles,
-                                               ws.recs, ws.pos, ws.runs_tm, nullptr, dev_n_tiles);
+                                               ws.recs, ws.pos, ws.runs_tm, nullptr, dev_n_tiles, 1u);
     else
       RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
-                      n_tiles, ws.recs, ws.pos, ws.runs_tm, static_cast<int64_t*>(nullptr), dev_n_tiles);
+                      n_tiles, ws.recs, ws.pos, ws.runs_tm, static_cast<int64_t*>(nullptr), dev_n_tiles, tm);
     prof5_.end();
     RPT_LAUNCHED("partition_kernel");
     int st2 = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
@@ -1019,19 +1033,23 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     const uint32_t n_items = grid_slices * splits;
     ProfScope prof6_("slice_probe_kernel", s);
     hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(n_items, resident))),
-                       dim3(rpt::kSliceThreads), 0, s, bf->words, splits, n_tiles, ws.recs, ws.runs, ws.passb, tile_slices,
-                       bucket_tiles, n_items);
+                       dim3(rpt::kSliceThreads), 0, s, bf->words, splits, n_tiles, ws.recs, ws.runs, ws.passb,
+                       static_cast<uint32_t>(rpt::tile_cap_for(tile_slices, tm)), bucket_tiles, n_items);
     prof6_.end();
     RPT_LAUNCHED("slice_probe_kernel");
     ProfScope prof7_("unpermute_kernel", s);
-    const uint64_t cap = rpt::tile_cap_for(tile_slices);
-    hipLaunchKernelGGL(rpt::unpermute_kernel, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8, s,
-                       ws.pos, ws.passb, n_part, cap, part_bits, part_counts, dev_n_tiles);
+    const uint64_t cap = rpt::tile_cap_for(tile_slices, tm);
+    if (tm == 2)
+      hipLaunchKernelGGL(rpt::unpermute_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8,
+                         s, ws.pos, ws.passb, n_part, cap, part_bits, part_counts, dev_n_tiles);
+    else
+      hipLaunchKernelGGL(rpt::unpermute_kernel<1>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8,
+                         s, ws.pos, ws.passb, n_part, cap, part_bits, part_counts, dev_n_tiles);
     prof7_.end();
     RPT_LAUNCHED("unpermute_kernel");
     if (buck) {
       ProfScope prof8b_("bucket_unpermute_kernel", s);
-      hipLaunchKernelGGL(rpt::bucket_unpermute_kernel, dim3(static_cast<unsigned>(ceil_div(n, rpt::kTileRows))),
+      hipLaunchKernelGGL(rpt::bucket_unpermute_kernel, dim3(static_cast<unsigned>(ceil_div(n, rpt::kL1TileRows))),
                          dim3(rpt::kBucketUnpermuteThreads), 0, s, ws.pos1, ws.bits2, n, bucket_count(L) - 1,
                          ws.counts_tm, ws.pre_tm, ws.bbase, ws.bits, ws.seg_counts);
       prof8b_.end();

@@ -85,6 +85,7 @@ SIGNATURES = {
     "rpt_probe_strategy_supported": (c_int, [c_int, c_int]),
     "rpt_bf_probe_strategy": (c_int, [c_void_p]),
     "rpt_bf_probe_strategy_for": (c_int, [c_void_p, c_uint64]),
+    "rpt_bf_probe_is_fused": (c_int, [c_void_p, c_uint64]),
     "rpt_bf_insert_strategy_for": (c_int, [c_void_p, c_uint64]),
     "rpt_bf_probe_workspace_bytes": (c_size_t, [c_void_p, c_uint64]),
     "rpt_bf_create": (c_int, [c_int, c_uint64, POINTER(c_void_p)]),

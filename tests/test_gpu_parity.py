@@ -437,3 +437,22 @@ def test_small_batch_fused_probe(rpt, dtype, n):
             bf.probe_strategy = strategy
             got = bf.lookup_sel(keys, **kw).cpu().numpy().view(np.uint32)
             assert np.array_equal(got, exp), (name, strategy)
+
+
+@pytest.mark.parametrize("n", [1, 32767, 32768, 32769, 3 * 32768 + 5, 300007])
+def test_double_tile_edges_vs_oracle(rpt, n):
+    """Filters of more than 512 slices (here 2^24 blocks = 1024 slices) partition 32 Ki-row tiles
+    with an unpadded LDS copy (rpt::tile_mult): ragged tile boundaries for the probe and the insert."""
+    log_nb = 24
+    rng = np.random.default_rng(n + 5)
+    build = rng.integers(-2**40, 2**40, size=max(n // 2, 1), dtype=np.int64)
+    probe = np.concatenate([build[rng.integers(0, build.size, size=n // 3)],
+                            rng.integers(-2**40, 2**40, size=n - n // 3, dtype=np.int64)])
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, build)
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.insert(dev(build), strategy=rpt.RPT_INSERT_PARTITIONED)
+    assert np.array_equal(bf.export_words(), w)
+    bf.probe_strategy = STRATEGIES["partitioned"]
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
