@@ -30,12 +30,13 @@ __host__ __device__ constexpr uint32_t pad_run(uint32_t c) { return (c + kRunPad
 __host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices, uint32_t tm = 1) {
   return (kTileRows * tm + static_cast<uint64_t>(kRunPad) * n_slices + 127) & ~127ULL;
 }
-// The plain partitioned strategy doubles its tiles above 512 slices (filters > 64 MiB): a tile's run
-// per slice would otherwise average under 16 records (64 B), and the slice probe's reads fragment
-// (C3, 1024 slices: slice probe 2.67 -> 1.73 ms, partition 2.78 -> 2.66 ms with 32 Ki-row tiles;
-// at 128 slices 32 Ki-row tiles lose: one workgroup per CU, partition 2.31 -> 2.59 ms). The
-// bucketed strategy's level 2 (128 slices per bucket) keeps tm = 1.
-__host__ __device__ constexpr uint32_t tile_mult(uint32_t n_slices) { return n_slices > 512 ? 2u : 1u; }
+// The plain partitioned strategy doubles its tiles above 128 slices (filters > 16 MiB): a tile's run
+// per slice would otherwise average under 64 records and the slice probe's reads fragment. Measured
+// (probe ms per 1e9 keys, 16 Ki -> 32 Ki rows): 1024 slices 6.25 -> 5.12, 512 slices 5.05 -> 4.6,
+// 256 slices 4.31 -> 4.30 (build 0.26 -> 0.22 ms), 128 slices 3.95 -> 4.22 (one workgroup per CU
+// costs the partition more than the longer runs save). The bucketed strategy's level 2 (128 slices
+// per bucket) keeps tm = 1.
+__host__ __device__ constexpr uint32_t tile_mult(uint32_t n_slices) { return n_slices > 128 ? 2u : 1u; }
 // Bucketed strategy (filters > 128 MiB): 16 MiB buckets of 128 slices, at most 1024 buckets (16 GiB).
 constexpr int kBucketSliceLog = 7;
 constexpr uint32_t kBucketSlices = 1u << kBucketSliceLog;

@@ -50,7 +50,7 @@ __device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_
 // the slice kernel. Two passes over the rows held in registers: count per slice (LDS atomics), scan,
 // then claim positions with an LDS cursor per slice and scatter.
 // TM = 1 (16 Ki rows): the LDS copy of the tile has the padded layout of the output (tile_cap records)
-// and leaves as one contiguous 16-B stream. TM = 2 (32 Ki rows, P > 512, where the padded copy would
+// and leaves as one contiguous 16-B stream. TM = 2 (32 Ki rows, P > 128; at P = 1024 a padded copy would
 // not fit in 160 KiB): the LDS copy is UNPADDED (kTileRows records) and the padding exists only in global
 // memory. A record at unpadded LDS position q of slice s goes to padded position q + s_delta[s]; the
 // copy-out walks the padded layout in 16-B pieces (a piece never straddles two runs: runs start at

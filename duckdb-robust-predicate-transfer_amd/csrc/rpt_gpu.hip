@@ -245,6 +245,16 @@ uint64_t level2_tiles_max(uint64_t n, int log_num_blocks) {
   return ceil_div(n, rpt::kTileRows) + std::min<uint64_t>(bucket_count(log_num_blocks), n);
 }
 
+// rpt::tile_mult, with its slice threshold overridable for tuning runs (RPT_TILE_MULT_SLICES: tiles
+// double above that many slices).
+uint32_t tile_mult_of(uint32_t n_slices) {
+  static const uint32_t above = [] {
+    const char* e = std::getenv("RPT_TILE_MULT_SLICES");
+    return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : 0u;
+  }();
+  return above ? (n_slices > above ? 2u : 1u) : rpt::tile_mult(n_slices);
+}
+
 // Layout (all 256-aligned): bits | seg_counts | group_sums | group_offs, then for the partitioned
 // strategy recs | pos | passb | runs | runs_tm (whole 16 Ki-row tiles), and for the bucketed one the
 // same level-2 arrays over level2_tiles_max tiles of 128 slices plus the level-1 arrays.
@@ -258,7 +268,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
   const bool part = strategy == RPT_PROBE_PARTITIONED, buck = strategy == RPT_PROBE_BUCKETED;
   if (part || buck) {
     const uint32_t slices = part ? slice_count(log_num_blocks) : rpt::kBucketSlices;
-    const uint32_t tm = part ? rpt::tile_mult(slices) : 1u;
+    const uint32_t tm = part ? tile_mult_of(slices) : 1u;
     const uint64_t tiles = part ? ceil_div(n, T * tm) : level2_tiles_max(n, log_num_blocks);
     const uint64_t cap = rpt::tile_cap_for(slices, tm);
     sz[4] = align256(tiles * cap * 4);
@@ -331,7 +341,7 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
   if (strategy != RPT_INSERT_PARTITIONED && !buck) return 0;
   const uint64_t T = rpt::kTileRows;
   const uint32_t slices = buck ? rpt::kBucketSlices : slice_count(log_num_blocks);
-  const uint32_t tm = buck ? 1u : rpt::tile_mult(slices);
+  const uint32_t tm = buck ? 1u : tile_mult_of(slices);
   const uint64_t tiles = buck ? level2_tiles_max(n, log_num_blocks) : ceil_div(n, T * tm);
   constexpr int kParts = 11;
   size_t sz[kParts] = {align256(tiles * rpt::tile_cap_for(slices, tm) * 4), align256(static_cast<uint64_t>(slices) * tiles * 4),
@@ -879,7 +889,7 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
   const bool dense = dense_ok(col, nullptr);
   // the partition input: the key column itself, or (bucketed) the level-2 hash array
-  uint32_t tile_slices = slice_count(L), tm = rpt::tile_mult(tile_slices);
+  uint32_t tile_slices = slice_count(L), tm = tile_mult_of(tile_slices);
   uint64_t n_tiles = ceil_div(n, rpt::kTileRows * tm), n_part = n;
   rpt::KeyArgs pa = a;
   int p_type = col->key_type;
@@ -985,7 +995,7 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     // same pipeline over the level-2 hash array (tiles of 128 slices, bucket by bucket), then level 1's
     // unpermute.
     const bool buck = strategy == RPT_PROBE_BUCKETED;
-    uint32_t tile_slices = slice_count(L), grid_slices = tile_slices, tm = rpt::tile_mult(tile_slices);
+    uint32_t tile_slices = slice_count(L), grid_slices = tile_slices, tm = tile_mult_of(tile_slices);
     uint64_t n_tiles = ceil_div(n, rpt::kTileRows * tm), n_part = n;
     rpt::KeyArgs pa = a;
     int p_type = col->key_type;
