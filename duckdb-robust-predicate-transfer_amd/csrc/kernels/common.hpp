@@ -25,10 +25,16 @@ constexpr uint64_t kTileRows = 16384;                  // rows per partition til
 // results form one byte of bits. Tile capacity is a multiple of 128 so the tile's pass bits are
 // whole 16-byte vectors.
 constexpr uint32_t kRunPad = 8;
-__host__ __device__ constexpr uint32_t pad_run(uint32_t c) { return (c + kRunPad - 1) & ~(kRunPad - 1); }
+// Runs start at multiples of kRunAlign records (a multiple of kRunPad; tuning: RPT_RUN_ALIGN).
+#ifndef RPT_RUN_ALIGN
+#define RPT_RUN_ALIGN 8
+#endif
+constexpr uint32_t kRunAlign = RPT_RUN_ALIGN;
+static_assert(kRunAlign % kRunPad == 0, "runs start at lane boundaries");
+__host__ __device__ constexpr uint32_t pad_run(uint32_t c) { return (c + kRunAlign - 1) & ~(kRunAlign - 1); }
 // Tiles of tm * kTileRows rows (tm = 1 or 2).
 __host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices, uint32_t tm = 1) {
-  return (kTileRows * tm + static_cast<uint64_t>(kRunPad) * n_slices + 127) & ~127ULL;
+  return (kTileRows * tm + static_cast<uint64_t>(kRunAlign) * n_slices + 127) & ~127ULL;
 }
 // The plain partitioned strategy doubles its tiles above 128 slices (filters > 16 MiB): a tile's run
 // per slice would otherwise average under 64 records and the slice probe's reads fragment. Measured
