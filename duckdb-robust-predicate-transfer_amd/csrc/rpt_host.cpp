@@ -884,4 +884,60 @@ uint64_t UseBF::Execute(DeviceContext& ctx, const DataChunk& input, SelectionVec
   return out.size();
 }
 
+uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& inputs,
+                             std::vector<SelectionVector>& outs) const {
+  outs.assign(inputs.size(), SelectionVector());
+  const uint64_t total = total_rows(inputs);
+  auto all_rows = [&] {
+    for (size_t i = 0; i < inputs.size(); i++) {
+      outs[i].resize(inputs[i]->count);
+      for (uint64_t r = 0; r < inputs[i]->count; r++) outs[i][r] = static_cast<uint32_t>(r);
+    }
+    return total;
+  };
+  if (passthrough_) return all_rows();  // physical_use_bf.cpp:62-66
+  rows_in_ += total;
+  if (filters_.empty() || total == 0) {  // cpp:113-121
+    rows_out_ += total;
+    return all_rows();
+  }
+  if (total >= (1ULL << 32)) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "batch exceeds uint32 row ids");
+  auto s = static_cast<hipStream_t>(ctx.stream());
+  uint32_t* d_rows = nullptr;  // surviving row ids (ascending, over the batch); nullptr = every row
+  uint64_t count = total;
+  int cur = 12;  // device slots 12 / 13: the survivors before and after a filter, 14: the count
+  auto* d_cnt = static_cast<uint64_t*>(ctx.dev(14, 8));
+  auto* h_cnt = static_cast<uint64_t*>(ctx.host(2, 8));
+  for (size_t i = 0; i < filters_.size(); i++) {
+    const auto& bf = filters_[i];
+    if (!bf || !bf->finalized_) continue;  // cpp:139-142
+    if (bf->IsEmpty()) return 0;           // cpp:145-155
+    // this filter's key column for the whole batch; the probe reads only the surviving rows
+    // (row_sel, physical_use_bf.cpp:163,176-179)
+    const rpt_key_column kc = stage(ctx, inputs, cols_[i], total);
+    const size_t ws_bytes = rpt_bf_probe_workspace_bytes(bf->native(), count);
+    void* ws = ctx.dev(2, std::max<size_t>(ws_bytes, 16));
+    auto* d_next = static_cast<uint32_t*>(ctx.dev(cur == 12 ? 13 : 12, std::max<uint64_t>(count, 1) * 4));
+    check(rpt_bf_probe(bf->native(), &kc, d_rows, count, d_next, d_cnt, ws, ws_bytes, s));
+    check_hip(hipMemcpyAsync(h_cnt, d_cnt, 8, hipMemcpyDeviceToHost, s), "copy count");
+    ctx.synchronize();  // the next filter needs the count (and reuses the staging slots)
+    count = *h_cnt;
+    if (count == 0) return 0;  // cpp:166-173
+    d_rows = d_next;
+    cur = cur == 12 ? 13 : 12;
+  }
+  rows_out_ += count;
+  if (d_rows == nullptr) return all_rows();  // every filter skipped
+  auto* h_rows = static_cast<uint32_t*>(ctx.host(3, count * 4));
+  check_hip(hipMemcpyAsync(h_rows, d_rows, count * 4, hipMemcpyDeviceToHost, s), "copy sel");
+  ctx.synchronize();
+  uint64_t k = 0, start = 0;
+  for (size_t i = 0; i < inputs.size(); i++) {
+    const uint64_t end = start + inputs[i]->count;
+    while (k < count && h_rows[k] < end) outs[i].push_back(static_cast<uint32_t>(h_rows[k++] - start));
+    start = end;
+  }
+  return count;
+}
+
 }  // namespace rpt

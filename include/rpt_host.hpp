@@ -256,6 +256,11 @@ class UseBF {
   UseBF(std::vector<std::shared_ptr<PTBloomFilter>> filters, std::vector<uint64_t> bound_column_indices,
         bool passthrough = false);
   uint64_t Execute(DeviceContext& ctx, const DataChunk& input, SelectionVector& out) const;
+  // The same filter chain over many chunks at once (a caching USE_BF): each filter probes the whole
+  // batch's surviving rows in one device call (the survivors stay on the device between filters);
+  // outs[i] == Execute(inputs[i]). Returns the batch's surviving rows.
+  uint64_t ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& inputs,
+                        std::vector<SelectionVector>& outs) const;
   uint64_t rows_in() const { return rows_in_; }
   uint64_t rows_out() const { return rows_out_; }
 

@@ -302,6 +302,25 @@ int main() {
       base += ch.count;
     }
     EXPECT(use.rows_in() == np && use.rows_out() == total, "USE_BF counters");
+    // the same chain over the whole batch at once (survivors stay on the device between filters)
+    {
+      std::vector<const rpt::DataChunk*> ptrs;
+      for (const auto& ch : pst.chunks) ptrs.push_back(&ch);
+      rpt::UseBF ub({f0, f1}, {0, 1});
+      std::vector<rpt::SelectionVector> outs;
+      const uint64_t got = ub.ExecuteBatch(ctx, ptrs, outs);
+      EXPECT(got == total && ub.rows_in() == np && ub.rows_out() == total, "batched USE_BF counters %llu",
+             (unsigned long long)got);
+      for (size_t k = 0; k < ptrs.size(); k++) {
+        rpt::SelectionVector one;
+        use.Execute(ctx, *ptrs[k], one);
+        EXPECT(outs[k] == one, "batched USE_BF differs at chunk %zu", k);
+      }
+      auto nf = std::make_shared<rpt::PTBloomFilter>();
+      nf->Initialize(dev, 10);  // never finalized: skipped
+      rpt::UseBF skip({nf}, {0});
+      EXPECT(skip.ExecuteBatch(ctx, ptrs, outs) == np && outs[1].size() == ptrs[1]->count, "batched skip");
+    }
     // batch lookup == per-chunk lookup
     {
       std::vector<const rpt::DataChunk*> ptrs;

@@ -101,6 +101,53 @@ int main() {
            per_call, cs.pipeline_rows == ~0ULL ? -1LL : static_cast<long long>(cs.pipeline_rows), cs.threads, rows, calls,
            s / calls * 1e6, rows / s, static_cast<double>(survivors) / rows);
   }
+  // USE_BF as DuckDB runs it: T operator threads, each with its own DeviceContext (stream + staging),
+  // each calling LookupSel on one 2048-row vector at a time
+  for (int T : {1, 4, 8, 16}) {
+    const size_t per_thread = 1000;
+    std::vector<std::unique_ptr<rpt::DeviceContext>> ctxs;
+    for (int t = 0; t < T; t++) ctxs.push_back(std::make_unique<rpt::DeviceContext>(dev));
+    for (int t = 0; t < T; t++) {  // warm-up: staging buffers
+      rpt::SelectionVector sv;
+      bf.LookupSel(*ctxs[t], pchunks[t], sv, {0});
+    }
+    std::vector<size_t> surv(T, 0);
+    auto t0 = clk::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      th.emplace_back([&, t] {
+        rpt::SelectionVector sv;
+        for (size_t c = 0; c < per_thread; c++) {
+          bf.LookupSel(*ctxs[t], pchunks[(t * per_thread + c) % pchunks.size()], sv, {0});
+          surv[t] += sv.size();
+        }
+      });
+    for (auto& x : th) x.join();
+    const double s = std::chrono::duration<double>(clk::now() - t0).count();
+    const double rows = static_cast<double>(T) * per_thread * 2048;
+    printf("{\"op\": \"LookupSel\", \"threads\": %d, \"calls_per_thread\": %zu, \"us_per_call\": %.1f, \"rows_per_s\": %.4g}\n",
+           T, per_thread, s / per_thread * 1e6, rows / s);
+  }
+  // a caching USE_BF: UseBF::ExecuteBatch over 16 .. 1024 chunks per call (one filter)
+  {
+    rpt::UseBF ub({std::shared_ptr<rpt::PTBloomFilter>(&bf, [](rpt::PTBloomFilter*) {})}, {0});
+    for (size_t per_call : {16, 128, 1024}) {
+      std::vector<rpt::SelectionVector> outs;
+      std::vector<const rpt::DataChunk*> b;
+      for (size_t k = 0; k < per_call; k++) b.push_back(&pchunks[k]);
+      ub.ExecuteBatch(ctx, b, outs);  // warm-up
+      const size_t calls = std::min<size_t>(pchunks.size() / per_call, 256);
+      auto t0 = clk::now();
+      for (size_t c = 0; c < calls; c++) {
+        b.clear();
+        for (size_t k = 0; k < per_call; k++) b.push_back(&pchunks[c * per_call + k]);
+        ub.ExecuteBatch(ctx, b, outs);
+      }
+      const double s = std::chrono::duration<double>(clk::now() - t0).count();
+      printf("{\"op\": \"UseBF::ExecuteBatch\", \"chunks_per_call\": %zu, \"calls\": %zu, \"us_per_call\": %.1f, \"rows_per_s\": %.4g}\n",
+             per_call, calls, s / calls * 1e6, static_cast<double>(calls) * per_call * 2048 / s);
+    }
+  }
   // CREATE_BF end to end on a 1e8-row build: 8 sink threads over 2048-row chunks (sink batches staged
   // to HBM), Combine, then Finalize with an under-estimated cardinality so the filter is resized and
   // rehashed -- from the HBM key segments -- versus the same rehash re-staging the materialized host
