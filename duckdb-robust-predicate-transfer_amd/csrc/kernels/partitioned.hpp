@@ -329,6 +329,94 @@ __device__ __forceinline__ void probe_slice_runs(const uint64_t* s_slice, const 
         uint32_t bits = 0;
 #pragma unroll
         for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
+#ifdef RPT_EXP_NO_PASS_WRITE  // experiment: pass-bit stores suppressed (the test still runs)
+        if (off[u] != ~0u && bits == tile_cap) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
+#else
+        if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
+#endif
+      }
+    }
+  }
+}
+
+// Inclusive wave-wide max scan of non-negative values (DPP: rows of 16, then row broadcasts 15 / 31).
+__device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false)));
+  return v;
+}
+
+// Same walk as probe_slice_runs, with the slot -> run lookup through a per-wave LDS window instead of
+// a uniform loop over the runs a step overlaps (whose cost grows with the number of runs per step:
+// ~14 at P = 1024). A slot is 8 records (kRunPad) of one run; a window is the kUnroll steps of 64
+// slots a wave has in flight. Per window each non-empty run marks its first slot in the window with
+// its lane + 1 (the run covering the window start marks slot 0), a max scan over the window carries
+// the marks forward, and two ds_bpermutes fetch the run's base slot and stream prefix: ~15 VALU per
+// step whatever the run lengths.
+__device__ __forceinline__ void probe_slice_runs_tbl(const uint64_t* s_slice, const uint64_t* s_rmasks,
+                                                     uint32_t* s_win, const SliceWork& sw, uint64_t n_tiles,
+                                                     const uint32_t* __restrict__ recs,
+                                                     const uint32_t* __restrict__ runs,
+                                                     uint8_t* __restrict__ passbits, uint32_t tile_cap) {
+  constexpr int kUnroll = RPT_SLICE_UNROLL;
+  constexpr uint32_t kWin = 64 * kUnroll;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr uint32_t kWaves = kSliceThreads / 64;
+  uint32_t* win = s_win + wave * kWin;
+  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
+  const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
+  const uint32_t bt = batch_tiles(t_hi - t_lo);
+  const uint32_t my = lane < bt ? lane : ~0u >> 1;  // lanes >= bt hold no run
+  uint32_t info_next = (t_lo + wave * bt + my < t_hi) ? my_runs[t_lo + wave * bt + my] : 0u;
+  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
+    const uint32_t info = info_next;  // the next batch's runs are fetched while this one is probed
+    info_next = (tb + kWaves * bt + my < t_hi) ? my_runs[tb + kWaves * bt + my] : 0u;
+    const uint32_t nslot = pad_run(info & 0xFFFFu) / kRunPad;
+    const uint32_t base = (lane * tile_cap + (info >> 16)) / kRunPad;  // first slot, relative to the batch
+    const uint32_t* brecs = recs + tb * tile_cap;                     // uniform
+    uint8_t* bpass = passbits + tb * (tile_cap / kRunPad);
+    const uint32_t incl = wave_inclusive_sum(nslot);
+    const uint32_t excl = incl - nslot;
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    const int base_m_excl = static_cast<int>(base - excl);  // slot s of this run -> base + (s - excl)
+    for (uint32_t w0 = 0; w0 < total; w0 += kWin) {
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) win[u * 64 + lane] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (nslot != 0 && excl < w0 + kWin && incl > w0) win[(excl > w0 ? excl : w0) - w0] = lane + 1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      uint32_t off[kUnroll];
+      u32x4 rec[kUnroll][2];
+      uint32_t carry = 0;
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        const uint32_t slot = w0 + u * 64 + lane;
+        uint32_t m = wave_inclusive_max(win[u * 64 + lane]);
+        m = max(m, carry);
+        carry = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(m), 63));
+        const int src = static_cast<int>(m - 1) << 2;  // lane of the run holding this slot (byte address)
+        const uint32_t rel = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, base_m_excl)) + slot;
+        off[u] = slot < total ? rel * kRunPad : ~0u;
+        rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
+        if (w0 + u * 64 < total && off[u] != ~0u) {  // (first test uniform: the window's tail steps)
+          rec[u][0] = *reinterpret_cast<const u32x4*>(brecs + off[u]);
+          rec[u][1] = *reinterpret_cast<const u32x4*>(brecs + off[u] + 4);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int u = 0; u < kUnroll; u++) {
+        if (w0 + u * 64 >= total) break;  // uniform: a batch's last window is often part-filled
+        uint32_t bits = 0;
+#pragma unroll
+        for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
         if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
       }
     }
@@ -361,6 +449,9 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   uint64_t* const s_rmasks = s_lds;
   uint64_t* const s_slice = s_lds + kRotMasks;
   u64x2* const s_slice2 = reinterpret_cast<u64x2*>(s_slice);
+#if RPT_SLICE_SLOT_TABLE
+  __shared__ uint32_t s_win[kSliceThreads * RPT_SLICE_UNROLL];  // per-wave slot windows (16 KiB)
+#endif
   constexpr uint32_t kPre = kSliceWords / 2 / kSliceThreads;  // 16-B pieces of a slice per thread
   SliceWork cur;
   uint32_t item = next_item(blockIdx.x, n_items, splits, n_tiles, bucket_tiles, cur);
@@ -381,7 +472,11 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 #pragma unroll
       for (uint32_t i = 0; i < kPre; i++) pre[i] = src[threadIdx.x + i * kSliceThreads];
     }
+#if RPT_SLICE_SLOT_TABLE
+    probe_slice_runs_tbl(s_slice, s_rmasks, s_win, cur, n_tiles, recs, runs, passbits, tile_cap);
+#else
     probe_slice_runs(s_slice, s_rmasks, cur, n_tiles, recs, runs, passbits, tile_cap);
+#endif
     if (nitem >= n_items) break;
     __syncthreads();  // every wave is done with this slice
     for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = pre[i];  // unrolled by the compiler
