@@ -499,6 +499,9 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
   uint64_t* const s_rmasks = s_lds;
   uint64_t* const s_slice = s_lds + kRotMasks;
+#if RPT_SLICE_SLOT_TABLE
+  __shared__ uint32_t s_win[kSliceThreads * RPT_SLICE_UNROLL];  // per-wave slot windows (16 KiB)
+#endif
   const SliceWork sw = slice_work(blockIdx.x, splits, n_tiles, bucket_tiles);
   const uint32_t slice = sw.slice;
   const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
@@ -510,6 +513,65 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   constexpr uint32_t kWaves = kSliceThreads / 64;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
   const uint32_t bt = batch_tiles(t_hi - t_lo);  // as slice_probe_kernel
+#if RPT_SLICE_SLOT_TABLE
+  // slot -> run through the wave's LDS window, as probe_slice_runs_tbl
+  constexpr uint32_t kWin = 64 * RPT_SLICE_UNROLL;
+  uint32_t* win = s_win + wave * kWin;
+  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
+    const uint32_t info = (lane < bt && tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
+    const uint32_t real = info & 0xFFFFu;  // records of the run (pad slots are stale)
+    const uint32_t nslot = pad_run(real) / kRunPad;
+    const uint32_t base = (lane * tile_cap + (info >> 16)) / kRunPad;  // first slot, relative to the batch
+    const uint32_t* brecs = recs + tb * tile_cap;                     // uniform
+    const uint32_t incl = wave_inclusive_sum(nslot);
+    const uint32_t excl = incl - nslot;
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    const int base_m_excl = static_cast<int>(base - excl);
+    const int real_p_excl = static_cast<int>(real + excl * kRunPad);  // real records before slot s: s*8 - excl*8
+    for (uint32_t w0 = 0; w0 < total; w0 += kWin) {
+#pragma unroll
+      for (int u = 0; u < RPT_SLICE_UNROLL; u++) win[u * 64 + lane] = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (nslot != 0 && excl < w0 + kWin && incl > w0) win[(excl > w0 ? excl : w0) - w0] = lane + 1;
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      uint32_t nreal[RPT_SLICE_UNROLL];
+      u32x4 rec[RPT_SLICE_UNROLL][2];
+      uint32_t carry = 0;
+#pragma unroll
+      for (int u = 0; u < RPT_SLICE_UNROLL; u++) {
+        const uint32_t slot = w0 + u * 64 + lane;
+        uint32_t m = wave_inclusive_max(win[u * 64 + lane]);
+        m = max(m, carry);
+        carry = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(m), 63));
+        const int src = static_cast<int>(m - 1) << 2;
+        const uint32_t rel = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, base_m_excl)) + slot;
+        const int left = __builtin_amdgcn_ds_bpermute(src, real_p_excl) - static_cast<int>(slot * kRunPad);
+        nreal[u] = (slot < total && left > 0) ? (left < static_cast<int>(kRunPad) ? static_cast<uint32_t>(left) : kRunPad) : 0u;
+        rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
+        if (w0 + u * 64 < total && nreal[u] != 0) {
+          rec[u][0] = *reinterpret_cast<const u32x4*>(brecs + rel * kRunPad);
+          rec[u][1] = *reinterpret_cast<const u32x4*>(brecs + rel * kRunPad + 4);
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int u = 0; u < RPT_SLICE_UNROLL; u++) {
+        if (w0 + u * 64 >= total) break;  // uniform
+#pragma unroll
+        for (uint32_t e = 0; e < kRunPad; e++) {
+          if (e < nreal[u]) {
+            const uint32_t rec1 = rec[u][e >> 2][e & 3];
+            atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[rec_word(rec1)]),
+                     static_cast<unsigned long long>(rec_mask(s_rmasks, rec1)));
+          }
+        }
+      }
+    }
+  }
+#else
   for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
     const uint32_t info = (lane < bt && tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
     const uint32_t real = info & 0xFFFFu;      // records of the run
@@ -554,6 +616,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
       }
     }
   }
+#endif
   __syncthreads();
   uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
   for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
