@@ -267,6 +267,21 @@ __device__ __forceinline__ SliceWork slice_work(uint32_t item, uint32_t splits, 
   return SliceWork{slice, row, lo + cnt * part / splits, lo + cnt * (part + 1) / splits};
 }
 
+// Work items are dealt to workgroups round-robin, and workgroup b runs on XCD b % 8. With
+// RPT_SLICE_XCD_MAP the items are renumbered so that each XCD gets a contiguous range of
+// (slice, split) items. The workgroups resident on one XCD then probe adjacent slices over the same
+// tiles at about the same time. Adjacent slices' runs are adjacent in each tile, so a run's partial
+// first and last 128-B lines, fetched by its neighbour's workgroup, can be L2 hits instead of
+// over-fetch. Needs item and grid counts divisible by the XCD count (otherwise: identity).
+#ifndef RPT_SLICE_XCD_MAP
+#define RPT_SLICE_XCD_MAP 1
+#endif
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t xcd_item(uint32_t item, uint32_t n_items) {
+  if (!RPT_SLICE_XCD_MAP || n_items % kXcds != 0 || gridDim.x % kXcds != 0) return item;
+  return (item % kXcds) * (n_items / kXcds) + item / kXcds;
+}
+
 // Probe the runs of tiles [sw.t_lo, sw.t_hi) of one slice held in LDS (see above).
 // Tiles per wave batch: 64 (one run per lane), or fewer so that all kSliceThreads/64 waves get work.
 __device__ __forceinline__ uint32_t batch_tiles(uint64_t n_t) {
@@ -427,7 +442,7 @@ __device__ __forceinline__ void probe_slice_runs_tbl(const uint64_t* s_slice, co
 __device__ __forceinline__ uint32_t next_item(uint32_t item, uint32_t n_items, uint32_t splits, uint64_t n_tiles,
                                               const uint32_t* bucket_tiles, SliceWork& sw) {
   for (; item < n_items; item += gridDim.x) {
-    sw = slice_work(item, splits, n_tiles, bucket_tiles);
+    sw = slice_work(xcd_item(item, n_items), splits, n_tiles, bucket_tiles);
     if (sw.t_lo < sw.t_hi) break;
   }
   return item;
@@ -502,7 +517,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
 #if RPT_SLICE_SLOT_TABLE
   __shared__ uint32_t s_win[kSliceThreads * RPT_SLICE_UNROLL];  // per-wave slot windows (16 KiB)
 #endif
-  const SliceWork sw = slice_work(blockIdx.x, splits, n_tiles, bucket_tiles);
+  const SliceWork sw = slice_work(xcd_item(blockIdx.x, gridDim.x), splits, n_tiles, bucket_tiles);
   const uint32_t slice = sw.slice;
   const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
   if (t_lo >= t_hi) return;  // no rows reach this slice (uniform)
