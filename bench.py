@@ -54,10 +54,12 @@ def parse():
 def algorithmic_bytes(kernel: str, n: int, survivors: int) -> int:
     """SURVEY §8(d) per-unit bytes for the kernel's part of the probe: every kernel that streams the
     key column is charged 8 B/key (the key read; its own intermediates are implementation traffic,
-    counted in `traffic`); the compaction is charged the 4 B/survivor selection vector it writes."""
-    if kernel.startswith("compact"):
+    counted in `traffic`); the kernels that write the selection vector (the compaction, or the fused
+    unpermute) are charged the 4 B/survivor they write."""
+    if kernel.startswith(("compact", "unpermute_sel")):
         return SEL_BYTES * survivors
-    if kernel.startswith(("slice_probe", "unpermute", "group_", "bucket_unpermute", "bucket_scan", "runs_transpose")):
+    if kernel.startswith(("slice_probe", "unpermute", "group_", "bucket_unpermute", "bucket_scan", "runs_transpose",
+                          "tile_count")):
         return 0
     return KEY_BYTES * n
 
@@ -202,19 +204,17 @@ def main():
     stream = torch.cuda.current_stream(device)
 
     def step(ev=None):
+        # one LookupSel over the whole per-GPU column (rpt_bf_probe: hash, probe, ascending sel)
         if ev is not None:
             ev[0].record(stream)
-        bf.probe_phase1(keys, ws, n=n_probe)
+        bf.probe_async(keys, n=n_probe, out_sel=out_sel, out_count=out_count, workspace=ws)
         if ev is not None:
             ev[1].record(stream)
-        bf.probe_phase2(n_probe, out_sel, out_count, ws)
-        if ev is not None:
-            ev[2].record(stream)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    events = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    events = [[torch.cuda.Event(enable_timing=True) for _ in range(2)] for _ in range(args.steps)]
     # per-kernel HIP events on the launch stream (rpt_profiling_*) over the timed region
     rpt_lib.profiling_reset()
     rpt_lib.profiling(True)
@@ -230,8 +230,7 @@ def main():
     ktimes = rpt_lib.kernel_times()
 
     survivors = int(out_count.item())
-    p1_ms = statistics.mean(e[0].elapsed_time(e[1]) for e in events)
-    probe_ms = statistics.mean(e[0].elapsed_time(e[2]) for e in events)
+    probe_ms = statistics.mean(e[0].elapsed_time(e[1]) for e in events)
 
     t = torch.tensor([elapsed, (t1 - t0) / build_reps, t2 - t1], dtype=torch.float64,
                      device=device if backend == "nccl" else "cpu")
@@ -296,7 +295,6 @@ def main():
                 "algorithmic_bytes_per_launch": dom_bytes,
             },
             "kernels_ms": {k: v[1] / v[0] for k, v in sorted(ktimes.items(), key=lambda kv: -kv[1][1])},
-            "phase1_ms": p1_ms,
             "probe_total": {
                 "avg_ms": probe_ms,
                 "algorithmic_bytes": probe_bytes,

@@ -56,9 +56,6 @@ constexpr uint64_t kL1TileRows = 16384;
 constexpr int kL1SegsPerWave = static_cast<int>(kL1TileRows / kTileThreads / 8);
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
 constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
-#ifndef RPT_SLICE_SLOT_TABLE
-#define RPT_SLICE_SLOT_TABLE 1                         // slice probe: slot -> run via a per-wave LDS window
-#endif
 #ifndef RPT_SLICE_UNROLL
 #define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
 #endif

@@ -243,9 +243,9 @@ __global__ __launch_bounds__(kBlockThreads) void runs_transpose_kernel(const uin
 // The runs of 64 consecutive tiles are walked as ONE flattened record stream per wave: record k of
 // the stream belongs to the tile whose inclusive run-length prefix first exceeds k. Runs are padded
 // to kRunPad = 8 records, so each lane owns 8 consecutive, 32-byte aligned records of one run: two
-// 16-B loads and one byte of pass bits per lane, 512 records per wave step. The (uniform) tile cursor
-// lives in scalar registers; a step visits only the few tiles its 512 records overlap. Record offsets
-// are 32-bit relative to the batch's first tile (a uniform base pointer).
+// 16-B loads and one byte of pass bits per lane, 512 records per wave step. Each lane finds the run
+// of its 8-record slot through a per-wave LDS window (probe_slice_runs_tbl). Record offsets are
+// 32-bit relative to the batch's first tile (a uniform base pointer).
 // Which tiles and run-table row a slice workgroup walks. Plain partitioned: all n_tiles tiles, run row
 // = slice. Bucketed (bucket_tiles != nullptr): global slice g = bucket * kBucketSlices + local slice;
 // the bucket's tiles are [bucket_tiles[b], bucket_tiles[b+1]) and the run row is the local slice.
@@ -289,71 +289,6 @@ __device__ __forceinline__ uint32_t batch_tiles(uint64_t n_t) {
   return static_cast<uint32_t>(n_t >= 64 * kWaves ? 64 : (n_t + kWaves - 1) / kWaves);
 }
 
-__device__ __forceinline__ void probe_slice_runs(const uint64_t* s_slice, const uint64_t* s_rmasks, const SliceWork& sw,
-                                                 uint64_t n_tiles, const uint32_t* __restrict__ recs,
-                                                 const uint32_t* __restrict__ runs, uint8_t* __restrict__ passbits,
-                                                 uint32_t tile_cap) {
-  constexpr int kUnroll = RPT_SLICE_UNROLL;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr uint32_t kWaves = kSliceThreads / 64;
-  const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
-  const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
-  // a wave walks batches of bt <= 64 consecutive tiles (one run per lane); few tiles per slice (the
-  // bucketed strategy) are spread over all waves in smaller batches
-  const uint32_t bt = batch_tiles(t_hi - t_lo);
-  const uint32_t my = lane < bt ? lane : ~0u >> 1;  // lanes >= bt hold no run
-  uint32_t info_next = (t_lo + wave * bt + my < t_hi) ? my_runs[t_lo + wave * bt + my] : 0u;
-  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
-    const uint32_t info = info_next;  // the next batch's runs are fetched while this one is probed
-    info_next = (tb + kWaves * bt + my < t_hi) ? my_runs[tb + kWaves * bt + my] : 0u;
-    const uint32_t cnt = pad_run(info & 0xFFFFu);  // padded run length (multiple of kRunPad)
-    const uint32_t start = lane * tile_cap + (info >> 16);
-    const uint32_t* brecs = recs + tb * tile_cap;  // uniform
-    uint8_t* bpass = passbits + tb * (tile_cap / kRunPad);
-    const uint32_t incl = wave_inclusive_sum(cnt);
-    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-    uint32_t j = 0;  // uniform: first tile of the batch whose inclusive prefix exceeds the step start
-    constexpr uint32_t kStep = 64 * kRunPad;  // records per wave step
-    for (uint32_t k0 = 0; k0 < total; k0 += kStep * kUnroll) {
-      uint32_t off[kUnroll];
-      u32x4 rec[kUnroll][2];
-#pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        const uint32_t kf = k0 + u * kStep;
-        const uint32_t k = kf + lane * kRunPad;
-        off[u] = ~0u;
-        if (kf < total) {
-          while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
-          const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
-          for (uint32_t jj = j;; jj++) {
-            const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
-            const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
-            const uint32_t b = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(start), jj));
-            if (k >= inc - c && k < inc) off[u] = b + (k - (inc - c));
-            if (inc > kl) break;
-          }
-        }
-        rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
-        if (off[u] != ~0u) {
-          rec[u][0] = *reinterpret_cast<const u32x4*>(brecs + off[u]);
-          rec[u][1] = *reinterpret_cast<const u32x4*>(brecs + off[u] + 4);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kUnroll; u++) {
-        uint32_t bits = 0;
-#pragma unroll
-        for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
-#ifdef RPT_EXP_NO_PASS_WRITE  // experiment: pass-bit stores suppressed (the test still runs)
-        if (off[u] != ~0u && bits == tile_cap) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
-#else
-        if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
-#endif
-      }
-    }
-  }
-}
-
 // Inclusive wave-wide max scan of non-negative values (DPP: rows of 16, then row broadcasts 15 / 31).
 __device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
   v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false)));
@@ -362,6 +297,17 @@ __device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
   v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false)));
   v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false)));
   v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false)));
+  return v;
+}
+
+// Inclusive wave-wide prefix sum (DPP, as wave_inclusive_max; wave_inclusive_sum goes through ds_bpermute).
+__device__ __forceinline__ uint32_t wave_inclusive_sum_dpp(uint32_t v) {
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
   return v;
 }
 
@@ -398,6 +344,7 @@ __device__ __forceinline__ void probe_slice_runs_tbl(const uint64_t* s_slice, co
     const uint32_t excl = incl - nslot;
     const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
     const int base_m_excl = static_cast<int>(base - excl);  // slot s of this run -> base + (s - excl)
+    const int real_p_excl = static_cast<int>((info & 0xFFFFu) + excl * kRunPad);  // real records left: this - 8 s
     for (uint32_t w0 = 0; w0 < total; w0 += kWin) {
 #pragma unroll
       for (int u = 0; u < kUnroll; u++) win[u * 64 + lane] = 0u;
@@ -406,7 +353,7 @@ __device__ __forceinline__ void probe_slice_runs_tbl(const uint64_t* s_slice, co
       if (nslot != 0 && excl < w0 + kWin && incl > w0) win[(excl > w0 ? excl : w0) - w0] = lane + 1;
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       __builtin_amdgcn_wave_barrier();
-      uint32_t off[kUnroll];
+      uint32_t off[kUnroll], keep[kUnroll];
       u32x4 rec[kUnroll][2];
       uint32_t carry = 0;
 #pragma unroll
@@ -417,6 +364,9 @@ __device__ __forceinline__ void probe_slice_runs_tbl(const uint64_t* s_slice, co
         carry = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(m), 63));
         const int src = static_cast<int>(m - 1) << 2;  // lane of the run holding this slot (byte address)
         const uint32_t rel = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, base_m_excl)) + slot;
+        // pad slots get pass bit 0, so a tile's pass-bit popcount is its survivor count
+        const int left = __builtin_amdgcn_ds_bpermute(src, real_p_excl) - static_cast<int>(slot * kRunPad);
+        keep[u] = left >= 8 ? 0xFFu : (left > 0 ? (1u << left) - 1u : 0u);
         off[u] = slot < total ? rel * kRunPad : ~0u;
         rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
         if (w0 + u * 64 < total && off[u] != ~0u) {  // (first test uniform: the window's tail steps)
@@ -432,7 +382,7 @@ __device__ __forceinline__ void probe_slice_runs_tbl(const uint64_t* s_slice, co
         uint32_t bits = 0;
 #pragma unroll
         for (int e = 0; e < 8; e++) bits |= static_cast<uint32_t>(probe_rec(s_slice, s_rmasks, rec[u][e >> 2][e & 3])) << e;
-        if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits);
+        if (off[u] != ~0u) bpass[off[u] / kRunPad] = static_cast<uint8_t>(bits & keep[u]);
       }
     }
   }
@@ -464,9 +414,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   uint64_t* const s_rmasks = s_lds;
   uint64_t* const s_slice = s_lds + kRotMasks;
   u64x2* const s_slice2 = reinterpret_cast<u64x2*>(s_slice);
-#if RPT_SLICE_SLOT_TABLE
   __shared__ uint32_t s_win[kSliceThreads * RPT_SLICE_UNROLL];  // per-wave slot windows (16 KiB)
-#endif
   constexpr uint32_t kPre = kSliceWords / 2 / kSliceThreads;  // 16-B pieces of a slice per thread
   SliceWork cur;
   uint32_t item = next_item(blockIdx.x, n_items, splits, n_tiles, bucket_tiles, cur);
@@ -487,11 +435,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 #pragma unroll
       for (uint32_t i = 0; i < kPre; i++) pre[i] = src[threadIdx.x + i * kSliceThreads];
     }
-#if RPT_SLICE_SLOT_TABLE
     probe_slice_runs_tbl(s_slice, s_rmasks, s_win, cur, n_tiles, recs, runs, passbits, tile_cap);
-#else
-    probe_slice_runs(s_slice, s_rmasks, cur, n_tiles, recs, runs, passbits, tile_cap);
-#endif
     if (nitem >= n_items) break;
     __syncthreads();  // every wave is done with this slice
     for (uint32_t i = 0; i < kPre; i++) s_slice2[threadIdx.x + i * kSliceThreads] = pre[i];  // unrolled by the compiler
@@ -514,9 +458,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
   uint64_t* const s_rmasks = s_lds;
   uint64_t* const s_slice = s_lds + kRotMasks;
-#if RPT_SLICE_SLOT_TABLE
   __shared__ uint32_t s_win[kSliceThreads * RPT_SLICE_UNROLL];  // per-wave slot windows (16 KiB)
-#endif
   const SliceWork sw = slice_work(xcd_item(blockIdx.x, gridDim.x), splits, n_tiles, bucket_tiles);
   const uint32_t slice = sw.slice;
   const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
@@ -528,7 +470,6 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   constexpr uint32_t kWaves = kSliceThreads / 64;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
   const uint32_t bt = batch_tiles(t_hi - t_lo);  // as slice_probe_kernel
-#if RPT_SLICE_SLOT_TABLE
   // slot -> run through the wave's LDS window, as probe_slice_runs_tbl
   constexpr uint32_t kWin = 64 * RPT_SLICE_UNROLL;
   uint32_t* win = s_win + wave * kWin;
@@ -586,52 +527,6 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
       }
     }
   }
-#else
-  for (uint64_t tb = t_lo + wave * bt; tb < t_hi; tb += kWaves * bt) {
-    const uint32_t info = (lane < bt && tb + lane < t_hi) ? my_runs[tb + lane] : 0u;
-    const uint32_t real = info & 0xFFFFu;      // records of the run
-    const uint32_t cnt = pad_run(real);          // padded length (k-space)
-    const uint64_t base = (tb + lane) * tile_cap + (info >> 16);
-    const uint32_t base_lo = static_cast<uint32_t>(base), base_hi = static_cast<uint32_t>(base >> 32);
-    const uint32_t incl = wave_inclusive_sum(cnt);
-    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-    uint32_t j = 0;
-    constexpr uint32_t kStep = 64 * kRunPad;
-    for (uint32_t kf = 0; kf < total; kf += kStep) {
-      const uint32_t k = kf + lane * kRunPad;
-      while (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), j)) <= kf) j++;
-      const uint32_t kl = (kf + kStep - 1 < total) ? kf + kStep - 1 : total - 1;
-      uint64_t addr = ~0ULL;
-      uint32_t nreal = 0;  // how many of this lane's kRunPad slots are real records (pad slots are stale)
-      for (uint32_t jj = j;; jj++) {
-        const uint32_t inc = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), jj));
-        const uint32_t c = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cnt), jj));
-        const uint32_t rl = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(real), jj));
-        const uint64_t b =
-            static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_lo), jj))) |
-            (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(base_hi), jj))) << 32);
-        if (k >= inc - c && k < inc) {
-          const uint32_t off = k - (inc - c);
-          addr = b + off;
-          nreal = rl > off ? (rl - off < kRunPad ? rl - off : kRunPad) : 0;
-        }
-        if (inc > kl) break;
-      }
-      if (addr != ~0ULL) {
-        const u32x4 r0 = *reinterpret_cast<const u32x4*>(recs + addr);
-        const u32x4 r1 = *reinterpret_cast<const u32x4*>(recs + addr + 4);
-#pragma unroll
-        for (uint32_t e = 0; e < kRunPad; e++) {
-          if (e < nreal) {
-            const uint32_t rec = e < 4 ? r0[e] : r1[e - 4];
-            atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[rec_word(rec)]),
-                     static_cast<unsigned long long>(rec_mask(s_rmasks, rec)));
-          }
-        }
-      }
-    }
-  }
-#endif
   __syncthreads();
   uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
   for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
@@ -687,6 +582,125 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint
     if (seg_counts != nullptr) {
       const uint32_t cnt = wave_sum(__popc(byte));
       if (lane == 0) seg_counts[seg] = cnt;
+    }
+  }
+}
+}  // namespace rpt
+
+namespace rpt {
+// ---- partitioned probe, C': restore row order straight into the selection vector -----------------
+// LookupSel's fused tail (rpt_bf_probe, PARTITIONED strategy): a tile's survivor count is the
+// popcount of its pass bits (the slice probe writes 0 for pad slots), so the tiles' output offsets are
+// known before the unpermute. The unpermute then writes ascending row ids directly. This replaces
+// the result bit vector, its per-segment counts, and the separate compaction pass.
+
+// C'1: survivors per tile: popcount of the tile's used pass-bit bytes (its padded runs), one wave per tile.
+constexpr int kTileCountThreads = 256;
+__global__ __launch_bounds__(kTileCountThreads) void tile_count_kernel(const uint8_t* __restrict__ passbits,
+                                                                      const uint32_t* __restrict__ runs_tm,
+                                                                      uint32_t n_slices, uint64_t n_tiles,
+                                                                      uint64_t tile_cap,
+                                                                      uint32_t* __restrict__ tile_counts) {
+  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * (kTileCountThreads / 64) + (threadIdx.x >> 6);
+  if (tile >= n_tiles) return;  // wave-uniform
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t last = runs_tm[tile * n_slices + n_slices - 1];  // the last slice's run ends the used records
+  const uint32_t used = ((last >> 16) + pad_run(last & 0xFFFFu)) / kRunPad;  // bytes of pass bits
+  const u32x4* blk = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / kRunPad));
+  uint32_t c = 0;
+  for (uint32_t i = lane; i * 16 < used; i += 64) {
+    const u32x4 v = blk[i];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+      const uint32_t b0 = i * 16 + e * 4;  // first byte of this word
+      uint32_t w = v[e];
+      if (b0 + 4 > used) w = b0 >= used ? 0u : w & ((1u << (8 * (used - b0))) - 1u);
+      c += __popc(w);
+    }
+  }
+  c = wave_sum(c);
+  if (lane == 0) tile_counts[tile] = c;
+}
+
+// C'1b: blocks of 256 tiles: each tile's exclusive prefix inside its block (in place) + the block sums
+// (group_scan_kernel then scans the few block sums).
+constexpr int kTileBlock = 256;
+__global__ __launch_bounds__(kTileBlock) void tile_block_scan_kernel(uint32_t* __restrict__ tile_counts, uint64_t n_tiles,
+                                                                    uint32_t* __restrict__ block_sums) {
+  __shared__ uint32_t s_w[kTileBlock / 64];
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * kTileBlock + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t c = t < n_tiles ? tile_counts[t] : 0u;
+  const uint32_t inc = wave_inclusive_sum_dpp(c);
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  uint32_t off = 0, all = 0;
+  for (uint32_t w = 0; w < kTileBlock / 64; w++) {
+    off += w < wave ? s_w[w] : 0u;
+    all += s_w[w];
+  }
+  if (t < n_tiles) tile_counts[t] = off + inc - c;
+  if (threadIdx.x == 0) block_sums[blockIdx.x] = all;
+}
+
+// C'2 (tile_pre = prefix inside the tile's block, block_offs = the blocks' scan): one 256-thread workgroup per
+// tile, as unpermute_kernel; each wave's segments are consecutive rows, so a survivor's sel index is
+// tile offset + earlier waves' survivors + earlier segments of this wave + earlier lanes of its segment.
+template <int TM>
+__global__ __launch_bounds__(kUnpermuteThreads) void unpermute_sel_kernel(const uint16_t* __restrict__ pos,
+                                                                         const uint8_t* __restrict__ passbits,
+                                                                         uint64_t n, uint64_t tile_cap,
+                                                                         const uint32_t* __restrict__ tile_pre,
+                                                                         const uint32_t* __restrict__ block_offs,
+                                                                         const uint32_t* __restrict__ row_sel,
+                                                                         uint32_t* __restrict__ out_sel) {
+  extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
+  __shared__ uint32_t s_wtot[kUnpermuteThreads / 64];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
+  constexpr uint32_t kSegsPerWave = (kTileRows * TM / kSegRows) / (kUnpermuteThreads / 64);
+  const uint64_t tile = blockIdx.x;
+  const uint64_t seg0 = tile * (kTileRows * TM / kSegRows) + wave * kSegsPerWave;
+  u32x4 pv[kSegsPerWave];  // 8 row positions (u16) per lane per segment
+#pragma unroll
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    pv[sg] = u32x4{0, 0, 0, 0};
+    if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos + (seg0 + sg) * kSegRows + lane * 8);
+  }
+  {
+    const u32x4* src = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / 8));
+    for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
+  }
+  __syncthreads();
+  uint32_t bytes[kSegsPerWave], excl[kSegsPerWave], run = 0;
+#pragma unroll
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    uint32_t byte = 0;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+      byte |= ((static_cast<uint32_t>(s_pass[p >> 3]) >> (p & 7)) & 1u) << e;
+    }
+    const uint64_t row0 = (seg0 + sg) * kSegRows + lane * 8;  // rows >= n carry don't-care positions
+    if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
+    bytes[sg] = byte;
+    const uint32_t c = __popc(byte);
+    const uint32_t inc = wave_inclusive_sum_dpp(c);
+    excl[sg] = run + inc - c;
+    run += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
+  }
+  if (lane == 0) s_wtot[wave] = run;
+  __syncthreads();
+  uint32_t woff = block_offs[tile / kTileBlock] + tile_pre[tile];
+  for (uint32_t w = 0; w < wave; w++) woff += s_wtot[w];
+#pragma unroll
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    uint32_t b = bytes[sg], o = woff + excl[sg];
+    const uint32_t row0 = static_cast<uint32_t>((seg0 + sg) * kSegRows) + lane * 8;
+    while (b) {
+      const uint32_t row = row0 + static_cast<uint32_t>(__builtin_ctz(b));
+      out_sel[o++] = row_sel ? row_sel[row] : row;
+      b &= b - 1;
     }
   }
 }

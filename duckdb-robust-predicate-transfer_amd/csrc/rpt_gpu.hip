@@ -954,8 +954,15 @@ int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, ui
   return RPT_OK;
 }
 
-int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
-                        void* workspace, size_t workspace_bytes, rpt_stream_t stream) {
+#ifndef RPT_FUSED_SEL
+#define RPT_FUSED_SEL 1  // rpt_bf_probe, PARTITIONED: the unpermute writes the selection vector itself
+#endif
+
+// Phase 1 of rpt_bf_probe. With out_sel (rpt_bf_probe only) the plain PARTITIONED pipeline ends in the
+// fused selection-vector tail instead of the result bits, and *done is set: phase 2 is skipped.
+static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
+                             void* workspace, size_t workspace_bytes, rpt_stream_t stream, uint32_t* out_sel,
+                             uint64_t* out_count_dev, bool* done) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
   if (n >= (1ULL << 32)) return fail(RPT_ERR_INVALID_ARGUMENT, "n=%llu rows exceeds uint32 sel_t", (unsigned long long)n);
   if (n == 0) return RPT_OK;
@@ -1047,8 +1054,39 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
                        static_cast<uint32_t>(rpt::tile_cap_for(tile_slices, tm)), bucket_tiles, n_items);
     prof6_.end();
     RPT_LAUNCHED("slice_probe_kernel");
-    ProfScope prof7_("unpermute_kernel", s);
     const uint64_t cap = rpt::tile_cap_for(tile_slices, tm);
+    if (RPT_FUSED_SEL && !buck && out_sel != nullptr && out_count_dev != nullptr) {
+      // tile survivor counts (in seg_counts; then their prefix inside blocks of 256 tiles) -> block sums and
+      // block offsets (in the unused result-bit area) -> sel
+      uint32_t* tile_counts = ws.seg_counts;
+      const uint64_t n_blocks = ceil_div(n_tiles, rpt::kTileBlock);
+      uint32_t* block_sums = reinterpret_cast<uint32_t*>(ws.bits);
+      uint32_t* block_offs = block_sums + n_blocks;
+      ProfScope prof7a_("tile_count_kernel", s);
+      hipLaunchKernelGGL(rpt::tile_count_kernel, dim3(static_cast<unsigned>(ceil_div(n_tiles, rpt::kTileCountThreads / 64))),
+                         dim3(rpt::kTileCountThreads), 0, s, ws.passb, ws.runs_tm, tile_slices, n_tiles, cap, tile_counts);
+      prof7a_.end();
+      RPT_LAUNCHED("tile_count_kernel");
+      ProfScope prof7b_("group_scan_kernel", s);
+      hipLaunchKernelGGL(rpt::tile_block_scan_kernel, dim3(static_cast<unsigned>(n_blocks)), dim3(rpt::kTileBlock), 0, s,
+                         tile_counts, n_tiles, block_sums);
+      hipLaunchKernelGGL(rpt::group_scan_kernel, dim3(1), dim3(1024), 0, s, block_sums, static_cast<uint32_t>(n_blocks),
+                         block_offs, out_count_dev);
+      prof7b_.end();
+      RPT_LAUNCHED("group_scan_kernel");
+      ProfScope prof7c_("unpermute_sel_kernel", s);
+      if (tm == 2)
+        hipLaunchKernelGGL(rpt::unpermute_sel_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads),
+                           cap / 8, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
+      else
+        hipLaunchKernelGGL(rpt::unpermute_sel_kernel<1>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads),
+                           cap / 8, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
+      prof7c_.end();
+      RPT_LAUNCHED("unpermute_sel_kernel");
+      *done = true;
+      return RPT_OK;
+    }
+    ProfScope prof7_("unpermute_kernel", s);
     if (tm == 2)
       hipLaunchKernelGGL(rpt::unpermute_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8,
                          s, ws.pos, ws.passb, n_part, cap, part_bits, part_counts, dev_n_tiles);
@@ -1067,6 +1105,12 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
     }
   }
   return RPT_OK;
+}
+
+int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
+                        void* workspace, size_t workspace_bytes, rpt_stream_t stream) {
+  bool done = false;
+  return probe_phase1_impl(bf, col, row_sel, n, workspace, workspace_bytes, stream, nullptr, nullptr, &done);
 }
 
 int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, uint32_t* out_sel,
@@ -1131,8 +1175,9 @@ int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* ro
     RPT_LAUNCHED("probe_small_kernel");
     return RPT_OK;
   }
-  int st = rpt_bf_probe_phase1(bf, col, row_sel, n, workspace, workspace_bytes, stream);
-  if (st != RPT_OK) return st;
+  bool done = false;
+  int st = probe_phase1_impl(bf, col, row_sel, n, workspace, workspace_bytes, stream, out_sel, out_count_dev, &done);
+  if (st != RPT_OK || done) return st;
   return rpt_bf_probe_phase2(bf, row_sel, n, out_sel, out_count_dev, workspace, workspace_bytes, stream);
 }
 
