@@ -456,3 +456,34 @@ def test_double_tile_edges_vs_oracle(rpt, n):
     bf.probe_strategy = STRATEGIES["partitioned"]
     sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
     assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
+
+
+@pytest.mark.parametrize("log_nb", [17, 21, 24])
+@pytest.mark.parametrize("use_row_sel", [False, True])
+def test_fused_sel_tail_equals_two_phase_path(rpt, log_nb, use_row_sel):
+    """rpt_bf_probe's partitioned pipeline ends in the fused tail (tile counts -> offsets -> the unpermute
+    writes the sel); rpt_bf_probe_phase1 + phase2 keep the result-bit path. Both must give the oracle's
+    sel and count, with and without a row selection, for 16 Ki- (2^17, 2^21) and 32 Ki-row (2^24) tiles."""
+    build = orc.synth_build_keys(200000)
+    n = 3 * 32768 + 777
+    probe = orc.synth_probe_keys(n, 200000, 250)
+    bf = with_strategy(rpt.BloomFilter(log_num_blocks=log_nb), "partitioned")
+    bf.insert(dev(build))
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, build)
+    rng = np.random.default_rng(log_nb)
+    row_sel = np.sort(rng.choice(n, size=n // 3, replace=False)).astype(np.uint32) if use_row_sel else None
+    ref = orc.probe_keys(w, log_nb, probe)
+    exp = ref if row_sel is None else np.intersect1d(row_sel, ref).astype(np.uint32)
+    rs = dev(row_sel) if row_sel is not None else None
+    m = row_sel.size if row_sel is not None else n
+    keys = dev(probe)
+    fused = bf.lookup_sel(keys, row_sel=rs).cpu().numpy().view(np.uint32)
+    ws = torch.empty(bf.workspace_bytes(m), dtype=torch.uint8, device="cuda:0")
+    out = torch.full((m,), -1, dtype=torch.int32, device="cuda:0")
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    bf.probe_phase1(keys, ws, n=m, row_sel=rs)
+    bf.probe_phase2(m, out, cnt, ws, row_sel=rs)
+    two = out[: int(cnt.item())].cpu().numpy().view(np.uint32)
+    assert np.array_equal(fused, exp)
+    assert np.array_equal(two, exp)
