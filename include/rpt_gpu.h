@@ -191,7 +191,9 @@ int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* ro
 /* rpt_bf_probe in its two stream-ordered phases (same filter, workspace and stream), for callers that
  * time or overlap them. GATHER / LDS: phase 1 = hash + gather + result bits + per-segment counts,
  * phase 2 = scan + expansion into out_sel. PARTITIONED: phase 1 = partition rows by filter slice +
- * probe each slice from LDS + restore row order into the result bits, phase 2 = as above. */
+ * probe each slice from LDS + restore row order into the result bits, phase 2 = as above.
+ * (rpt_bf_probe itself runs the PARTITIONED strategy without the result bits: per-tile survivor counts
+ * give each tile's offset and the row-order restore writes out_sel directly. Same sel and count.) */
 int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
                         void* workspace, size_t workspace_bytes, rpt_stream_t stream);
 int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, uint32_t* out_sel,
