@@ -211,7 +211,14 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kBucketUnpermuteThreads / 64;
   const uint32_t nb = bucket_mask + 1;
+#if RPT_BUCKET_UNPERMUTE_XCD_MAP
+  // XCD-contiguous tiles, as the scatter: neighbouring tiles' runs are adjacent in every bucket's array,
+  // so the 64-bit pass-bit pieces one tile gathers share lines with its neighbours' in the same L2
+  const uint32_t per_xcd = gridDim.x / 8, xcd = blockIdx.x % 8;
+  const uint64_t tile = blockIdx.x < per_xcd * 8 ? static_cast<uint64_t>(xcd) * per_xcd + blockIdx.x / 8 : blockIdx.x;
+#else
   const uint64_t tile = blockIdx.x;
+#endif
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
   constexpr uint32_t kSegsPerWave = (kL1TileRows / kSegRows) / kWaves;
   const uint64_t seg0 = tile * (kL1TileRows / kSegRows) + wave * kSegsPerWave;
