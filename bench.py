@@ -46,12 +46,14 @@ def parse():
                     help="probe rows in the CPU-baseline sample (default: the whole per-GPU probe workload)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--key-type", default="i64", choices=["i64", "i32"],
+                    help="key column type (i32: the synthetic keys truncated to int32, as JOB's INTEGER keys)")
     ap.add_argument("--strategy", default="auto", choices=["auto", "gather", "lds", "partitioned", "bucketed"],
                     help="probe strategy (auto picks by filter size)")
     return ap.parse_args()
 
 
-def algorithmic_bytes(kernel: str, n: int, survivors: int) -> int:
+def algorithmic_bytes(kernel: str, n: int, survivors: int, key_bytes: int = KEY_BYTES) -> int:
     """SURVEY §8(d) per-unit bytes for the kernel's part of the probe: every kernel that streams the
     key column is charged 8 B/key (the key read; its own intermediates are implementation traffic,
     counted in `traffic`); the kernels that write the selection vector (the compaction, or the fused
@@ -61,10 +63,10 @@ def algorithmic_bytes(kernel: str, n: int, survivors: int) -> int:
     if kernel.startswith(("slice_probe", "unpermute", "group_", "bucket_unpermute", "bucket_scan", "runs_transpose",
                           "tile_count")):
         return 0
-    return KEY_BYTES * n
+    return key_bytes * n
 
 
-def pmc_traffic(kernel: str):
+def pmc_traffic(kernel: str, key_k: int = 0):
     """HBM bytes per launch of `kernel` from the PMC summary tools/pmc_summary.py wrote for this build
     (FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE, separate rocprofv3 --pmc passes)."""
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
@@ -74,16 +76,21 @@ def pmc_traffic(kernel: str):
     except (OSError, ValueError):
         return None
     # the kernel's instantiations (name or name<template args>); the probe's is the longest-running
+    # (key-typed instantiations: the first template argument is the key type, 0 = int64, 1 = int32)
     cands = [v for name, v in d.get("kernels", {}).items()
-             if (name == kernel or name.startswith(kernel + "<")) and "hbm_bytes_per_launch" in v]
+             if (name == kernel or name.startswith(kernel + "<")) and "hbm_bytes_per_launch" in v
+             and not (name.startswith(kernel + "<") and name[len(kernel) + 1:].split(",")[0] in ("0", "1")
+                      and name[len(kernel) + 1:].split(",")[0] != str(key_k))]
     if not cands:
         return None
     k = max(cands, key=lambda v: v.get("avg_ms", 0.0))
     return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": f"profiles/pmc_latest.json ({d.get('round')})"}
 
 
-def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int) -> dict:
-    """The C++ restatement of the reference CPU path, morsel-parallel in 2048-row vectors."""
+def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int, key_type: str = "i64") -> dict:
+    """The C++ restatement of the reference CPU path, morsel-parallel in 2048-row vectors. int32 keys run
+    zero-extended to int64: DuckDB hashes an INTEGER through uint32 -> uint64, so hashes and survivors
+    are the same (the port then reads 8 B per key instead of 4)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import rpt_oracle as orc
@@ -91,10 +98,11 @@ def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int) -> di
     threads = max(1, min(threads, len(os.sched_getaffinity(0))))
     lnb = orc.log_num_blocks(n_build)
     words = orc.new_words(lnb)
-    build_keys = orc.synth_build_keys(n_build)
+    as_i32 = (lambda k: k.astype(np.int32).view(np.uint32).astype(np.int64)) if key_type == "i32" else (lambda k: k)
+    build_keys = as_i32(orc.synth_build_keys(n_build))
     build_s = orc.build_mt(words, lnb, build_keys, threads)
     del build_keys
-    keys = orc.synth_probe_keys(sample, n_build, p_permille)
+    keys = as_i32(orc.synth_probe_keys(sample, n_build, p_permille))
     orc.probe_mt(words, lnb, keys, threads)  # warm-up
     runs = [orc.probe_mt(words, lnb, keys, threads) for _ in range(5)]
     med = statistics.median(r[0] for r in runs)
@@ -106,6 +114,7 @@ def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int) -> di
         "sample": (f"probe of the first {sample:.0e} rows (the GPU's whole per-step workload when equal to its "
                    f"probe rows) of the same synthetic probe stream against the same "
                    f"{n_build:.0e}-key filter (2^{lnb} blocks), {threads} std::threads, 2048-row vectors, "
+                   f"{'int32 keys zero-extended (same hashes), ' if key_type == 'i32' else ''}"
                    f"hash included; median of 5 after 1 warm-up; build of the filter {n_build / build_s:.3e} keys/s"),
         "cpu_model": _cpu_model(),
         "survivors": runs[0][1],
@@ -161,6 +170,8 @@ def main():
     # ---- CREATE_BF: sharded build + OR merge (reported, not the headline) -------------------------
     lo, hi = shard_range(n_build, rank, world)
     build_keys = rpt_amd.synth_build_keys(hi - lo, start=lo, device=device)
+    if args.key_type == "i32":
+        build_keys = build_keys.to(torch.int32)
     bf = rpt_amd.BloomFilter(n_filter, device=device)
     bf.insert(build_keys)  # warm-up: workspace allocation, code-object load
     build_reps = 5
@@ -180,7 +191,8 @@ def main():
     if world > 1:
         # untimed: the OR-merged filter must be bit-identical to a single-GPU build of all rows
         ref = rpt_amd.BloomFilter(n_filter, device=device)
-        ref.insert(rpt_amd.synth_build_keys(n_build, device=device))
+        all_keys = rpt_amd.synth_build_keys(n_build, device=device)
+        ref.insert(all_keys.to(torch.int32) if args.key_type == "i32" else all_keys)
         a = torch.empty(bf.num_blocks, dtype=torch.int64, device=device)
         b = torch.empty_like(a)
         bf.copy_words_to(a)
@@ -198,6 +210,11 @@ def main():
 
     # ---- USE_BF probe workload: this rank's slice of the global probe column --------------------
     keys = rpt_amd.synth_probe_keys(n_probe, n_build, p_permille, start=rank * n_probe, device=device)
+    key_bytes = KEY_BYTES
+    if args.key_type == "i32":
+        keys = keys.to(torch.int32)
+        key_bytes = 4
+        torch.cuda.empty_cache()
     out_sel = torch.empty(n_probe, dtype=torch.int32, device=device)
     out_count = torch.zeros(1, dtype=torch.int64, device=device)
     ws = torch.empty(bf.workspace_bytes(n_probe), dtype=torch.uint8, device=device)
@@ -241,17 +258,18 @@ def main():
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = world * n_probe * args.steps / elapsed
-        probe_bytes = KEY_BYTES * n_probe + SEL_BYTES * survivors
+        probe_bytes = key_bytes * n_probe + SEL_BYTES * survivors
         # dominant kernel of the step (largest total device time)
         dom_name, (dom_calls, dom_total) = max(ktimes.items(), key=lambda kv: kv[1][1])
         dom_ms = dom_total / dom_calls
-        dom_bytes = algorithmic_bytes(dom_name, n_probe, survivors)
+        dom_bytes = algorithmic_bytes(dom_name, n_probe, survivors, key_bytes)
         achieved = dom_bytes / (dom_ms * 1e-3)
-        traffic = pmc_traffic(dom_name)
+        key_k = 1 if args.key_type == "i32" else 0
+        traffic = pmc_traffic(dom_name, key_k)
         # whole-step HBM traffic: every kernel of the step at its PMC bytes per launch
         step_traffic, unprofiled = 0.0, []
         for name, (calls, _total) in ktimes.items():
-            t = pmc_traffic(name)
+            t = pmc_traffic(name, key_k)
             if t is None:
                 unprofiled.append(name)
             else:
@@ -267,10 +285,10 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int64",
+            "dtype": "int32" if args.key_type == "i32" else "int64",
             "data": "synthetic: seeded splitmix64 int64 key columns generated on device (SURVEY §8d)",
             "config": {
-                "workload": (f"{cfg}: USE_BF probe of {n_probe:.0e} int64 keys per GPU against a blocked Bloom "
+                "workload": (f"{cfg}: USE_BF probe of {n_probe:.0e} {'int32' if args.key_type == 'i32' else 'int64'} keys per GPU against a blocked Bloom "
                              f"filter built from {n_build:.0e} keys (sized for {n_filter:.0e}: "
                              f"2^{bf.log_num_blocks} blocks = {bf.num_blocks * 8 / 2**20:.0f} MiB), p={args.p}"),
                 "probe_rows_per_gpu": n_probe,
@@ -315,7 +333,7 @@ def main():
         }
         if not args.no_cpu_baseline and world == 1:
             sample = int(args.cpu_sample) if args.cpu_sample else n_probe
-            cb = cpu_baseline(n_build, p_permille, sample, args.cpu_threads)
+            cb = cpu_baseline(n_build, p_permille, sample, args.cpu_threads, args.key_type)
             if sample == n_probe:  # same rows, same filter: a full-size cross-check of the survivor count
                 cb["survivors_match_gpu"] = cb["survivors"] == survivors
             line["cpu_baseline"] = cb
