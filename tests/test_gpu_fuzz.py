@@ -1,6 +1,8 @@
 """Seeded randomized parity sweep: random filter sizes, batch sizes, key types, NULL patterns,
 dictionary vectors and row selections; every applicable probe strategy and insert strategy must give
 the oracle's filter words and survivors. Bit-exact."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -53,7 +55,7 @@ def case(seed):
                 use_dict=use_dict, use_rowsel=use_rowsel, rng=rng)
 
 
-@pytest.mark.parametrize("seed", range(24))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("RPT_FUZZ_SEEDS", "24"))))
 def test_random_configuration(rpt, seed):
     c = case(seed)
     lnb, rng = c["log_nb"], c["rng"]
