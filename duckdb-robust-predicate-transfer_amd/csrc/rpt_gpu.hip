@@ -15,6 +15,7 @@
 //   insert  : atomic OR per key (misc.hpp), or the partitioned / bucketed routing with the slices
 //             ORed in LDS; the build's key min/max is folded in on the way.
 //   merge   : OR of partial filters / peer slices;  fold;  popcount (misc.hpp).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -25,6 +26,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "rpt_bloom_device.hpp"
@@ -660,6 +662,7 @@ const char* rpt_status_string(int status) {
     case RPT_ERR_OUT_OF_MEMORY: return "out of device memory";
     case RPT_ERR_WORKSPACE: return "workspace too small";
     case RPT_ERR_SHAPE_MISMATCH: return "filter shape mismatch";
+    case RPT_ERR_COLLECTIVE: return "collective (RCCL) failed";
     default: return "unknown status";
   }
 }
@@ -1227,6 +1230,137 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
   if (src->has_data.load()) dst->has_data.store(1);
   return RPT_OK;
 }
+
+// ---- multi-GPU Combine over RCCL ------------------------------------------------------------------
+}  // extern "C"
+namespace {
+// The RCCL entry points rpt_bf_allreduce_or uses, resolved from librccl on first use (rccl.h types:
+// ncclResult_t = int, ncclComm_t = opaque pointer, ncclDataType_t / ncclRedOp_t = int enums).
+struct RcclApi {
+  int (*group_start)() = nullptr;
+  int (*group_end)() = nullptr;
+  int (*send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*recv)(void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
+  int (*comm_count)(void*, int*) = nullptr;
+  int (*comm_user_rank)(void*, int*) = nullptr;
+  const char* (*error_string)(int) = nullptr;
+  std::string load_error;
+};
+constexpr int kNcclInt64 = 4, kNcclUint64 = 5, kNcclMin = 3;  // rccl.h ncclDataType_t / ncclRedOp_t
+const RcclApi& rccl_api() {
+  static const RcclApi api = [] {
+    RcclApi a;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      a.load_error = e ? e : "dlopen(librccl) failed";
+      return a;
+    }
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      if (!fn && a.load_error.empty()) a.load_error = std::string("librccl lacks ") + name;
+    };
+    sym(a.group_start, "ncclGroupStart");
+    sym(a.group_end, "ncclGroupEnd");
+    sym(a.send, "ncclSend");
+    sym(a.recv, "ncclRecv");
+    sym(a.all_reduce, "ncclAllReduce");
+    sym(a.comm_count, "ncclCommCount");
+    sym(a.comm_user_rank, "ncclCommUserRank");
+    sym(a.error_string, "ncclGetErrorString");
+    return a;
+  }();
+  return api;
+}
+// {min, max, has_data} -> {min, ~max, ~has}: bit complement reverses the order without overflow, so one
+// MIN all-reduce gives the global min, max and has_data (an empty partial holds {INT64_MAX, INT64_MIN}).
+__global__ void minmax_pack_kernel(const int64_t* stats, int has, int64_t* v) {
+  v[0] = stats[0];
+  v[1] = ~stats[1];
+  v[2] = ~static_cast<int64_t>(has != 0);
+}
+__global__ void minmax_unpack_kernel(const int64_t* v, int64_t* stats, int* has) {
+  stats[0] = v[0];
+  stats[1] = ~v[1];
+  *has = static_cast<int>(~v[2]);
+}
+}  // namespace
+extern "C" {
+
+#define RPT_NCCL(call)                                                                          \
+  do {                                                                                         \
+    const int rc_ = (call);                                                                    \
+    if (rc_ != 0) return fail(RPT_ERR_COLLECTIVE, "%s: %s", #call, api.error_string(rc_));      \
+  } while (0)
+
+int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
+  if (!bf || !nccl_comm) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  const RcclApi& api = rccl_api();
+  if (!api.load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api.load_error.c_str());
+  RPT_ON_DEVICE(bf->device);
+  hipStream_t s = as_stream(stream);
+  int world = 1, me = 0;
+  RPT_NCCL(api.comm_count(nccl_comm, &world));
+  RPT_NCCL(api.comm_user_rank(nccl_comm, &me));
+  const uint64_t nw = 1ULL << bf->log_num_blocks;
+  auto lo = [&](int j) { return nw * static_cast<uint64_t>(j) / static_cast<uint64_t>(world); };
+  uint64_t* tmp = nullptr;
+  int64_t* v = nullptr;  // {min, ~max, ~has} then has_data (as int) in v[3]
+  const uint64_t mine = lo(me + 1) - lo(me);
+  const size_t tmp_bytes = world > 1 ? (static_cast<size_t>(world) - 1) * mine * 8 : 0;
+  if (hipMalloc(&v, 4 * sizeof(int64_t) + tmp_bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(RPT_ERR_OUT_OF_MEMORY, "allreduce staging of %zu bytes", tmp_bytes);
+  }
+  tmp = reinterpret_cast<uint64_t*>(v + 4);
+  auto run = [&]() -> int {
+    if (world > 1) {
+      // reduce-scatter by OR: rank `me` owns words [lo(me), lo(me + 1)); peers' copies land in tmp
+      RPT_NCCL(api.group_start());
+      for (int p = 0, k = 0; p < world; p++) {
+        if (p == me) continue;
+        RPT_NCCL(api.send(bf->words + lo(p), lo(p + 1) - lo(p), kNcclUint64, p, nccl_comm, s));
+        RPT_NCCL(api.recv(tmp + static_cast<uint64_t>(k++) * mine, mine, kNcclUint64, p, nccl_comm, s));
+      }
+      RPT_NCCL(api.group_end());
+      if (mine > 0) {
+        const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(mine / 2 + 1, rpt::kBlockThreads), 4096)));
+        hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words + lo(me), tmp,
+                           static_cast<uint32_t>(world - 1), mine, 1);
+        RPT_LAUNCHED("or_slices_kernel");
+      }
+      // all-gather: every rank's merged words to every peer
+      RPT_NCCL(api.group_start());
+      for (int p = 0; p < world; p++) {
+        if (p == me) continue;
+        RPT_NCCL(api.send(bf->words + lo(me), mine, kNcclUint64, p, nccl_comm, s));
+        RPT_NCCL(api.recv(bf->words + lo(p), lo(p + 1) - lo(p), kNcclUint64, p, nccl_comm, s));
+      }
+      RPT_NCCL(api.group_end());
+    }
+    hipLaunchKernelGGL(minmax_pack_kernel, dim3(1), dim3(1), 0, s, bf->stats, bf->has_data.load(), v);
+    RPT_LAUNCHED("minmax_pack_kernel");
+    RPT_NCCL(api.all_reduce(v, v, 3, kNcclInt64, kNcclMin, nccl_comm, s));
+    hipLaunchKernelGGL(minmax_unpack_kernel, dim3(1), dim3(1), 0, s, v, bf->stats, reinterpret_cast<int*>(v + 3));
+    RPT_LAUNCHED("minmax_unpack_kernel");
+    int has = 0;
+    RPT_HIP(hipMemcpyAsync(&has, v + 3, sizeof(int), hipMemcpyDeviceToHost, s));
+    RPT_HIP(hipStreamSynchronize(s));
+    bf->has_data.store(has ? 1 : 0);
+    return RPT_OK;
+  };
+  const int st = run();
+  if (st == RPT_OK) {
+    (void)hipFree(v);
+  } else {
+    (void)hipStreamSynchronize(s);  // nothing may still use the staging buffer
+    (void)hipFree(v);
+  }
+  return st;
+}
+#undef RPT_NCCL
 
 int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out) {
   if (!bf || !out) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");

@@ -19,6 +19,7 @@ RPT_ERR_HIP = 2
 RPT_ERR_OUT_OF_MEMORY = 3
 RPT_ERR_WORKSPACE = 4
 RPT_ERR_SHAPE_MISMATCH = 5
+RPT_ERR_COLLECTIVE = 6
 
 RPT_PROBE_AUTO = 0
 RPT_PROBE_GATHER = 1
@@ -116,6 +117,7 @@ SIGNATURES = {
     "rpt_hash_keys": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_hash_combine": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_bf_merge_or": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "rpt_bf_allreduce_or": (c_int, [c_void_p, c_void_p, c_void_p]),
     "rpt_words_or": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_words_or_slices": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p]),
     "rpt_bf_count_bits": (c_int, [c_void_p, POINTER(c_uint64)]),

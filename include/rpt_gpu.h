@@ -39,7 +39,8 @@ typedef enum rpt_status {
   RPT_ERR_HIP = 2,              /* a HIP runtime call failed; rpt_last_error() has the text */
   RPT_ERR_OUT_OF_MEMORY = 3,    /* device allocation failed */
   RPT_ERR_WORKSPACE = 4,        /* caller workspace smaller than rpt_probe_workspace_bytes() */
-  RPT_ERR_SHAPE_MISMATCH = 5    /* merge of filters with different log_num_blocks / devices */
+  RPT_ERR_SHAPE_MISMATCH = 5,   /* merge of filters with different log_num_blocks / devices */
+  RPT_ERR_COLLECTIVE = 6        /* librccl could not be loaded, or an RCCL call failed */
 } rpt_status;
 
 typedef enum rpt_key_type {
@@ -214,6 +215,15 @@ int rpt_hash_combine(const rpt_key_column* col, uint64_t n, uint64_t* inout_hash
 /* dst |= src (same log_num_blocks, same device): merging per-thread or per-GPU partial filters
  * built over disjoint row ranges gives the filter of the union, bit-identical to one build. */
 int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream);
+/* Multi-GPU CREATE_BF Combine: OR all-reduce of every rank's partial filter over an RCCL
+ * communicator (`comm` is an ncclComm_t, one rank per GPU; every rank's filter has the same
+ * log_num_blocks). It is composed as a reduce-scatter by OR (grouped ncclSend/ncclRecv of 1/W of the
+ * words, then an OR kernel) and an all-gather (grouped ncclSend/ncclRecv). RCCL has no bitwise-OR
+ * ncclRedOp_t. The key min/max and has_data are reduced too, in one ncclAllReduce(MIN). Collective:
+ * every rank of the communicator must call it. Stream-ordered on `stream`; returns after has_data is
+ * known (one stream sync). librccl is loaded on first use (dlopen), so the library itself does not
+ * depend on it. */
+int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream);
 /* dst[i] |= src[i] for n_words words (device pointers): the local step of the multi-GPU
  * OR all-reduce (reduce-scatter slices). */
 int rpt_words_or(uint64_t* dst, const uint64_t* src, uint64_t n_words, rpt_stream_t stream);

@@ -43,6 +43,13 @@ def test_abi_version_and_status_strings():
     assert lib.rpt_abi_version() == 1
     assert lib.rpt_status_string(0) == b"ok"
     assert lib.rpt_status_string(4) == b"workspace too small"
+    assert lib.rpt_status_string(6) == b"collective (RCCL) failed"
+
+
+def test_allreduce_or_rejects_null_communicator():
+    lib = _lib.load()
+    # argument checks run before RCCL is loaded or any device is touched
+    assert lib.rpt_bf_allreduce_or(None, None, None) == _lib.RPT_ERR_INVALID_ARGUMENT
 
 
 @pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 100, 129, 1000, 4096, 10**5, 10**6, 10**7, 10**8, 10**9,
