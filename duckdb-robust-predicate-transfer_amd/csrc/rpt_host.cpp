@@ -703,6 +703,10 @@ std::vector<uint64_t> PTBloomFilter::ExportWords() const {
   return w;
 }
 
+void PTBloomFilter::AllReduceOr(DeviceContext& ctx, void* nccl_comm) {
+  check(rpt_bf_allreduce_or(bf_, nccl_comm, ctx.stream()));
+}
+
 // ---- CreateBF ------------------------------------------------------------------------------------
 CreateBF::CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices,
                    uint64_t sink_flush_rows)

@@ -162,6 +162,9 @@ class PTBloomFilter {
   // Min/max of the valid I32/I64 keys inserted (the min/max dynamic filter; false: none yet).
   bool MinMax(int64_t& min_value, int64_t& max_value) const;
   std::vector<uint64_t> ExportWords() const;
+  // Multi-GPU Combine: OR all-reduce of every rank's partial filter over an RCCL communicator
+  // (ncclComm_t, one rank per GPU; collective: every rank calls it). rpt_bf_allreduce_or.
+  void AllReduceOr(DeviceContext& ctx, void* nccl_comm);
   rpt_bf* native() const { return bf_; }
 
   bool finalized_ = false;
