@@ -114,7 +114,8 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
                                                                       uint8_t* __restrict__ hash_hi,
                                                                       uint16_t* __restrict__ pos_out) {
   extern __shared__ uint32_t s_lo[];  // kL1TileRows hash words (bits 0..31), bucket-sorted, then
-  uint8_t* s_hi = reinterpret_cast<uint8_t*>(s_lo + kL1TileRows);  // their bits 32..39
+  uint8_t* s_hi = reinterpret_cast<uint8_t*>(s_lo + kL1TileRows);  // their bits 32..39, then
+  uint16_t* s_bk = reinterpret_cast<uint16_t*>(s_hi + kL1TileRows);  // their bucket (RPT_SCATTER_FLAT_COPY)
   __shared__ uint32_t s_start[kMaxBuckets], s_cur[kMaxBuckets];
   __shared__ uint64_t s_dst[kMaxBuckets];  // where each bucket's run goes in the level-2 array
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -157,9 +158,11 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
     for (int j = 0; j < 8; j++) {
       uint32_t p = 0;
       if (oo[j]) {
-        p = atomicAdd(&s_cur[bucket_of(hh[j], bucket_mask)], 1u);
+        const uint32_t b = bucket_of(hh[j], bucket_mask);
+        p = atomicAdd(&s_cur[b], 1u);
         s_lo[p] = static_cast<uint32_t>(hh[j]);
         s_hi[p] = static_cast<uint8_t>(hh[j] >> 32);
+        if (RPT_SCATTER_FLAT_COPY) s_bk[p] = static_cast<uint16_t>(b);
       }
       pv[j] = static_cast<uint16_t>(p);
     }
@@ -169,12 +172,25 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
     }
   }
   __syncthreads();
-  for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {  // LDS only: no global latency in the chain
-    const uint32_t c = s_cur[b] - s_start[b], s0 = s_start[b];
-    const uint64_t d = s_dst[b];
-    for (uint32_t i = lane; i < c; i += 64) {
-      hash_lo[d + i] = s_lo[s0 + i];
-      hash_hi[d + i] = s_hi[s0 + i];
+  if (RPT_SCATTER_FLAT_COPY) {
+    // the tile's bucket-sorted rows in order, every lane busy: a wave's 64 rows span ~2 runs, so each
+    // store instruction writes whole pieces of runs (a loop per bucket leaves half the lanes idle)
+    for (uint32_t b = threadIdx.x; b < nb; b += kTileThreads) s_dst[b] -= s_start[b];
+    __syncthreads();
+    const uint32_t used = s_cur[nb - 1];
+    for (uint32_t i = threadIdx.x; i < used; i += kTileThreads) {
+      const uint64_t d = s_dst[s_bk[i]] + i;
+      hash_lo[d] = s_lo[i];
+      hash_hi[d] = s_hi[i];
+    }
+  } else {
+    for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {  // LDS only: no global latency in the chain
+      const uint32_t c = s_cur[b] - s_start[b], s0 = s_start[b];
+      const uint64_t d = s_dst[b];
+      for (uint32_t i = lane; i < c; i += 64) {
+        hash_lo[d + i] = s_lo[s0 + i];
+        hash_hi[d + i] = s_hi[s0 + i];
+      }
     }
   }
 }

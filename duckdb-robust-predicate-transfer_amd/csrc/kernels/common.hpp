@@ -59,6 +59,9 @@ constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: who
 #ifndef RPT_BUCKET_UNPERMUTE_XCD_MAP
 #define RPT_BUCKET_UNPERMUTE_XCD_MAP 1
 #endif
+#ifndef RPT_SCATTER_FLAT_COPY
+#define RPT_SCATTER_FLAT_COPY 1                        // bucketed level-1 scatter: copy-out over sorted rows
+#endif
 #ifndef RPT_SLICE_UNROLL
 #define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
 #endif

@@ -502,7 +502,7 @@ template <int K, bool D>
 void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
                              const uint32_t* counts_tm, const uint32_t* pre_tm, const uint64_t* bbase, uint32_t* hash_lo,
                              uint8_t* hash_hi, uint16_t* pos1) {
-  const size_t lds = rpt::kL1TileRows * 5;
+  const size_t lds = rpt::kL1TileRows * (RPT_SCATTER_FLAT_COPY ? 7 : 5);
   static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into (160 KiB minus the static part)
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D>)); });
   hipLaunchKernelGGL((rpt::bucket_scatter_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, bucket_mask,
