@@ -643,11 +643,15 @@ __global__ __launch_bounds__(kTileBlock) void tile_block_scan_kernel(uint32_t* _
   if (threadIdx.x == 0) block_sums[blockIdx.x] = all;
 }
 
-// C'2 (tile_pre = prefix inside the tile's block, block_offs = the blocks' scan): one 256-thread workgroup per
+// C'2 (tile_pre = prefix inside the tile's block, block_offs = the blocks' scan). 256 threads per 16 Ki
+// rows (8 segments per wave at either tile size: 32 Ki-row tiles get 512 threads, not 16 segments'
+// worth of row-map registers per lane).: one 256-thread workgroup per
 // tile, as unpermute_kernel; each wave's segments are consecutive rows, so a survivor's sel index is
 // tile offset + earlier waves' survivors + earlier segments of this wave + earlier lanes of its segment.
 template <int TM>
-__global__ __launch_bounds__(kUnpermuteThreads) void unpermute_sel_kernel(const uint16_t* __restrict__ pos,
+constexpr int kUnpermuteSelThreads = kUnpermuteThreads * TM;
+template <int TM>
+__global__ __launch_bounds__(kUnpermuteSelThreads<TM>) void unpermute_sel_kernel(const uint16_t* __restrict__ pos,
                                                                          const uint8_t* __restrict__ passbits,
                                                                          uint64_t n, uint64_t tile_cap,
                                                                          const uint32_t* __restrict__ tile_pre,
@@ -655,10 +659,11 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_sel_kernel(const 
                                                                          const uint32_t* __restrict__ row_sel,
                                                                          uint32_t* __restrict__ out_sel) {
   extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
-  __shared__ uint32_t s_wtot[kUnpermuteThreads / 64];
+  constexpr int kThreads = kUnpermuteSelThreads<TM>;
+  __shared__ uint32_t s_wtot[kThreads / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
-  constexpr uint32_t kSegsPerWave = (kTileRows * TM / kSegRows) / (kUnpermuteThreads / 64);
+  constexpr uint32_t kSegsPerWave = (kTileRows * TM / kSegRows) / (kThreads / 64);
   const uint64_t tile = blockIdx.x;
   const uint64_t seg0 = tile * (kTileRows * TM / kSegRows) + wave * kSegsPerWave;
   u32x4 pv[kSegsPerWave];  // 8 row positions (u16) per lane per segment
@@ -669,7 +674,7 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_sel_kernel(const 
   }
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / 8));
-    for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kUnpermuteThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
+    for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
   }
   __syncthreads();
   uint32_t bytes[kSegsPerWave], excl[kSegsPerWave], run = 0;

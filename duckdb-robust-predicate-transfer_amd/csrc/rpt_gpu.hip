@@ -1079,10 +1079,10 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
       RPT_LAUNCHED("group_scan_kernel");
       ProfScope prof7c_("unpermute_sel_kernel", s);
       if (tm == 2)
-        hipLaunchKernelGGL(rpt::unpermute_sel_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads),
+        hipLaunchKernelGGL(rpt::unpermute_sel_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteSelThreads<2>),
                            cap / 8, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
       else
-        hipLaunchKernelGGL(rpt::unpermute_sel_kernel<1>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads),
+        hipLaunchKernelGGL(rpt::unpermute_sel_kernel<1>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteSelThreads<1>),
                            cap / 8, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
       prof7c_.end();
       RPT_LAUNCHED("unpermute_sel_kernel");
