@@ -55,7 +55,7 @@ constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per w
 constexpr uint64_t kL1TileRows = 16384;
 constexpr int kL1SegsPerWave = static_cast<int>(kL1TileRows / kTileThreads / 8);
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
-constexpr int kLdsDirectMaxLog = 13;                   // filters <= 64 KiB: whole filter in LDS
+constexpr int kLdsDirectMaxLog = 14;                   // filters <= 128 KiB: whole filter in LDS
 #ifndef RPT_BUCKET_UNPERMUTE_XCD_MAP
 #define RPT_BUCKET_UNPERMUTE_XCD_MAP 1
 #endif

@@ -6,9 +6,10 @@
 namespace rpt {
 
 // ---- P1: probe -> result bits + per-segment survivor counts ------------------------------------
-// FILTER_IN_LDS: the whole filter (<= 64 KiB) is staged in LDS and every gather is an LDS read.
-template <int K, bool DENSE, bool FILTER_IN_LDS>
-__global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_t* __restrict__ words,
+// FILTER_IN_LDS: the whole filter (<= 128 KiB) is staged in LDS and every gather is an LDS read. A
+// 128 KiB filter leaves room for one workgroup per CU: that case runs 1024-thread workgroups.
+template <int K, bool DENSE, bool FILTER_IN_LDS, int THREADS = kBlockThreads>
+__global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __restrict__ words,
                                                                   uint64_t block_mask, KeyArgs a, uint64_t n,
                                                                   uint64_t n_segs, uint64_t* __restrict__ out_bits,
                                                                   uint32_t* __restrict__ seg_counts) {
@@ -20,8 +21,9 @@ __global__ __launch_bounds__(kBlockThreads) void probe_bits_kernel(const uint64_
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
-  const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWavesPerBlock;
-  for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6); seg < n_segs;
+  constexpr uint32_t kWaves = THREADS / 64;
+  const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWaves;
+  for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6); seg < n_segs;
        seg += total_waves) {
     const uint64_t base = seg * kSegRows;
     uint64_t h[8];

@@ -234,7 +234,7 @@ int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_PROBE_AUTO) return requested;
   const int L = log_num_blocks;
   if (L <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
-  if (L <= rpt::kLdsDirectMaxLog + 2) return RPT_PROBE_GATHER;
+  if (L <= 15) return RPT_PROBE_GATHER;  // 256 KiB: L2-resident gathers beat the partitioned probe
   if (strategy_supported(RPT_PROBE_PARTITIONED, L))
     return n >= (L >= 20 ? (1ULL << 22) : (1ULL << 25)) ? RPT_PROBE_PARTITIONED : RPT_PROBE_GATHER;
   if (strategy_supported(RPT_PROBE_BUCKETED, L))
@@ -431,10 +431,18 @@ void launch_probe_small_t(hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a
 }
 
 // Whole filter in LDS (dynamic LDS = filter bytes); as many workgroups per CU as LDS allows.
+void allow_dynamic_lds(const void* fn);
 template <int K, bool D>
 void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
                              uint64_t n_segs, uint64_t* bits, uint32_t* counts) {
   const size_t lds = 8ULL << bf->log_num_blocks;
+  if (lds > (64u << 10)) {  // one workgroup per CU: 16 waves instead of 4
+    static std::once_flag once;
+    std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::probe_bits_kernel<K, D, true, 1024>)); });
+    hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, true, 1024>), dim3(grid), dim3(1024), lds, s, bf->words,
+                       (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+    return;
+  }
   hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, true>), dim3(grid), dim3(rpt::kBlockThreads), lds, s, bf->words,
                      (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
 }
@@ -994,8 +1002,9 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
   } else if (strategy == RPT_PROBE_LDS) {
     const uint64_t lds = (8ULL << L) + 8ULL * rpt::kNumMasks;
     const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(rpt::kBlocksPerCU, (160ULL << 10) / lds));
+    const uint64_t waves = (8ULL << L) > (64u << 10) ? 16 : rpt::kWavesPerBlock;  // launch_probe_bits_lds_t
     const unsigned grid = static_cast<unsigned>(
-        std::max<uint64_t>(1, std::min(ceil_div(n_segs, rpt::kWavesPerBlock), num_cus(bf->device) * per_cu)));
+        std::max<uint64_t>(1, std::min(ceil_div(n_segs, waves), num_cus(bf->device) * per_cu)));
     ProfScope prof4_("probe_bits_kernel<lds>", s);
     RPT_DISPATCH_KD(launch_probe_bits_lds_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
     prof4_.end();

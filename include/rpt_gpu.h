@@ -55,7 +55,7 @@ typedef enum rpt_probe_strategy {
                                 (<= 256 KiB: L2-resident), PARTITIONED (<= 128 MiB, n >= 4 Mi), BUCKETED
                                 (<= 16 GiB, n >= max(blocks/8, 32 Mi)), otherwise GATHER */
   RPT_PROBE_GATHER = 1,      /* one random 8-byte gather per key from L2 / Infinity Cache / HBM */
-  RPT_PROBE_LDS = 2,         /* whole filter staged in each workgroup's LDS (filters <= 64 KiB) */
+  RPT_PROBE_LDS = 2,         /* whole filter staged in each workgroup's LDS (filters <= 128 KiB) */
   RPT_PROBE_PARTITIONED = 3, /* rows bucketed per 16 Ki-row tile by 128 KiB filter slice; each slice is
                                 probed from LDS, then row order is restored (filters 128 KiB..128 MiB) */
   RPT_PROBE_BUCKETED = 4     /* two levels: rows first bucketed by 16 MiB filter region into contiguous

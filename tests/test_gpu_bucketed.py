@@ -111,7 +111,9 @@ def test_auto_routes_large_filters(rpt):
     bf = rpt.BloomFilter(log_num_blocks=log_nb)
     assert bf.insert_strategy_for(1 << 23) == INS_BUCKETED and bf.insert_strategy_for(1 << 21) == INS_ATOMIC
     assert bf.probe_strategy_for(1 << 25) == BUCKETED and bf.probe_strategy_for(10**7) == GATHER
-    small = rpt.BloomFilter(log_num_blocks=14)  # 128 KiB: stays in L2, always the gather
+    tiny = rpt.BloomFilter(log_num_blocks=14)  # 128 KiB: the whole filter in each CU's LDS
+    assert tiny.probe_strategy_for(1 << 28) == 2 and tiny.probe_strategy_for(1 << 16) == 2
+    small = rpt.BloomFilter(log_num_blocks=15)  # 256 KiB: stays in L2, always the gather
     assert small.probe_strategy_for(1 << 28) == GATHER
     mid = rpt.BloomFilter(log_num_blocks=21)  # 16 MiB (C2): routed from 4 Mi rows
     assert mid.probe_strategy_for(1 << 22) == PARTITIONED and mid.probe_strategy_for(1 << 21) == GATHER
