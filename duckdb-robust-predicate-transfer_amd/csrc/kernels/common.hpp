@@ -62,6 +62,9 @@ constexpr int kLdsDirectMaxLog = 14;                   // filters <= 128 KiB: wh
 #ifndef RPT_SCATTER_FLAT_COPY
 #define RPT_SCATTER_FLAT_COPY 1                        // bucketed level-1 scatter: copy-out over sorted rows
 #endif
+#ifndef RPT_PARTITION_SMALL_P
+#define RPT_PARTITION_SMALL_P 1                        // partition of <= 4-slice filters: wave-aggregated counters
+#endif
 #ifndef RPT_SLICE_UNROLL
 #define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
 #endif

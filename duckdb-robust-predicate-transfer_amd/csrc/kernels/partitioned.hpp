@@ -5,6 +5,28 @@
 
 namespace rpt {
 
+// Inclusive wave-wide max scan of non-negative values (DPP: rows of 16, then row broadcasts 15 / 31).
+__device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false)));
+  return v;
+}
+
+// Inclusive wave-wide prefix sum (DPP, as wave_inclusive_max; wave_inclusive_sum goes through ds_bpermute).
+__device__ __forceinline__ uint32_t wave_inclusive_sum_dpp(uint32_t v) {
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
+  return v;
+}
+
 // ---- slice records -------------------------------------------------------------------------------
 // A record carries the 30 hash bits a filter slice needs, laid out for the slice kernels' 32-bit ALU:
 //   [0..4]   rotation & 31  (v_alignbit reads the low 5 bits of its shift operand: no extract)
@@ -60,7 +82,11 @@ __host__ __device__ constexpr uint64_t partition_lds_bytes(uint32_t n_slices, ui
   return tm == 1 ? tile_cap_for(n_slices, 1) * 4 + 2ULL * n_slices * 4
                  : kTileRows * tm * 4 + 3ULL * n_slices * 4 + (tile_cap_for(n_slices, tm) / kRunPad) * 2;
 }
-template <int K, bool DENSE, bool MM, int TM>
+// SP > 0 (filters of at most SP slices, TM = 1): 16 Ki rows land on so few LDS counters that same-address
+// atomics serialize (P = 2: 4.3 ms per 1e9 rows, P = 4: 2.9 ms, P >= 8: 2.3-2.5 ms). Each lane then counts
+// its rows per slice in registers, a wave adds its totals with one atomic per slice, and rows take
+// positions from per-lane cursors (wave base + DPP prefix over lanes).
+template <int K, bool DENSE, bool MM, int TM, int SP = 0>
 __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4) void partition_kernel(
     KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
     uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm, int64_t* __restrict__ stats,
@@ -89,6 +115,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
     // slice ids stay in registers (2 per word).
     static_assert(kMaxSliceCount <= 65536, "slice ids are packed as 16 bits");
     uint32_t sl2[kRPT / 2] = {};
+    [[maybe_unused]] uint32_t lc[SP > 0 ? SP : 1] = {};  // SP: this lane's rows per slice
     int64_t wmn = kMinInit, wmx = kMaxInit;  // wave-uniform: the key min/max stays out of VGPRs
 #pragma unroll
     for (int sg = 0; sg < kSPW; sg++) {
@@ -107,10 +134,25 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
         const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
         s_rec[seg_local + seg_row<K, DENSE>(j, lane)] = slice_record(hh[j]);
         sl2[(sg * 8 + j) >> 1] |= sl << (16 * (j & 1));
-        if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
+        if constexpr (SP > 0) {
+#pragma unroll
+          for (int q = 0; q < SP; q++) lc[q] += (oo[j] && sl == static_cast<uint32_t>(q)) ? 1u : 0u;
+        } else {
+          if (oo[j]) atomicAdd(&s_cnt[sl], 1u);
+        }
       }
     }
     if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
+    [[maybe_unused]] uint32_t lofs[SP > 0 ? SP : 1], wtot[SP > 0 ? SP : 1];
+    if constexpr (SP > 0) {  // one atomic per wave and slice
+#pragma unroll
+      for (int q = 0; q < SP; q++) {
+        const uint32_t inc = wave_inclusive_sum_dpp(lc[q]);
+        lofs[q] = inc - lc[q];
+        wtot[q] = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
+        if (lane == 0 && wtot[q] != 0) atomicAdd(&s_cnt[q], wtot[q]);
+      }
+    }
     __syncthreads();
     if (wave == 0) {  // exclusive scans of the slice counts, unpadded and padded to kRunPad: kMaxSliceCount/64 per lane
       constexpr int kPer = kMaxSliceCount / 64;
@@ -147,6 +189,15 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
       for (int j = 0; j < 8; j++) rec[sg * 8 + j] = s_rec[seg_local + seg_row<K, DENSE>(j, lane)];
     }
     __syncthreads();
+    [[maybe_unused]] uint32_t cur[SP > 0 ? SP : 1];
+    if constexpr (SP > 0) {  // this lane's first position per slice: the wave's base + earlier lanes' rows
+#pragma unroll
+      for (int q = 0; q < SP; q++) {
+        uint32_t wb = 0;
+        if (lane == 0 && wtot[q] != 0) wb = atomicAdd(&s_cur[q], wtot[q]);
+        cur[q] = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(wb))) + lofs[q];
+      }
+    }
     // ... and scatter them to their slice-sorted (unpadded) LDS positions; the row map gets the padded one
 #pragma unroll
     for (int sg = 0; sg < kSPW; sg++) {
@@ -160,7 +211,16 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
         const bool ok = seg_row<K, DENSE>(j, lane) < seg_rem;
         uint32_t p = 0;
         if (ok) {
-          const uint32_t q = atomicAdd(&s_cur[sl], 1u);
+          uint32_t q;
+          if constexpr (SP > 0) {
+            q = cur[0];
+#pragma unroll
+            for (int t = 1; t < SP; t++) q = sl == static_cast<uint32_t>(t) ? cur[t] : q;
+#pragma unroll
+            for (int t = 0; t < SP; t++) cur[t] += sl == static_cast<uint32_t>(t) ? 1u : 0u;
+          } else {
+            q = atomicAdd(&s_cur[sl], 1u);
+          }
           s_rec[q] = rec[jj];
           p = PAD ? q : q + s_delta[sl];
         }
@@ -287,28 +347,6 @@ __device__ __forceinline__ uint32_t xcd_item(uint32_t item, uint32_t n_items) {
 __device__ __forceinline__ uint32_t batch_tiles(uint64_t n_t) {
   constexpr uint64_t kWaves = kSliceThreads / 64;
   return static_cast<uint32_t>(n_t >= 64 * kWaves ? 64 : (n_t + kWaves - 1) / kWaves);
-}
-
-// Inclusive wave-wide max scan of non-negative values (DPP: rows of 16, then row broadcasts 15 / 31).
-__device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false)));
-  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false)));
-  return v;
-}
-
-// Inclusive wave-wide prefix sum (DPP, as wave_inclusive_max; wave_inclusive_sum goes through ds_bpermute).
-__device__ __forceinline__ uint32_t wave_inclusive_sum_dpp(uint32_t v) {
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
-  return v;
 }
 
 // Same walk as probe_slice_runs, with the slot -> run lookup through a per-wave LDS window instead of

@@ -234,9 +234,11 @@ int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_PROBE_AUTO) return requested;
   const int L = log_num_blocks;
   if (L <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
-  if (L <= 15) return RPT_PROBE_GATHER;  // 256 KiB: L2-resident gathers beat the partitioned probe
+  // measured crossovers (tools/strategy_crossover.py --mid, profiles/r01/strategy_crossover_mid.jsonl):
+  // the partitioned probe overtakes the (partly L2-resident) gather from 2^25 rows for 256 KiB..2 MiB
+  // filters and from 2^22 rows above
   if (strategy_supported(RPT_PROBE_PARTITIONED, L))
-    return n >= (L >= 20 ? (1ULL << 22) : (1ULL << 25)) ? RPT_PROBE_PARTITIONED : RPT_PROBE_GATHER;
+    return n >= (L >= 19 ? (1ULL << 22) : (1ULL << 25)) ? RPT_PROBE_PARTITIONED : RPT_PROBE_GATHER;
   if (strategy_supported(RPT_PROBE_BUCKETED, L))
     return n >= std::max<uint64_t>((1ULL << L) >> 3, 1ULL << 25) ? RPT_PROBE_BUCKETED : RPT_PROBE_GATHER;
   return RPT_PROBE_GATHER;
@@ -456,14 +458,20 @@ void allow_dynamic_lds(const void* fn) {
   (void)hipGetLastError();
 }
 
-template <int K, bool D, bool MM, int TM>
+template <int K, bool D, bool MM, int TM, int SP = 0>
 void launch_partition_tm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
                          uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
                          const uint32_t* dev_n_tiles) {
+  if constexpr (TM == 1 && SP == 0) {
+    if (RPT_PARTITION_SMALL_P && slice_mask + 1 <= 4) {  // few slices: wave-aggregated slice counters
+      launch_partition_tm<K, D, MM, 1, 4>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+      return;
+    }
+  }
   const size_t lds = rpt::partition_lds_bytes(slice_mask + 1, TM);
   static std::once_flag once;  // per instantiation; > 64 KiB of dynamic LDS must be opted into
-  std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM, TM>)); });
-  hipLaunchKernelGGL((rpt::partition_kernel<K, D, MM, TM>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n,
+  std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM, TM, SP>)); });
+  hipLaunchKernelGGL((rpt::partition_kernel<K, D, MM, TM, SP>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n,
                      slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
 }
 

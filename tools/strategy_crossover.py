@@ -58,9 +58,34 @@ def insert_sweep():
         torch.cuda.empty_cache()
 
 
+def mid_sweep():
+    """128 KiB .. 8 MiB filters (1 .. 64 slices), where the LDS, gather and partitioned probes cross."""
+    lib = rpt_amd.load()
+    n_max = 1 << 28
+    for build in (10**5, 2 * 10**5, 4 * 10**5, 8 * 10**5, 16 * 10**5, 32 * 10**5, 64 * 10**5):
+        bf = rpt_amd.BloomFilter(build)
+        bf.insert(rpt_amd.synth_build_keys(build))
+        L = bf.log_num_blocks
+        keys = rpt_amd.synth_probe_keys(n_max, build, 100)
+        for lg in range(16, 29, 2):
+            n = 1 << lg
+            row = {"op": "probe_mid", "build": build, "log_blocks": L, "n": n, "auto": bf.probe_strategy_for(n)}
+            for name, st in STRATS.items():
+                if st == 4 or not lib.rpt_probe_strategy_supported(st, L):
+                    continue
+                bf.probe_strategy = st
+                row[name] = round(time_probe(bf, keys, n), 4)
+            bf.probe_strategy = 0
+            print(json.dumps(row), flush=True)
+        del bf, keys
+        torch.cuda.empty_cache()
+
+
 def main():
     if "--insert" in sys.argv:
         return insert_sweep()
+    if "--mid" in sys.argv:
+        return mid_sweep()
     lib = rpt_amd.load()
     n_max = 1 << 28
     for build in (10**5, 10**7, 10**8, 10**9):
