@@ -16,16 +16,6 @@ __device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
   return v;
 }
 
-// Inclusive wave-wide prefix sum (DPP, as wave_inclusive_max; wave_inclusive_sum goes through ds_bpermute).
-__device__ __forceinline__ uint32_t wave_inclusive_sum_dpp(uint32_t v) {
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
-  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
-  return v;
-}
 
 // ---- slice records -------------------------------------------------------------------------------
 // A record carries the 30 hash bits a filter slice needs, laid out for the slice kernels' 32-bit ALU:
@@ -147,7 +137,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
     if constexpr (SP > 0) {  // one atomic per wave and slice
 #pragma unroll
       for (int q = 0; q < SP; q++) {
-        const uint32_t inc = wave_inclusive_sum_dpp(lc[q]);
+        const uint32_t inc = wave_inclusive_sum(lc[q]);
         lofs[q] = inc - lc[q];
         wtot[q] = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
         if (lane == 0 && wtot[q] != 0) atomicAdd(&s_cnt[q], wtot[q]);
@@ -669,7 +659,7 @@ __global__ __launch_bounds__(kTileBlock) void tile_block_scan_kernel(uint32_t* _
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * kTileBlock + threadIdx.x;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t c = t < n_tiles ? tile_counts[t] : 0u;
-  const uint32_t inc = wave_inclusive_sum_dpp(c);
+  const uint32_t inc = wave_inclusive_sum(c);
   if (lane == 63) s_w[wave] = inc;
   __syncthreads();
   uint32_t off = 0, all = 0;
@@ -728,7 +718,7 @@ __global__ __launch_bounds__(kUnpermuteSelThreads<TM>) void unpermute_sel_kernel
     if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
     bytes[sg] = byte;
     const uint32_t c = __popc(byte);
-    const uint32_t inc = wave_inclusive_sum_dpp(c);
+    const uint32_t inc = wave_inclusive_sum(c);
     excl[sg] = run + inc - c;
     run += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
   }

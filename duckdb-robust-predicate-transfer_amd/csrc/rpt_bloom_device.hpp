@@ -7,6 +7,10 @@
 //   MurmurHash64 finalizer; int32 keys zero-extended through uint32; NULL rows -> NULL_HASH.
 #pragma once
 
+#ifndef RPT_DPP_SCAN
+#define RPT_DPP_SCAN 1  // wave prefix sums through DPP (0: ds_bpermute shuffles)
+#endif
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -121,8 +125,18 @@ __device__ __forceinline__ uint64_t ballot64(bool p) { return __builtin_amdgcn_b
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
-// Inclusive wave-wide prefix sum of a 32-bit value.
+// Inclusive wave-wide prefix sum of a 32-bit value (whole wave active). DPP: shifts within rows of 16,
+// then row broadcasts 15 / 31 -- six dependent VALU ops instead of six ds_bpermute round trips.
 __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
+#if RPT_DPP_SCAN
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x111, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x112, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x114, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x118, 0xf, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x142, 0xa, 0xf, false));
+  v += static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x143, 0xc, 0xf, false));
+  return v;
+#else
   const uint32_t lane = lane_id();
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -130,6 +144,7 @@ __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t v) {
     if (lane >= static_cast<uint32_t>(d)) v += o;
   }
   return v;
+#endif
 }
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
