@@ -487,3 +487,33 @@ def test_fused_sel_tail_equals_two_phase_path(rpt, log_nb, use_row_sel):
     two = out[: int(cnt.item())].cpu().numpy().view(np.uint32)
     assert np.array_equal(fused, exp)
     assert np.array_equal(two, exp)
+
+
+@pytest.mark.parametrize("strategy", ["partitioned", "gather"])
+def test_concurrent_probes_on_two_streams(rpt, strategy):
+    """Two LookupSel calls in flight at once on two streams (DuckDB's operator threads each own a
+    stream and workspace): each gets the oracle's sel for its own rows."""
+    build = orc.synth_build_keys(300000)
+    lnb = 21
+    bf = with_strategy(rpt.BloomFilter(log_num_blocks=lnb), strategy)
+    bf.insert(dev(build))
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, build)
+    probes = [orc.synth_probe_keys(700001, 300000, 200), orc.synth_probe_keys(500003, 300000, 50, start=10**6)]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = []
+    torch.cuda.synchronize()
+    for keys, st in zip(probes, streams):
+        n = keys.size
+        ws = torch.empty(bf.workspace_bytes(n), dtype=torch.uint8, device="cuda:0")
+        sel = torch.empty(n, dtype=torch.int32, device="cuda:0")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+        kd = dev(keys)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            bf.probe_async(kd, n=n, out_sel=sel, out_count=cnt, workspace=ws, stream=st)
+        outs.append((sel, cnt, ws, kd))
+    torch.cuda.synchronize()
+    for (sel, cnt, _ws, _kd), keys in zip(outs, probes):
+        got = sel[: int(cnt.item())].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, orc.probe_keys(w, lnb, keys))
