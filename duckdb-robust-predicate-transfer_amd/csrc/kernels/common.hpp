@@ -65,6 +65,9 @@ constexpr int kLdsDirectMaxLog = 14;                   // filters <= 128 KiB: wh
 #ifndef RPT_PARTITION_SMALL_P
 #define RPT_PARTITION_SMALL_P 1                        // partition of <= 4-slice filters: wave-aggregated counters
 #endif
+#ifndef RPT_VALU_INTERLEAVE
+#define RPT_VALU_INTERLEAVE 1                          // store_segment_bits: bit interleave on VALU (lanes 0-7)
+#endif
 #ifndef RPT_SLICE_UNROLL
 #define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
 #endif
@@ -221,7 +224,30 @@ __device__ __forceinline__ void store_segment_bits(const bool (&pass)[8], uint32
                                                    uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
   uint64_t word[8];
   uint32_t cnt = 0;
-  if constexpr (DENSE) {
+  if constexpr (DENSE && RPT_VALU_INTERLEAVE) {
+    // lane w < 8 builds result word w from the two (V = 2) or four (V = 4) ballots it interleaves: the
+    // bit spreading runs once on the vector unit instead of eight times on the scalar unit
+    constexpr int V = KeyTraits<K>::kVec;
+    uint64_t b[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      b[j] = ballot64(pass[j]);
+      cnt += __popcll(b[j]);
+    }
+    const uint32_t w = lane & 7, c = w / V, q = w % V;
+    uint64_t mine = 0;
+#pragma unroll
+    for (int e = 0; e < V; e++) {
+      uint64_t src = 0;  // ballot c * V + e of this lane's word
+#pragma unroll
+      for (int cc = 0; cc < 8 / V; cc++) src = (c == static_cast<uint32_t>(cc)) ? b[cc * V + e] : src;
+      if constexpr (V == 2) mine |= spread2(src >> (32 * q)) << e;
+      else mine |= spread4(src >> (16 * q)) << e;
+    }
+    if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
+    if (seg_counts != nullptr && lane == 0) seg_counts[seg] = cnt;
+    return;
+  } else if constexpr (DENSE) {
     constexpr int V = KeyTraits<K>::kVec;
     uint64_t b[8];
 #pragma unroll
