@@ -56,6 +56,7 @@ constexpr uint64_t kL1TileRows = 16384;
 constexpr int kL1SegsPerWave = static_cast<int>(kL1TileRows / kTileThreads / 8);
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
 constexpr int kLdsDirectMaxLog = 14;                   // filters <= 128 KiB: whole filter in LDS
+constexpr int kLdsProbeThreads = 1024;                 // whole-filter LDS probe workgroup (16 waves)
 #ifndef RPT_BUCKET_UNPERMUTE_XCD_MAP
 #define RPT_BUCKET_UNPERMUTE_XCD_MAP 1
 #endif

@@ -6,8 +6,8 @@
 namespace rpt {
 
 // ---- P1: probe -> result bits + per-segment survivor counts ------------------------------------
-// FILTER_IN_LDS: the whole filter (<= 128 KiB) is staged in LDS and every gather is an LDS read. A
-// 128 KiB filter leaves room for one workgroup per CU: that case runs 1024-thread workgroups.
+// FILTER_IN_LDS: the whole filter (<= 128 KiB) is staged in LDS and every gather is an LDS read; it runs
+// 1024-thread workgroups (kLdsProbeThreads).
 template <int K, bool DENSE, bool FILTER_IN_LDS, int THREADS = kBlockThreads>
 __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __restrict__ words,
                                                                   uint64_t block_mask, KeyArgs a, uint64_t n,

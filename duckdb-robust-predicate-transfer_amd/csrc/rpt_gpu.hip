@@ -432,21 +432,18 @@ void launch_probe_small_t(hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a
                      (1ULL << bf->log_num_blocks) - 1, a, n, row_sel, out_sel, out_count);
 }
 
-// Whole filter in LDS (dynamic LDS = filter bytes); as many workgroups per CU as LDS allows.
+// Whole filter in LDS (dynamic LDS = filter bytes), 1024-thread workgroups (16 waves): as many per CU as
+// LDS allows. Measured against 256-thread workgroups: 16 KiB 1.79 -> 1.67 ms, 64 KiB 2.07 -> 1.73 ms per
+// 1e9 int64 keys (int32: 1.71 -> 1.26 ms); a 128 KiB filter fits one workgroup per CU either way.
 void allow_dynamic_lds(const void* fn);
 template <int K, bool D>
 void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
                              uint64_t n_segs, uint64_t* bits, uint32_t* counts) {
   const size_t lds = 8ULL << bf->log_num_blocks;
-  if (lds > (64u << 10)) {  // one workgroup per CU: 16 waves instead of 4
-    static std::once_flag once;
-    std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::probe_bits_kernel<K, D, true, 1024>)); });
-    hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, true, 1024>), dim3(grid), dim3(1024), lds, s, bf->words,
-                       (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
-    return;
-  }
-  hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, true>), dim3(grid), dim3(rpt::kBlockThreads), lds, s, bf->words,
-                     (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+  static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into
+  std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::probe_bits_kernel<K, D, true, rpt::kLdsProbeThreads>)); });
+  hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, true, rpt::kLdsProbeThreads>), dim3(grid), dim3(rpt::kLdsProbeThreads), lds,
+                     s, bf->words, (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
 }
 
 // Let `fn` use all of the CU's 160 KiB of LDS: dynamic allowance = 160 KiB - its static LDS.
@@ -1010,7 +1007,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
   } else if (strategy == RPT_PROBE_LDS) {
     const uint64_t lds = (8ULL << L) + 8ULL * rpt::kNumMasks;
     const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(rpt::kBlocksPerCU, (160ULL << 10) / lds));
-    const uint64_t waves = (8ULL << L) > (64u << 10) ? 16 : rpt::kWavesPerBlock;  // launch_probe_bits_lds_t
+    const uint64_t waves = rpt::kLdsProbeThreads / 64;  // launch_probe_bits_lds_t
     const unsigned grid = static_cast<unsigned>(
         std::max<uint64_t>(1, std::min(ceil_div(n_segs, waves), num_cus(bf->device) * per_cu)));
     ProfScope prof4_("probe_bits_kernel<lds>", s);
