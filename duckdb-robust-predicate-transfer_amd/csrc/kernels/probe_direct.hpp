@@ -8,6 +8,52 @@ namespace rpt {
 // ---- P1: probe -> result bits + per-segment survivor counts ------------------------------------
 // FILTER_IN_LDS: the whole filter (<= 128 KiB) is staged in LDS and every gather is an LDS read; it runs
 // 1024-thread workgroups (kLdsProbeThreads).
+//
+// Full segments of flat columns without validity take a software-pipelined loop: the wave's next
+// segment is loaded into a second set of registers (ping-pong, so no register copy has to wait for
+// it) while the current one is hashed and probed. The general loop (load_hashes: tails, validity,
+// dictionaries) takes whatever is left.
+#ifndef RPT_PROBE_PREFETCH
+#define RPT_PROBE_PREFETCH 1
+#endif
+template <int K> struct RawSeg {
+  static constexpr int V = KeyTraits<K>::kVec;
+  static constexpr int kLoads = 8 / V;
+  using Vec = typename std::conditional<V == 2, u64x2, u32x4>::type;
+  Vec r[kLoads];
+  __device__ __forceinline__ void load(const void* keys, uint64_t seg, uint32_t lane) {
+    using T = typename KeyTraits<K>::T;
+    const T* kb = static_cast<const T*>(keys) + seg * kSegRows + lane * V;
+#pragma unroll
+    for (int c = 0; c < kLoads; c++) r[c] = *reinterpret_cast<const Vec*>(kb + c * 64 * V);
+  }
+  __device__ __forceinline__ void hashes(uint64_t (&h)[8]) const {
+    using T = typename KeyTraits<K>::T;
+#pragma unroll
+    for (int c = 0; c < kLoads; c++)
+#pragma unroll
+      for (int e = 0; e < V; e++) h[c * V + e] = KeyTraits<K>::hash(static_cast<T>(r[c][e]));
+  }
+};
+
+template <bool FILTER_IN_LDS>
+__device__ __forceinline__ void probe8(const uint64_t* __restrict__ words, const uint64_t* s_filter,
+                                       const uint64_t* s_masks, uint64_t block_mask, const uint64_t (&h)[8],
+                                       const bool (&ok)[8], bool (&pass)[8]) {
+  uint64_t w[8], m[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    m[j] = mask_of(s_masks, h[j]);
+    if constexpr (FILTER_IN_LDS) {
+      w[j] = s_filter[block_of(h[j], block_mask)];
+    } else {
+      w[j] = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; j++) pass[j] = ok[j] && (w[j] & m[j]) == m[j];
+}
+
 template <int K, bool DENSE, bool FILTER_IN_LDS, int THREADS = kBlockThreads>
 __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __restrict__ words,
                                                                   uint64_t block_mask, KeyArgs a, uint64_t n,
@@ -23,25 +69,44 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
   const uint32_t lane = threadIdx.x & 63;
   constexpr uint32_t kWaves = THREADS / 64;
   const uint64_t total_waves = static_cast<uint64_t>(gridDim.x) * kWaves;
-  for (uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWaves + (threadIdx.x >> 6); seg < n_segs;
-       seg += total_waves) {
-    const uint64_t base = seg * kSegRows;
-    uint64_t h[8];
-    bool ok[8];
-    load_hashes<K, DENSE>(a, base, n, lane, h, ok);
-    uint64_t w[8], m[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      m[j] = mask_of(s_masks, h[j]);
-      if constexpr (FILTER_IN_LDS) {
-        w[j] = s_filter[block_of(h[j], block_mask)];
-      } else {
-        w[j] = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
+  // the wave index is uniform: keep seg in scalar registers
+  uint64_t seg = static_cast<uint64_t>(blockIdx.x) * kWaves +
+                 static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6)));
+#if RPT_PROBE_PREFETCH
+  if constexpr (DENSE && K != kKeySplit) {
+    const uint64_t n_full = n / kSegRows;
+    if (a.validity == nullptr && seg < n_full) {
+      const bool ok[8] = {true, true, true, true, true, true, true, true};
+      RawSeg<K> A, B;
+      A.load(a.keys, seg, lane);
+      for (;;) {
+        uint64_t h[8];
+        bool pass[8];
+        uint64_t nx = seg + total_waves;
+        B.load(a.keys, nx < n_full ? nx : seg, lane);
+        asm volatile("" ::: "memory");  // issue the next segment's loads before this one's work
+        A.hashes(h);
+        probe8<FILTER_IN_LDS>(words, s_filter, s_masks, block_mask, h, ok, pass);
+        store_segment_bits<K, DENSE>(pass, lane, seg, out_bits, seg_counts);
+        seg = nx;
+        if (seg >= n_full) break;
+        nx = seg + total_waves;
+        A.load(a.keys, nx < n_full ? nx : seg, lane);
+        asm volatile("" ::: "memory");  // issue the next segment's loads before this one's work
+        B.hashes(h);
+        probe8<FILTER_IN_LDS>(words, s_filter, s_masks, block_mask, h, ok, pass);
+        store_segment_bits<K, DENSE>(pass, lane, seg, out_bits, seg_counts);
+        seg = nx;
+        if (seg >= n_full) break;
       }
     }
-    bool pass[8];
-#pragma unroll
-    for (int j = 0; j < 8; j++) pass[j] = ok[j] && (w[j] & m[j]) == m[j];
+  }
+#endif
+  for (; seg < n_segs; seg += total_waves) {
+    uint64_t h[8];
+    bool ok[8], pass[8];
+    load_hashes<K, DENSE>(a, seg * kSegRows, n, lane, h, ok);
+    probe8<FILTER_IN_LDS>(words, s_filter, s_masks, block_mask, h, ok, pass);
     store_segment_bits<K, DENSE>(pass, lane, seg, out_bits, seg_counts);
   }
 }
