@@ -51,9 +51,10 @@ typedef enum rpt_key_type {
 
 /* How a probe reaches the filter blocks (rpt_bf_set_probe_strategy). All give identical results. */
 typedef enum rpt_probe_strategy {
-  RPT_PROBE_AUTO = 0,        /* by filter and batch size (measured crossovers): LDS (<= 64 KiB), GATHER
-                                (<= 256 KiB: L2-resident), PARTITIONED (<= 128 MiB, n >= 4 Mi), BUCKETED
-                                (<= 16 GiB, n >= max(blocks/8, 32 Mi)), otherwise GATHER */
+  RPT_PROBE_AUTO = 0,        /* by filter and batch size (measured crossovers): LDS (<= 128 KiB);
+                                PARTITIONED (<= 128 MiB) for n >= 32 Mi (256 KiB..2 MiB) or n >= 4 Mi
+                                (4 MiB and up); BUCKETED (<= 16 GiB, n >= max(blocks/8, 32 Mi));
+                                otherwise GATHER */
   RPT_PROBE_GATHER = 1,      /* one random 8-byte gather per key from L2 / Infinity Cache / HBM */
   RPT_PROBE_LDS = 2,         /* whole filter staged in each workgroup's LDS (filters <= 128 KiB) */
   RPT_PROBE_PARTITIONED = 3, /* rows bucketed per 16 Ki-row tile by 128 KiB filter slice; each slice is
