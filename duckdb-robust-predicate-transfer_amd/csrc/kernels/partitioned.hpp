@@ -54,6 +54,22 @@ __device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_
   return ((~xl & static_cast<uint32_t>(e)) | (~xh & static_cast<uint32_t>(e >> 32))) == 0u;
 }
 
+// Where pass 1 parks a row's record in LDS until pass 2 takes it back (same thread, same slot): any
+// per-segment bijection works, so lane-major slots (j * 64 + lane: consecutive words across the wave,
+// no bank conflicts) instead of the row's own position (stride V words across lanes: 2- / 4-way
+// conflicts for int64 / int32 keys).
+#ifndef RPT_PARK_LANE_MAJOR
+#define RPT_PARK_LANE_MAJOR 1
+#endif
+template <int K, bool DENSE>
+__device__ __forceinline__ uint32_t park_slot(int j, uint32_t lane) {
+#if RPT_PARK_LANE_MAJOR
+  return static_cast<uint32_t>(j) * 64u + lane;
+#else
+  return seg_row<K, DENSE>(j, lane);
+#endif
+}
+
 // ---- partitioned probe, A: bucket a tile of kTileRows rows by filter slice ------------------------
 // Row r of the tile gets record slice_record(hash) stored at position pos(r) of the tile's
 // slice-sorted record array (runs padded to kRunPad records); pos(r) is written per row (u16) so
@@ -122,7 +138,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
-        s_rec[seg_local + seg_row<K, DENSE>(j, lane)] = slice_record(hh[j]);
+        s_rec[seg_local + park_slot<K, DENSE>(j, lane)] = slice_record(hh[j]);
         sl2[(sg * 8 + j) >> 1] |= sl << (16 * (j & 1));
         if constexpr (SP > 0) {
 #pragma unroll
@@ -176,7 +192,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
     for (int sg = 0; sg < kSPW; sg++) {
       const uint32_t seg_local = wave * (kSPW * kSegRows) + sg * kSegRows;
 #pragma unroll
-      for (int j = 0; j < 8; j++) rec[sg * 8 + j] = s_rec[seg_local + seg_row<K, DENSE>(j, lane)];
+      for (int j = 0; j < 8; j++) rec[sg * 8 + j] = s_rec[seg_local + park_slot<K, DENSE>(j, lane)];
     }
     __syncthreads();
     [[maybe_unused]] uint32_t cur[SP > 0 ? SP : 1];
