@@ -517,3 +517,22 @@ def test_concurrent_probes_on_two_streams(rpt, strategy):
     for (sel, cnt, _ws, _kd), keys in zip(outs, probes):
         got = sel[: int(cnt.item())].cpu().numpy().view(np.uint32)
         assert np.array_equal(got, orc.probe_keys(w, lnb, keys))
+
+
+@pytest.mark.parametrize("strategy", ["gather", "lds"])
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+@pytest.mark.parametrize("n", [2**22 + 5, 5 * 2**21, 2**24 + 3 * 512 + 1, 20000003])
+def test_direct_probe_pipelined_rounds_vs_oracle(rpt, strategy, dtype, n):
+    """The direct probes' software-pipelined loop over full 512-row segments: several rounds of the
+    whole grid, groups cut off by the last full segment, and the ragged tail taken by the general loop."""
+    rng = np.random.default_rng(n + 7 * (dtype == np.int32))
+    build = rng.integers(-2**31, 2**31, size=20000, dtype=np.int64).astype(dtype)
+    probe = rng.integers(-2**31, 2**31, size=n, dtype=np.int64).astype(dtype)
+    probe[rng.integers(0, n, size=n // 10)] = build[rng.integers(0, build.size, size=n // 10)]
+    lnb = orc.log_num_blocks(build.size)
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, build)
+    bf = with_strategy(rpt.BloomFilter(build.size), strategy)
+    bf.insert(dev(build))
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, lnb, probe))
