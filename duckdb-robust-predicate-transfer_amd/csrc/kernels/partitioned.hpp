@@ -54,6 +54,23 @@ __device__ __forceinline__ bool probe_rec(const uint64_t* s_slice, const uint64_
   return ((~xl & static_cast<uint32_t>(e)) | (~xh & static_cast<uint32_t>(e >> 32))) == 0u;
 }
 
+// Stores of the partition's outputs (records, row map). With 16 Ki-row tiles (TM = 1) they are
+// non-temporal: gigabytes re-read by the next kernels from HBM anyway, and keeping them out of the
+// caches helps the neighbours (C2: partition 2.26 -> 2.25 ms, slice probe 0.877 -> 0.863 ms). The
+// TM = 2 copy-out (16-B pieces assembled from unpadded LDS) got much slower with them: C3 partition
+// 2.59 -> 3.39 ms.
+#ifndef RPT_NT_PART_STORES
+#define RPT_NT_PART_STORES 1
+#endif
+template <bool NT, typename T>
+__device__ __forceinline__ void part_store(T* p, T v) {
+  if constexpr (NT && RPT_NT_PART_STORES) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
 // Where pass 1 parks a row's record in LDS until pass 2 takes it back (same thread, same slot): any
 // per-segment bijection works, so lane-major slots (j * 64 + lane: consecutive words across the wave,
 // no bank conflicts) instead of the row's own position (stride V words across lanes: 2- / 4-way
@@ -240,12 +257,12 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
         for (int c = 0; c < 8 / V; c++) {
           const uint64_t row0 = base + static_cast<uint64_t>(c) * 64 * V + static_cast<uint64_t>(lane) * V;
           if constexpr (V == 2) {
-            *reinterpret_cast<uint32_t*>(pos_out + row0) =
-                static_cast<uint32_t>(pv[c * 2]) | (static_cast<uint32_t>(pv[c * 2 + 1]) << 16);
+            part_store<TM == 1>(reinterpret_cast<uint32_t*>(pos_out + row0),
+                       static_cast<uint32_t>(pv[c * 2]) | (static_cast<uint32_t>(pv[c * 2 + 1]) << 16));
           } else {
-            *reinterpret_cast<uint64_t*>(pos_out + row0) =
-                static_cast<uint64_t>(pv[c * 4]) | (static_cast<uint64_t>(pv[c * 4 + 1]) << 16) |
-                (static_cast<uint64_t>(pv[c * 4 + 2]) << 32) | (static_cast<uint64_t>(pv[c * 4 + 3]) << 48);
+            part_store<TM == 1>(reinterpret_cast<uint64_t*>(pos_out + row0),
+                       static_cast<uint64_t>(pv[c * 4]) | (static_cast<uint64_t>(pv[c * 4 + 1]) << 16) |
+                           (static_cast<uint64_t>(pv[c * 4 + 2]) << 32) | (static_cast<uint64_t>(pv[c * 4 + 3]) << 48));
           }
         }
       } else {
@@ -260,7 +277,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
     if constexpr (PAD) {
       const uint32_t used = s_cur[slice_mask] - s_cnt[slice_mask] + pad_run(s_cnt[slice_mask]);
       const u32x4* src = reinterpret_cast<const u32x4*>(s_rec);
-      for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) dst[i] = src[i];
+      for (uint32_t i = threadIdx.x; i < used / 4; i += kTileThreads) part_store<TM == 1>(dst + i, src[i]);
       for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
         runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i]) << 16) | s_cnt[i];  // padded start | true count
     } else {
@@ -276,7 +293,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
         u32x4 v;
 #pragma unroll
         for (int e = 0; e < 4; e++) v[e] = s_rec[min(q + e, static_cast<uint32_t>(kTR) - 1)];
-        dst[i] = v;
+        part_store<TM == 1>(dst + i, v);
       }
       for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads)
         runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i] + s_delta[i]) << 16) | s_cnt[i];  // padded start | true count
