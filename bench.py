@@ -1,25 +1,40 @@
 #!/usr/bin/env python3
 """Headline benchmark: USE_BF Bloom-filter probe throughput on MI355X (BASELINE.json metric
-"bloom probe keys/sec (whole node)", config C2).
+"bloom probe keys/sec (whole node)"; default config C2).
 
 One step = one probe pass of the hot path (PTBloomFilter::LookupSel, reference
 src/bloom_filter.cpp:60-68, as PhysicalUseBF::ExecuteInternal drives it) over this rank's batch of
-1e9 device-resident int64 keys against the filter CREATE_BF built from 1e7 keys: hash, gather,
-ascending uint32 selection vector + survivor count. Multi-GPU (torch.distributed.run, one process
-per GPU): the build rows are split by row range, partial filters are OR-merged over RCCL, and
-every rank probes its own 1e9-row slice of the global probe column (weak scaling, no data-path
-collective in the probe).
+1e9 device-resident int64 keys against the filter CREATE_BF built: hash, filter test, ascending
+uint32 selection vector + survivor count.
 
-Prints ONE JSON line on rank 0. `roofline` prices the dominant kernel (probe phase 1) from HIP
-events recorded on the launch stream; `cpu_baseline` times the C++ restatement (oracle/) on a
-bounded sample on rank 0's host cores.
+Configs (--config; BASELINE.json configs[1], [2], [4]):
+  C2  1e7-key build (16 MiB filter), 1e9-key probe per GPU                     (default)
+  C3  1e8-key build (128 MiB filter), 1e9-key probe per GPU
+  C5  filter sized for 8e9 rows (8 GiB); every rank inserts its 1e9-row shard of the build column
+      (8e9 rows at 8 GPUs, weak-scaled below), partial filters OR-merged over RCCL, 1e9-key probe per GPU
+
+Multi-GPU: one process per GPU. `--gpus N` without a launcher starts N ranks itself
+(torch.distributed.run, 127.0.0.1) before any GPU call; under a launcher WORLD_SIZE must equal N.
+The build rows are split by row range, each rank's partial filter (sized for the GLOBAL row count)
+is OR-merged through the C-ABI's rpt_bf_allreduce_or over an RCCL communicator the library creates
+(the product path a C++ caller gets), checked bit-identical to a single-GPU build of all rows, and
+every rank probes its own 1e9-row slice of the global probe column (weak scaling, no data-path
+collective in the probe). RPT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (the merge then
+runs the torch.distributed composition over host memory).
+
+Prints ONE JSON line on rank 0. `roofline` prices the dominant kernel from HIP events the library
+records on the launch stream (rpt_profiling_*) and its PMC traffic from profiles/pmc/<config>.json
+(the exact template instantiation, or null); `cpu_baseline` times the C++ restatement (oracle/) on
+rank 0's host cores.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
 import statistics
+import subprocess
 import sys
 import time
 
@@ -30,73 +45,99 @@ HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 KEY_BYTES = 8           # int64 key read per probed row (algorithmic)
 SEL_BYTES = 4           # uint32 sel entry written per survivor (algorithmic)
 
+CONFIGS = {  # name -> (global build rows at N GPUs, filter sized for, description)
+    "C2": (lambda n: 10**7, lambda n: 10**7),
+    "C3": (lambda n: 10**8, lambda n: 10**8),
+    "C5": (lambda n: n * 10**9, lambda n: 8 * 10**9),
+}
+
+
+def cpu_share() -> int:
+    """Host threads this process may use: the affinity mask, capped by the cgroup CPU quota (the GPU
+    box grants each job a share of a larger machine: `nproc` shows the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return n
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                    help="BASELINE config (sets --build-rows / --filter-rows); default C2")
     ap.add_argument("--probe-rows", type=float, default=1e9, help="probe rows per GPU")
-    ap.add_argument("--build-rows", type=float, default=1e7, help="global build rows")
+    ap.add_argument("--build-rows", type=float, default=None, help="global build rows (default: the config's)")
     ap.add_argument("--filter-rows", type=float, default=None,
-                    help="size the filter for this many rows (default: --build-rows). C5 on one GPU = one "
-                         "rank's share: --filter-rows 8e9 --build-rows 1e9")
+                    help="size the filter for this many rows (default: the config's, else --build-rows)")
     ap.add_argument("--p", type=float, default=0.10, help="fraction of probe rows drawn from the build keys")
     ap.add_argument("--cpu-sample", type=float, default=None,
                     help="probe rows in the CPU-baseline sample (default: the whole per-GPU probe workload)")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "16")))
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "0")) or None,
+                    help="CPU-baseline threads (default: this process's CPU share, see cpu_share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-merge-check", action="store_true",
+                    help="skip the (untimed) bit-identity check of the OR-merged filter (N > 1)")
     ap.add_argument("--key-type", default="i64", choices=["i64", "i32"],
                     help="key column type (i32: the synthetic keys truncated to int32, as JOB's INTEGER keys)")
     ap.add_argument("--strategy", default="auto", choices=["auto", "gather", "lds", "partitioned", "bucketed"],
-                    help="probe strategy (auto picks by filter size)")
+                    help="probe strategy (auto picks by filter and batch size)")
     return ap.parse_args()
 
 
+def config_tag(cfg: str, key_type: str) -> str:
+    return cfg + ("-i32" if key_type == "i32" else "")
+
+
 def algorithmic_bytes(kernel: str, n: int, survivors: int, key_bytes: int = KEY_BYTES) -> int:
-    """SURVEY §8(d) per-unit bytes for the kernel's part of the probe: every kernel that streams the
-    key column is charged 8 B/key (the key read; its own intermediates are implementation traffic,
+    """SURVEY §8(d) per-unit bytes for the kernel's part of the probe: kernels that stream the key
+    column are charged 8 B/key (4 B for int32; their own intermediates are implementation traffic,
     counted in `traffic`); the kernels that write the selection vector (the compaction, or the fused
-    unpermute) are charged the 4 B/survivor they write."""
+    unpermute) are charged the 4 B/survivor they write; everything else (routing intermediates, scans,
+    the bucketed level-2 pass over the split-hash array) is charged 0."""
     if kernel.startswith(("compact", "unpermute_sel")):
         return SEL_BYTES * survivors
-    if kernel.startswith(("slice_probe", "unpermute", "group_", "bucket_unpermute", "bucket_scan", "runs_transpose",
-                          "tile_count")):
-        return 0
-    return key_bytes * n
+    if kernel.startswith(("probe_bits", "probe_small", "bucket_count", "bucket_scatter")):
+        return key_bytes * n
+    if kernel.startswith("partition_kernel<") and kernel[len("partition_kernel<"):].split(",")[0] in ("0", "1", "2"):
+        return key_bytes * n
+    return 0
 
 
-def pmc_traffic(kernel: str, key_k: int = 0):
-    """HBM bytes per launch of `kernel` from the PMC summary tools/pmc_summary.py wrote for this build
-    (FETCH_SIZE doubled per the gfx950 correction + WRITE_SIZE, separate rocprofv3 --pmc passes)."""
-    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+def pmc_traffic(kernel: str, tag: str):
+    """HBM bytes per launch of exactly this kernel instantiation in this config, from the PMC summary
+    tools/profile_round.sh wrote (profiles/pmc/<tag>.json: FETCH_SIZE doubled per the gfx950 correction +
+    WRITE_SIZE, separate rocprofv3 --pmc passes of the same bench command). None if not profiled."""
+    path = os.path.join(REPO, "profiles", "pmc", f"{tag}.json")
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    # the kernel's instantiations (name or name<template args>); the probe's is the longest-running
-    # (key-typed instantiations: the first template argument is the key type, 0 = int64, 1 = int32)
-    cands = [v for name, v in d.get("kernels", {}).items()
-             if (name == kernel or name.startswith(kernel + "<")) and "hbm_bytes_per_launch" in v
-             and not (name.startswith(kernel + "<") and name[len(kernel) + 1:].split(",")[0] in ("0", "1")
-                      and name[len(kernel) + 1:].split(",")[0] != str(key_k))]
-    if not cands:
+    k = d.get("kernels", {}).get(kernel)
+    if not k or "hbm_bytes_per_launch" not in k:
         return None
-    k = max(cands, key=lambda v: v.get("avg_ms", 0.0))
-    return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": f"profiles/pmc_latest.json ({d.get('round')})"}
+    return {"bytes_per_launch": k["hbm_bytes_per_launch"], "source": f"profiles/pmc/{tag}.json ({d.get('round')})"}
 
 
-def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int, key_type: str = "i64") -> dict:
-    """The C++ restatement of the reference CPU path, morsel-parallel in 2048-row vectors. int32 keys run
+def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, threads: int, threads_src: str,
+                 key_type: str = "i64") -> dict:
+    """The C++ restatement of the reference CPU path, morsel-parallel in 2048-row vectors, against the
+    SAME filter geometry the GPU probes (sized for n_filter rows, n_build keys inserted). int32 keys run
     zero-extended to int64: DuckDB hashes an INTEGER through uint32 -> uint64, so hashes and survivors
     are the same (the port then reads 8 B per key instead of 4)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import rpt_oracle as orc
 
-    threads = max(1, min(threads, len(os.sched_getaffinity(0))))
-    lnb = orc.log_num_blocks(n_build)
+    lnb = orc.log_num_blocks(n_filter)
     words = orc.new_words(lnb)
     as_i32 = (lambda k: k.astype(np.int32).view(np.uint32).astype(np.int64)) if key_type == "i32" else (lambda k: k)
     build_keys = as_i32(orc.synth_build_keys(n_build))
@@ -112,8 +153,9 @@ def cpu_baseline(n_build: int, p_permille: int, sample: int, threads: int, key_t
         "cores": threads,
         "kind": "port",
         "sample": (f"probe of the first {sample:.0e} rows (the GPU's whole per-step workload when equal to its "
-                   f"probe rows) of the same synthetic probe stream against the same "
-                   f"{n_build:.0e}-key filter (2^{lnb} blocks), {threads} std::threads, 2048-row vectors, "
+                   f"probe rows) of the same synthetic probe stream against the same filter "
+                   f"({n_build:.0e} keys inserted, sized for {n_filter:.0e} rows: 2^{lnb} blocks), {threads} "
+                   f"std::threads ({threads_src}), 2048-row vectors, "
                    f"{'int32 keys zero-extended (same hashes), ' if key_type == 'i32' else ''}"
                    f"hash included; median of 5 after 1 warm-up; build of the filter {n_build / build_s:.3e} keys/s"),
         "cpu_model": _cpu_model(),
@@ -132,16 +174,37 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """Start n ranks of this script under torch.distributed.run (before this process touches a GPU) and
+    return their exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0:
+        if args.gpus > 1:
+            sys.exit(launch_ranks(args.gpus))
+        world = 1
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with --nproc-per-node {args.gpus}")
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # RPT_BENCH_BACKEND=gloo is a rehearsal mode for boxes with fewer GPUs than ranks: ranks share
-    # devices and the OR-merge collectives run over gloo through host memory. Default: RCCL.
+    # devices and the OR merge runs the torch.distributed composition over host memory. Default: RCCL.
     backend = os.environ.get("RPT_BENCH_BACKEND", "nccl")
     dev_index = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(dev_index)
@@ -154,24 +217,33 @@ def main():
 
     import rpt_amd
     from rpt_amd import _lib as rpt_lib
-    from rpt_amd.distributed import allreduce_or_filter, shard_range
+    from rpt_amd.distributed import RcclComm, allreduce_or_filter, allreduce_or_native, shard_range
 
+    cfg = args.config or ("C2" if args.build_rows is None and args.filter_rows is None else None)
     n_probe = int(args.probe_rows)
-    n_build = int(args.build_rows)
-    n_filter = int(args.filter_rows) if args.filter_rows else n_build
+    if cfg is not None:
+        n_build = int(args.build_rows) if args.build_rows else CONFIGS[cfg][0](world)
+        n_filter = int(args.filter_rows) if args.filter_rows else CONFIGS[cfg][1](world)
+    else:
+        n_build = int(args.build_rows)
+        n_filter = int(args.filter_rows) if args.filter_rows else n_build
+    if cfg is not None and (n_build, n_filter) != (CONFIGS[cfg][0](world), CONFIGS[cfg][1](world)):
+        cfg = None
+    if cfg is None:
+        cfg = "custom"
+    tag = config_tag(cfg, args.key_type)
     p_permille = int(round(args.p * 1000))
-    cfg = {(10**7, 10**7): "C2", (10**8, 10**8): "C3", (10**9, 8 * 10**9): "C5 (one rank's share)",
-           (8 * 10**9, 8 * 10**9): "C5"}.get((n_build, n_filter), "custom")
 
     def barrier():
         if world > 1:
             dist.barrier(device_ids=[dev_index]) if backend == "nccl" else dist.barrier()
 
+    def keys_of(t):
+        return t.to(torch.int32) if args.key_type == "i32" else t
+
     # ---- CREATE_BF: sharded build + OR merge (reported, not the headline) -------------------------
     lo, hi = shard_range(n_build, rank, world)
-    build_keys = rpt_amd.synth_build_keys(hi - lo, start=lo, device=device)
-    if args.key_type == "i32":
-        build_keys = build_keys.to(torch.int32)
+    build_keys = keys_of(rpt_amd.synth_build_keys(hi - lo, start=lo, device=device))
     bf = rpt_amd.BloomFilter(n_filter, device=device)
     bf.insert(build_keys)  # warm-up: workspace allocation, code-object load
     build_reps = 5
@@ -183,30 +255,40 @@ def main():
         bf.insert(build_keys)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    allreduce_or_filter(bf) if world > 1 else None
+    del build_keys
+    comm = RcclComm(device) if world > 1 and backend == "nccl" else None
+    barrier()
+    t1 = time.perf_counter() if world > 1 else t1
+    if comm is not None:
+        allreduce_or_native(bf, comm)  # rpt_bf_allreduce_or (C-ABI), the product merge
+    elif world > 1:
+        allreduce_or_filter(bf)  # gloo rehearsal
     torch.cuda.synchronize()
     t2 = time.perf_counter()
     bf.finalized = True
     merge_check = None
-    if world > 1:
-        # untimed: the OR-merged filter must be bit-identical to a single-GPU build of all rows
+    if world > 1 and not args.no_merge_check:
+        # untimed: the OR-merged filter must be bit-identical to a single-GPU build of all rows (built
+        # here in 1e9-row pieces: inserts into one filter compose)
         ref = rpt_amd.BloomFilter(n_filter, device=device)
-        all_keys = rpt_amd.synth_build_keys(n_build, device=device)
-        ref.insert(all_keys.to(torch.int32) if args.key_type == "i32" else all_keys)
+        piece = 10**9
+        for s0 in range(0, n_build, piece):
+            ref.insert(keys_of(rpt_amd.synth_build_keys(min(piece, n_build - s0), start=s0, device=device)))
         a = torch.empty(bf.num_blocks, dtype=torch.int64, device=device)
         b = torch.empty_like(a)
         bf.copy_words_to(a)
         ref.copy_words_to(b)
-        ok = torch.tensor([1 if torch.equal(a, b) else 0], dtype=torch.int64,
-                          device=device if backend == "nccl" else "cpu")
+        same = torch.equal(a, b) and bf.minmax() == ref.minmax()
+        ok = torch.tensor([1 if same else 0], dtype=torch.int64, device=device if backend == "nccl" else "cpu")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        merge_check = "bit-identical to a single-GPU build on every rank" if ok.item() else "MISMATCH"
+        merge_check = ("bit-identical (words + key min/max) to a single-GPU build of all rows on every rank"
+                       if ok.item() else "MISMATCH")
         del ref, a, b
+        torch.cuda.empty_cache()
         if not ok.item():
             raise SystemExit("OR-merged filter differs from the single-GPU build")
     bf.probe_strategy = {"auto": 0, "gather": 1, "lds": 2, "partitioned": 3, "bucketed": 4}[args.strategy]
     strategy_name = {1: "gather", 2: "lds", 3: "partitioned", 4: "bucketed"}[bf.probe_strategy_for(n_probe)]
-    del build_keys
 
     # ---- USE_BF probe workload: this rank's slice of the global probe column --------------------
     keys = rpt_amd.synth_probe_keys(n_probe, n_build, p_permille, start=rank * n_probe, device=device)
@@ -262,18 +344,19 @@ def main():
         # dominant kernel of the step (largest total device time)
         dom_name, (dom_calls, dom_total) = max(ktimes.items(), key=lambda kv: kv[1][1])
         dom_ms = dom_total / dom_calls
-        dom_bytes = algorithmic_bytes(dom_name, n_probe, survivors, key_bytes)
+        dom_calls_per_step = dom_calls / args.steps
+        dom_bytes = algorithmic_bytes(dom_name, n_probe, survivors, key_bytes) / dom_calls_per_step
         achieved = dom_bytes / (dom_ms * 1e-3)
-        key_k = 1 if args.key_type == "i32" else 0
-        traffic = pmc_traffic(dom_name, key_k)
+        traffic = pmc_traffic(dom_name, tag)
         # whole-step HBM traffic: every kernel of the step at its PMC bytes per launch
         step_traffic, unprofiled = 0.0, []
         for name, (calls, _total) in ktimes.items():
-            t = pmc_traffic(name, key_k)
-            if t is None:
+            tr = pmc_traffic(name, tag)
+            if tr is None:
                 unprofiled.append(name)
             else:
-                step_traffic += t["bytes_per_launch"] * calls / args.steps
+                step_traffic += tr["bytes_per_launch"] * calls / args.steps
+        filter_bytes = bf.num_blocks * 8
         line = {
             "metric": "bloom probe keys/sec (whole node)",
             "value": value,
@@ -288,15 +371,16 @@ def main():
             "dtype": "int32" if args.key_type == "i32" else "int64",
             "data": "synthetic: seeded splitmix64 int64 key columns generated on device (SURVEY §8d)",
             "config": {
-                "workload": (f"{cfg}: USE_BF probe of {n_probe:.0e} {'int32' if args.key_type == 'i32' else 'int64'} keys per GPU against a blocked Bloom "
-                             f"filter built from {n_build:.0e} keys (sized for {n_filter:.0e}: "
-                             f"2^{bf.log_num_blocks} blocks = {bf.num_blocks * 8 / 2**20:.0f} MiB), p={args.p}"),
+                "workload": (f"{cfg}: USE_BF probe of {n_probe:.0e} {'int32' if args.key_type == 'i32' else 'int64'} keys "
+                             f"per GPU against a blocked Bloom filter built from {n_build:.0e} keys (sized for "
+                             f"{n_filter:.0e}: 2^{bf.log_num_blocks} blocks = {filter_bytes / 2**20:.0f} MiB), p={args.p}"),
+                "config": cfg,
                 "probe_rows_per_gpu": n_probe,
                 "build_rows": n_build,
-                "filter_bytes": bf.num_blocks * 8,
+                "filter_bytes": filter_bytes,
                 "pass_fraction": survivors / n_probe,
                 "parallelism": f"row-range shards over {world} GPU(s), filter replicated "
-                               f"({'RCCL' if backend == 'nccl' else backend + ' rehearsal'} OR-merge)",
+                               f"({'RCCL rpt_bf_allreduce_or' if comm is not None else (backend + ' rehearsal' if world > 1 else 'no')} OR-merge)",
                 "probe_strategy": strategy_name,
                 "job_geomean": "not measured: needs DuckDB v1.4.4 + job.duckdb (SURVEY §8f row 1)",
             },
@@ -310,9 +394,11 @@ def main():
                 "traffic": traffic["bytes_per_launch"] if traffic else None,
                 "traffic_source": traffic["source"] if traffic else None,
                 "avg_launch_ms": dom_ms,
+                "launches_per_step": dom_calls_per_step,
                 "algorithmic_bytes_per_launch": dom_bytes,
             },
             "kernels_ms": {k: v[1] / v[0] for k, v in sorted(ktimes.items(), key=lambda kv: -kv[1][1])},
+            "kernels_launches_per_step": {k: v[0] / args.steps for k, v in ktimes.items()},
             "probe_total": {
                 "avg_ms": probe_ms,
                 "algorithmic_bytes": probe_bytes,
@@ -328,17 +414,24 @@ def main():
                 "insert_ms": insert_s * 1e3,
                 "insert_keys_per_s": (n_build / world) / insert_s if insert_s > 0 else None,
                 "or_merge_ms": merge_s * 1e3,
+                # per-GPU xGMI bytes of the OR all-reduce: 2 (W-1)/W of the filter
+                "or_merge_GBps_per_gpu": (2 * (world - 1) / world * filter_bytes / merge_s / 1e9
+                                          if world > 1 and merge_s > 0 else None),
                 "merge_check": merge_check,
             },
         }
         if not args.no_cpu_baseline and world == 1:
             sample = int(args.cpu_sample) if args.cpu_sample else n_probe
-            cb = cpu_baseline(n_build, p_permille, sample, args.cpu_threads, args.key_type)
+            threads = args.cpu_threads or cpu_share()
+            src = "--cpu-threads" if args.cpu_threads else "this process's CPU share: affinity mask capped by the cgroup quota"
+            cb = cpu_baseline(n_build, n_filter, p_permille, sample, threads, src, args.key_type)
             if sample == n_probe:  # same rows, same filter: a full-size cross-check of the survivor count
                 cb["survivors_match_gpu"] = cb["survivors"] == survivors
             line["cpu_baseline"] = cb
         print(json.dumps(line), flush=True)
 
+    if comm is not None:
+        comm.close()
     if world > 1:
         barrier()
         dist.destroy_process_group()

@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <list>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -151,6 +152,29 @@ struct ProfScope {
     start = nullptr;
   }
 };
+
+// Profiling name of a kernel template instantiation, spelled as tools/pmc_summary.py short() spells
+// rocprofv3's kernel names ("partition_kernel<0,true,false,1,0>"), so bench.py can match the PMC
+// counters of exactly the instantiation that ran. Interned once per (instantiation, base name).
+template <typename T>
+std::string targ_str(T v) {
+  if constexpr (std::is_same_v<T, bool>) return v ? "true" : "false";
+  else return std::to_string(v);
+}
+template <auto... A>
+const char* inst_name(const char* base) {
+  static std::mutex mu;
+  static std::list<std::pair<const char*, std::string>> names;  // list: c_str() pointers stay valid
+  std::lock_guard<std::mutex> lk(mu);
+  for (const auto& e : names)
+    if (e.first == base) return e.second.c_str();
+  std::string s = base;
+  s += '<';
+  ((s += targ_str(A), s += ','), ...);
+  s.back() = '>';
+  names.emplace_back(base, std::move(s));
+  return names.back().second.c_str();
+}
 
 int num_cus(int device) {
   static std::mutex mu;
@@ -421,15 +445,19 @@ unsigned persistent_grid(int device, uint64_t n_segs) {
 template <int K, bool D>
 void launch_probe_bits_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
                          uint64_t n_segs, uint64_t* bits, uint32_t* counts) {
+  ProfScope prof(inst_name<K, D, false, rpt::kBlockThreads>("probe_bits_kernel"), s);
   hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, false>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
                      (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+  prof.end();
 }
 
 template <int K, bool D>
 void launch_probe_small_t(hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n, const uint32_t* row_sel,
                           uint32_t* out_sel, uint64_t* out_count) {
+  ProfScope prof(inst_name<K, D>("probe_small_kernel"), s);
   hipLaunchKernelGGL((rpt::probe_small_kernel<K, D>), dim3(1), dim3(rpt::kSmallThreads), 0, s, bf->words,
                      (1ULL << bf->log_num_blocks) - 1, a, n, row_sel, out_sel, out_count);
+  prof.end();
 }
 
 // Whole filter in LDS (dynamic LDS = filter bytes), 1024-thread workgroups (16 waves): as many per CU as
@@ -442,8 +470,10 @@ void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, con
   const size_t lds = 8ULL << bf->log_num_blocks;
   static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::probe_bits_kernel<K, D, true, rpt::kLdsProbeThreads>)); });
+  ProfScope prof(inst_name<K, D, true, rpt::kLdsProbeThreads>("probe_bits_kernel"), s);
   hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, true, rpt::kLdsProbeThreads>), dim3(grid), dim3(rpt::kLdsProbeThreads), lds,
                      s, bf->words, (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+  prof.end();
 }
 
 // Let `fn` use all of the CU's 160 KiB of LDS: dynamic allowance = 160 KiB - its static LDS.
@@ -468,8 +498,10 @@ void launch_partition_tm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, ui
   const size_t lds = rpt::partition_lds_bytes(slice_mask + 1, TM);
   static std::once_flag once;  // per instantiation; > 64 KiB of dynamic LDS must be opted into
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM, TM, SP>)); });
+  ProfScope prof(inst_name<K, D, MM, TM, SP>("partition_kernel"), s);
   hipLaunchKernelGGL((rpt::partition_kernel<K, D, MM, TM, SP>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n,
                      slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+  prof.end();
 }
 
 // Tiles of tm * kTileRows rows (rpt::tile_mult; the bucketed level 2 always passes tm = 1).
@@ -496,19 +528,26 @@ void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uin
 
 template <int K, bool D>
 void launch_insert_t(unsigned grid, hipStream_t s, rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n, uint64_t n_segs) {
+  ProfScope prof(inst_name<K, D>("insert_kernel"), s);
   hipLaunchKernelGGL((rpt::insert_kernel<K, D>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
                      (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bf->stats);
+  prof.end();
 }
 
 template <int K, bool D>
 void launch_bucket_count_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
                            uint32_t* counts_tm, int64_t* stats) {
-  if (rpt::KeyTraits<K>::kValues && stats != nullptr)
+  if (rpt::KeyTraits<K>::kValues && stats != nullptr) {
+    ProfScope prof(inst_name<K, D, true>("bucket_count_kernel"), s);
     hipLaunchKernelGGL((rpt::bucket_count_kernel<K, D, true>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n,
                        bucket_mask, counts_tm, stats);
-  else
+    prof.end();
+  } else {
+    ProfScope prof(inst_name<K, D, false>("bucket_count_kernel"), s);
     hipLaunchKernelGGL((rpt::bucket_count_kernel<K, D, false>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n,
                        bucket_mask, counts_tm, static_cast<int64_t*>(nullptr));
+    prof.end();
+  }
 }
 
 template <int K, bool D>
@@ -518,8 +557,10 @@ void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a
   const size_t lds = rpt::kL1TileRows * (RPT_SCATTER_FLAT_COPY ? 7 : 5);
   static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into (160 KiB minus the static part)
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D>)); });
+  ProfScope prof(inst_name<K, D>("bucket_scatter_kernel"), s);
   hipLaunchKernelGGL((rpt::bucket_scatter_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, bucket_mask,
                      counts_tm, pre_tm, bbase, hash_lo, hash_hi, pos1);
+  prof.end();
 }
 
 #define RPT_DISPATCH_KD(fn, kt, dense, ...)                  \
@@ -565,27 +606,25 @@ int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool d
                       const BucketLevel1& w, int64_t* stats) {
   const uint32_t nb = bucket_count(L);
   const uint64_t t1 = ceil_div(n, rpt::kL1TileRows);
-  {
-    ProfScope prof_c("bucket_count_kernel", s);
-    RPT_DISPATCH_KD(launch_bucket_count_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm, stats);
-    prof_c.end();
-    RPT_LAUNCHED("bucket_count_kernel");
-  }
+  RPT_DISPATCH_KD(launch_bucket_count_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm, stats);
+  RPT_LAUNCHED("bucket_count_kernel");
   int st = transpose_u32(s, w.counts_tm, t1, nb, w.pre_bm);
   if (st != RPT_OK) return st;
   {
     ProfScope prof_s("bucket_scan_kernel", s);
     hipLaunchKernelGGL(rpt::bucket_scan_kernel, dim3(nb), dim3(1024), 0, s, w.pre_bm, t1, w.totals);
-    hipLaunchKernelGGL(rpt::bucket_base_kernel, dim3(1), dim3(1024), 0, s, w.totals, nb, w.bbase, w.bucket_tiles);
     prof_s.end();
+    ProfScope prof_b("bucket_base_kernel", s);
+    hipLaunchKernelGGL(rpt::bucket_base_kernel, dim3(1), dim3(1024), 0, s, w.totals, nb, w.bbase, w.bucket_tiles);
+    prof_b.end();
     RPT_LAUNCHED("bucket_scan_kernel");
   }
   st = transpose_u32(s, w.pre_bm, nb, t1, w.pre_tm);
   if (st != RPT_OK) return st;
   {
-    ProfScope prof_x("bucket_scatter_kernel", s);
     RPT_DISPATCH_KD(launch_bucket_scatter_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm,
                     w.pre_tm, w.bbase, w.hash_lo, w.hash_hi, w.pos1);
+    ProfScope prof_x("bucket_pad_kernel", s);
     hipLaunchKernelGGL(rpt::bucket_pad_kernel, dim3(nb), dim3(rpt::kBlockThreads), 0, s, w.totals, w.bbase, w.hash_lo,
                        w.hash_hi);
     prof_x.end();
@@ -651,13 +690,26 @@ int launch_hash(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, rpt
   const unsigned grid = static_cast<unsigned>(std::min<uint64_t>(ceil_div(n, rpt::kBlockThreads), 4096));
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
   hipStream_t s = as_stream(stream);
-  ProfScope prof_("hash_kernel", s);
   switch (col->key_type) {
-    case RPT_KEY_I64: hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyI64, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
-    case RPT_KEY_I32: hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyI32, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
-    default: hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyHash, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes); break;
+    case RPT_KEY_I64: {
+      ProfScope prof_(inst_name<rpt::kKeyI64, COMBINE>("hash_kernel"), s);
+      hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyI64, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes);
+      prof_.end();
+      break;
+    }
+    case RPT_KEY_I32: {
+      ProfScope prof_(inst_name<rpt::kKeyI32, COMBINE>("hash_kernel"), s);
+      hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyI32, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes);
+      prof_.end();
+      break;
+    }
+    default: {
+      ProfScope prof_(inst_name<rpt::kKeyHash, COMBINE>("hash_kernel"), s);
+      hipLaunchKernelGGL((rpt::hash_kernel<rpt::kKeyHash, COMBINE>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, a, n, out_hashes);
+      prof_.end();
+      break;
+    }
   }
-  prof_.end();
   RPT_LAUNCHED("hash_kernel");
   return RPT_OK;
 }
@@ -690,6 +742,12 @@ int rpt_bf_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows) {
   uint64_t alloc = 1;
   while (alloc < min_bits) alloc <<= 1;
   return actual_rows * 8 > alloc ? 1 : 0;
+}
+
+int rpt_bf_needs_resize_alloc(const rpt_bf* bf, uint64_t actual_rows) {
+  if (!bf) return -fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  if (actual_rows == 0) return 0;
+  return actual_rows > (64ULL << bf->log_num_blocks) / 8 ? 1 : 0;
 }
 
 size_t rpt_probe_workspace_bytes(uint64_t n_rows, int log_num_blocks) {
@@ -845,9 +903,7 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const unsigned grid = persistent_grid(bf->device, n_segs);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
-  ProfScope prof1_("insert_kernel", as_stream(stream));
   RPT_DISPATCH_KD(launch_insert_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n, n_segs);
-  prof1_.end();
   RPT_LAUNCHED("insert_kernel");
   return RPT_OK;
 }
@@ -931,14 +987,12 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
     dev_n_tiles = ws.bucket_tiles + bucket_count(L);
     grid_slices = bucket_count(L) * rpt::kBucketSlices;
   }
-  ProfScope prof_p("partition_kernel", s);
   if (p_type == rpt::kKeySplit)
     launch_partition_t<rpt::kKeySplit, true>(static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1, n_tiles,
                                              ws.recs, nullptr, ws.runs_tm, p_stats, dev_n_tiles, 1u);
   else
     RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
                     n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, p_stats, dev_n_tiles, tm);
-  prof_p.end();
   RPT_LAUNCHED("partition_kernel");
   st = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
   if (st != RPT_OK) return st;
@@ -962,10 +1016,8 @@ int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, ui
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const unsigned grid = persistent_grid(bf->device, n_segs);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
-  ProfScope prof2_("probe_bits_kernel", as_stream(stream));
   RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n,
                   n_segs, out_bits, static_cast<uint32_t*>(nullptr));
-  prof2_.end();
   RPT_LAUNCHED("probe_bits_kernel");
   return RPT_OK;
 }
@@ -1000,9 +1052,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
   const bool dense = dense_ok(col, row_sel);
   if (strategy == RPT_PROBE_GATHER) {
     const unsigned grid = persistent_grid(bf->device, n_segs);
-    ProfScope prof3_("probe_bits_kernel", s);
     RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
-    prof3_.end();
     RPT_LAUNCHED("probe_bits_kernel");
   } else if (strategy == RPT_PROBE_LDS) {
     const uint64_t lds = (8ULL << L) + 8ULL * rpt::kNumMasks;
@@ -1010,9 +1060,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     const uint64_t waves = rpt::kLdsProbeThreads / 64;  // launch_probe_bits_lds_t
     const unsigned grid = static_cast<unsigned>(
         std::max<uint64_t>(1, std::min(ceil_div(n_segs, waves), num_cus(bf->device) * per_cu)));
-    ProfScope prof4_("probe_bits_kernel<lds>", s);
     RPT_DISPATCH_KD(launch_probe_bits_lds_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
-    prof4_.end();
     RPT_LAUNCHED("probe_bits_kernel<lds>");
   } else {
     // PARTITIONED: the key column, tiles of slice_count(L) slices. BUCKETED: level 1 first, then the
@@ -1047,14 +1095,12 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
       part_counts = nullptr;
     }
     const int cus = num_cus(bf->device);
-    ProfScope prof5_("partition_kernel", s);
     if (p_type == rpt::kKeySplit)
       launch_partition_t<rpt::kKeySplit, true>(static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1, n_tiles,
                                                ws.recs, ws.pos, ws.runs_tm, nullptr, dev_n_tiles, 1u);
     else
       RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
                       n_tiles, ws.recs, ws.pos, ws.runs_tm, static_cast<int64_t*>(nullptr), dev_n_tiles, tm);
-    prof5_.end();
     RPT_LAUNCHED("partition_kernel");
     int st2 = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
     if (st2 != RPT_OK) return st2;
@@ -1084,14 +1130,16 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
                          dim3(rpt::kTileCountThreads), 0, s, ws.passb, ws.runs_tm, tile_slices, n_tiles, cap, tile_counts);
       prof7a_.end();
       RPT_LAUNCHED("tile_count_kernel");
-      ProfScope prof7b_("group_scan_kernel", s);
+      ProfScope prof7b_("tile_block_scan_kernel", s);
       hipLaunchKernelGGL(rpt::tile_block_scan_kernel, dim3(static_cast<unsigned>(n_blocks)), dim3(rpt::kTileBlock), 0, s,
                          tile_counts, n_tiles, block_sums);
+      prof7b_.end();
+      ProfScope prof7d_("group_scan_kernel", s);
       hipLaunchKernelGGL(rpt::group_scan_kernel, dim3(1), dim3(1024), 0, s, block_sums, static_cast<uint32_t>(n_blocks),
                          block_offs, out_count_dev);
-      prof7b_.end();
+      prof7d_.end();
       RPT_LAUNCHED("group_scan_kernel");
-      ProfScope prof7c_("unpermute_sel_kernel", s);
+      ProfScope prof7c_(tm == 2 ? "unpermute_sel_kernel<2>" : "unpermute_sel_kernel<1>", s);
       if (tm == 2)
         hipLaunchKernelGGL(rpt::unpermute_sel_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteSelThreads<2>),
                            cap / 8, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
@@ -1103,7 +1151,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
       *done = true;
       return RPT_OK;
     }
-    ProfScope prof7_("unpermute_kernel", s);
+    ProfScope prof7_(tm == 2 ? "unpermute_kernel<2>" : "unpermute_kernel<1>", s);
     if (tm == 2)
       hipLaunchKernelGGL(rpt::unpermute_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8,
                          s, ws.pos, ws.passb, n_part, cap, part_bits, part_counts, dev_n_tiles);
@@ -1185,10 +1233,8 @@ int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* ro
     if (!out_sel) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_sel");
     hipStream_t s = as_stream(stream);
     const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, row_sel};
-    ProfScope prof_("probe_small_kernel", s);
     RPT_DISPATCH_KD(launch_probe_small_t, col->key_type, dense_ok(col, row_sel), s, bf, a, n, row_sel, out_sel,
                     out_count_dev);
-    prof_.end();
     RPT_LAUNCHED("probe_small_kernel");
     return RPT_OK;
   }
@@ -1250,7 +1296,13 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
 namespace {
 // The RCCL entry points rpt_bf_allreduce_or uses, resolved from librccl on first use (rccl.h types:
 // ncclResult_t = int, ncclComm_t = opaque pointer, ncclDataType_t / ncclRedOp_t = int enums).
+struct RcclUniqueId {
+  char internal[RPT_RCCL_UNIQUE_ID_BYTES];  // rccl.h ncclUniqueId (passed by value to ncclCommInitRank)
+};
 struct RcclApi {
+  int (*get_unique_id)(RcclUniqueId*) = nullptr;
+  int (*comm_init_rank)(void**, int, RcclUniqueId, int) = nullptr;
+  int (*comm_destroy)(void*) = nullptr;
   int (*group_start)() = nullptr;
   int (*group_end)() = nullptr;
   int (*send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
@@ -1276,6 +1328,9 @@ const RcclApi& rccl_api() {
       fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
       if (!fn && a.load_error.empty()) a.load_error = std::string("librccl lacks ") + name;
     };
+    sym(a.get_unique_id, "ncclGetUniqueId");
+    sym(a.comm_init_rank, "ncclCommInitRank");
+    sym(a.comm_destroy, "ncclCommDestroy");
     sym(a.group_start, "ncclGroupStart");
     sym(a.group_end, "ncclGroupEnd");
     sym(a.send, "ncclSend");
@@ -1308,6 +1363,15 @@ extern "C" {
     const int rc_ = (call);                                                                    \
     if (rc_ != 0) return fail(RPT_ERR_COLLECTIVE, "%s: %s", #call, api.error_string(rc_));      \
   } while (0)
+// inside ncclGroupStart/End: close the group before returning, so the caller's RCCL state stays usable
+#define RPT_NCCL_IN_GROUP(call)                                                                 \
+  do {                                                                                         \
+    const int rc_ = (call);                                                                    \
+    if (rc_ != 0) {                                                                            \
+      (void)api.group_end();                                                                   \
+      return fail(RPT_ERR_COLLECTIVE, "%s: %s", #call, api.error_string(rc_));                 \
+    }                                                                                          \
+  } while (0)
 
 int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
   if (!bf || !nccl_comm) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
@@ -1335,8 +1399,8 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
       RPT_NCCL(api.group_start());
       for (int p = 0, k = 0; p < world; p++) {
         if (p == me) continue;
-        RPT_NCCL(api.send(bf->words + lo(p), lo(p + 1) - lo(p), kNcclUint64, p, nccl_comm, s));
-        RPT_NCCL(api.recv(tmp + static_cast<uint64_t>(k++) * mine, mine, kNcclUint64, p, nccl_comm, s));
+        RPT_NCCL_IN_GROUP(api.send(bf->words + lo(p), lo(p + 1) - lo(p), kNcclUint64, p, nccl_comm, s));
+        RPT_NCCL_IN_GROUP(api.recv(tmp + static_cast<uint64_t>(k++) * mine, mine, kNcclUint64, p, nccl_comm, s));
       }
       RPT_NCCL(api.group_end());
       if (mine > 0) {
@@ -1349,8 +1413,8 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
       RPT_NCCL(api.group_start());
       for (int p = 0; p < world; p++) {
         if (p == me) continue;
-        RPT_NCCL(api.send(bf->words + lo(me), mine, kNcclUint64, p, nccl_comm, s));
-        RPT_NCCL(api.recv(bf->words + lo(p), lo(p + 1) - lo(p), kNcclUint64, p, nccl_comm, s));
+        RPT_NCCL_IN_GROUP(api.send(bf->words + lo(me), mine, kNcclUint64, p, nccl_comm, s));
+        RPT_NCCL_IN_GROUP(api.recv(bf->words + lo(p), lo(p + 1) - lo(p), kNcclUint64, p, nccl_comm, s));
       }
       RPT_NCCL(api.group_end());
     }
@@ -1374,6 +1438,39 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
   }
   return st;
 }
+
+int rpt_rccl_get_unique_id(uint8_t* out_id) {
+  if (!out_id) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  const RcclApi& api = rccl_api();
+  if (!api.load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api.load_error.c_str());
+  RcclUniqueId id{};
+  RPT_NCCL(api.get_unique_id(&id));
+  std::memcpy(out_id, id.internal, RPT_RCCL_UNIQUE_ID_BYTES);
+  return RPT_OK;
+}
+
+int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, void** out_comm) {
+  if (!id || !out_comm || world < 1 || rank < 0 || rank >= world)
+    return fail(RPT_ERR_INVALID_ARGUMENT, "bad communicator arguments (world %d, rank %d)", world, rank);
+  const RcclApi& api = rccl_api();
+  if (!api.load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api.load_error.c_str());
+  RPT_ON_DEVICE(device);
+  RcclUniqueId uid{};
+  std::memcpy(uid.internal, id, RPT_RCCL_UNIQUE_ID_BYTES);
+  void* comm = nullptr;
+  RPT_NCCL(api.comm_init_rank(&comm, world, uid, rank));
+  *out_comm = comm;
+  return RPT_OK;
+}
+
+int rpt_rccl_comm_destroy(void* comm) {
+  if (!comm) return RPT_OK;
+  const RcclApi& api = rccl_api();
+  if (!api.load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api.load_error.c_str());
+  RPT_NCCL(api.comm_destroy(comm));
+  return RPT_OK;
+}
+#undef RPT_NCCL_IN_GROUP
 #undef RPT_NCCL
 
 int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out) {

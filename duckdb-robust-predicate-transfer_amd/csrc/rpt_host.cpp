@@ -677,6 +677,12 @@ uint64_t PTBloomFilter::SizedForRows() const {
   return i.sized_for_rows;
 }
 
+bool PTBloomFilter::NeedsResize(uint64_t actual_rows) const {
+  const int r = rpt_bf_needs_resize_alloc(bf_, actual_rows);
+  if (r < 0) check(-r);
+  return r == 1;
+}
+
 bool PTBloomFilter::IsEmpty() const {
   rpt_bf_info i;
   check(rpt_bf_get_info(bf_, &i));
@@ -788,9 +794,10 @@ void CreateBF::Finalize() {
     DeviceContext ctx(device_);
     for (size_t i = 0; i < filters_.size(); i++) {
       auto& bf = *filters_[i];
-      // physical_create_bf.cpp:394-398: resize iff actual*8 > NextPow2(max(512, sized_for*12)); the
-      // rehash reads the build column from HBM
-      if (rpt_bf_needs_resize(bf.SizedForRows(), actual_rows)) {
+      // physical_create_bf.cpp:383-398: resize iff the allocated filter gives < 8 bits per actual row
+      // (evaluated on this filter's real allocation, rpt_bf_needs_resize_alloc); the rehash reads the
+      // build column from HBM
+      if (bf.NeedsResize(actual_rows)) {
         bf.ReinitializeAndRehash(ctx, actual_rows, all_keys_[i]);
         resized_[i] = true;
       }

@@ -81,6 +81,7 @@ SIGNATURES = {
     "rpt_last_error": (c_char_p, []),
     "rpt_bf_log_num_blocks_for_rows": (c_int, [c_uint64]),
     "rpt_bf_needs_resize": (c_int, [c_uint64, c_uint64]),
+    "rpt_bf_needs_resize_alloc": (c_int, [c_void_p, c_uint64]),
     "rpt_probe_workspace_bytes": (c_size_t, [c_uint64, c_int]),
     "rpt_bf_set_probe_strategy": (c_int, [c_void_p, c_int]),
     "rpt_probe_strategy_supported": (c_int, [c_int, c_int]),
@@ -118,6 +119,9 @@ SIGNATURES = {
     "rpt_hash_combine": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_bf_merge_or": (c_int, [c_void_p, c_void_p, c_void_p]),
     "rpt_bf_allreduce_or": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "rpt_rccl_get_unique_id": (c_int, [c_void_p]),
+    "rpt_rccl_comm_init_rank": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),
+    "rpt_rccl_comm_destroy": (c_int, [c_void_p]),
     "rpt_words_or": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_words_or_slices": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p]),
     "rpt_bf_count_bits": (c_int, [c_void_p, POINTER(c_uint64)]),

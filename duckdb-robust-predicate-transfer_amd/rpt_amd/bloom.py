@@ -188,6 +188,14 @@ class BloomFilter:
             check(-v)
         return v
 
+    def needs_resize(self, actual_rows: int) -> bool:
+        """CREATE_BF Finalize's resize predicate on this filter's real allocation: fewer than 8 allocated
+        bits per actual row (physical_create_bf.cpp:383; rpt_bf_needs_resize_alloc)."""
+        v = self._lib.rpt_bf_needs_resize_alloc(self._h, int(actual_rows))
+        if v < 0:
+            check(-v)
+        return bool(v)
+
     def set_has_data(self, v: bool) -> None:
         check(self._lib.rpt_bf_set_has_data(self._h, int(bool(v))))
 

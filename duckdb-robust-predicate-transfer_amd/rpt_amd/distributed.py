@@ -15,10 +15,17 @@ MI355X-native scale-out of PhysicalCreateBF's parallel sink (physical_create_bf.
   * the probe is sharded by row range with a replicated filter: each rank's ascending local sel plus
     its row offset, concatenated in rank order, is the global ascending sel — no exchange.
 
-`or_slices` is injectable so the collective choreography runs on CPU (gloo) in tests.
+Two implementations of the OR all-reduce:
+  * `RcclComm` + `allreduce_or_native`: the product path. librpt_gpu.so's `rpt_bf_allreduce_or`
+    (grouped ncclSend/ncclRecv reduce-scatter by OR + all-gather, in place on the filter words) over a
+    communicator the library creates (`rpt_rccl_comm_init_rank`, unique id broadcast over the
+    torch.distributed group). This is what a C++ / DuckDB caller gets; bench.py uses it on GPUs.
+  * `allreduce_or_filter`: the same choreography in torch.distributed collectives, used to rehearse
+    the multi-rank path on CPU (gloo); `or_slices` is injectable so it runs without a GPU in tests.
 """
 from __future__ import annotations
 
+import ctypes
 import functools
 from typing import Callable, Optional
 
@@ -61,6 +68,53 @@ def or_allreduce_words(full: torch.Tensor, group=None, or_slices: Optional[OrSli
     mine = torch.empty(slice_words, dtype=full.dtype, device=full.device)
     or_slices(mine, recv, world, slice_words)
     dist.all_gather_into_tensor(full, mine, group=group)
+
+
+class RcclComm:
+    """An RCCL communicator created by librpt_gpu.so for the ranks of a torch.distributed group (one GPU
+    per rank): rank 0 draws the unique id (rpt_rccl_get_unique_id), the group broadcasts it, every rank
+    joins with rpt_rccl_comm_init_rank. Pass `.handle` to rpt_bf_allreduce_or (allreduce_or_native)."""
+
+    ID_BYTES = 128  # RPT_RCCL_UNIQUE_ID_BYTES
+
+    def __init__(self, device: torch.device, group=None):
+        from ._lib import check, load
+
+        self._lib = load()
+        self.device = torch.device(device)
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        uid = torch.zeros(self.ID_BYTES, dtype=torch.uint8)
+        if self.rank == 0:
+            check(self._lib.rpt_rccl_get_unique_id(uid.data_ptr()))
+        on_device = dist.get_backend(group) != "gloo"
+        t = uid.to(self.device) if on_device else uid
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = t.cpu().contiguous()
+        h = ctypes.c_void_p()
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        check(self._lib.rpt_rccl_comm_init_rank(dev, self.world, uid.data_ptr(), self.rank, ctypes.byref(h)))
+        self.handle = h
+
+    def close(self) -> None:
+        if self.handle is not None and self.handle.value:
+            self._lib.rpt_rccl_comm_destroy(self.handle)
+        self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def allreduce_or_native(bf, comm: RcclComm, stream=None) -> None:
+    """CREATE_BF Combine across GPUs through the C-ABI (rpt_bf_allreduce_or): words OR-merged in place,
+    key min/max and has_data reduced; returns once has_data is known (one stream sync)."""
+    from ._lib import check
+    from .bloom import _stream
+
+    check(bf._lib.rpt_bf_allreduce_or(bf.handle, comm.handle, _stream(bf.device, stream)))
 
 
 def allreduce_or_filter(bf, group=None) -> None:

@@ -111,6 +111,13 @@ int rpt_bf_log_num_blocks_for_rows(uint64_t n_rows);
 /* PhysicalCreateBF::Finalize resize rule, verbatim (physical_create_bf.cpp:394-398):
  * 1 iff actual_rows > 0 and actual_rows*8 > NextPow2(max(512, sized_for_rows*12)). */
 int rpt_bf_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows);
+/* The resize predicate CREATE_BF's Finalize applies here: the reference's stated intent ("resize iff
+ * allocated_bits / actual_rows < 8", physical_create_bf.cpp:383) evaluated on the filter actually
+ * allocated (64 * 2^log_num_blocks bits, Arrow sizing at 8 bits per estimated row): 1 iff
+ * actual_rows * 8 > 64 << log_num_blocks. The verbatim rule above assumes DuckDB's native 12-bit
+ * allocation and would leave an Arrow-sized filter at 4 bits per key (sized_for 1000, actual 2048);
+ * DESIGN.md §2. Negative rpt_status on error. */
+int rpt_bf_needs_resize_alloc(const rpt_bf* bf, uint64_t actual_rows);
 /* Device workspace a probe of n rows against a 2^log_num_blocks-block filter needs, for any
  * strategy (bytes, 256-aligned). rpt_bf_probe_workspace_bytes: for the strategy a probe of n rows
  * of this filter runs now (AUTO resolved), usually far less for very large filters. */
@@ -225,6 +232,15 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream);
  * known (one stream sync). librccl is loaded on first use (dlopen), so the library itself does not
  * depend on it. */
 int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream);
+/* RCCL communicator for callers that bring none (bench.py, tests; a DuckDB shim that owns an
+ * ncclComm_t passes it to rpt_bf_allreduce_or directly). Rank 0 calls rpt_rccl_get_unique_id, the
+ * caller broadcasts the RPT_RCCL_UNIQUE_ID_BYTES bytes out of band (torch.distributed, MPI, a file),
+ * then every rank calls rpt_rccl_comm_init_rank for its own GPU (collective; blocks until all ranks
+ * joined) — ncclGetUniqueId / ncclCommInitRank / ncclCommDestroy of the dlopened librccl. */
+#define RPT_RCCL_UNIQUE_ID_BYTES 128
+int rpt_rccl_get_unique_id(uint8_t* out_id);
+int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, void** out_comm);
+int rpt_rccl_comm_destroy(void* comm);
 /* dst[i] |= src[i] for n_words words (device pointers): the local step of the multi-GPU
  * OR all-reduce (reduce-scatter slices). */
 int rpt_words_or(uint64_t* dst, const uint64_t* src, uint64_t n_words, rpt_stream_t stream);

@@ -157,6 +157,8 @@ class PTBloomFilter {
   void ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const DeviceKeyColumn& keys);
 
   uint64_t SizedForRows() const;
+  // Finalize's resize predicate on this filter's real allocation (rpt_bf_needs_resize_alloc)
+  bool NeedsResize(uint64_t actual_rows) const;
   bool IsEmpty() const;
   int LogNumBlocks() const;
   // Min/max of the valid I32/I64 keys inserted (the min/max dynamic filter; false: none yet).

@@ -232,6 +232,16 @@ int rpt_oracle_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows) {
   return actual_rows * 8 > alloc ? 1 : 0;
 }
 
+// The same predicate against the filter actually allocated (the reference's stated intent,
+// physical_create_bf.cpp:383: "resize iff allocated_bits / actual_rows < 8"): the filter holds
+// 64 * 2^log_num_blocks bits (Arrow sizing, 8 bits per estimated row), so resize iff
+// actual * 8 > 64 << log_num_blocks.
+int rpt_oracle_needs_resize_alloc(int log_num_blocks, uint64_t actual_rows) {
+  if (actual_rows == 0) return 0;
+  const uint64_t alloc_bits = 64ULL << log_num_blocks;
+  return actual_rows > alloc_bits / 8 ? 1 : 0;
+}
+
 uint64_t rpt_oracle_murmur64(uint64_t x) { return murmur64(x); }
 uint64_t rpt_oracle_null_hash(void) { return kNullHash; }
 

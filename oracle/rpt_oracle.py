@@ -22,6 +22,7 @@ _SIG = {
     "rpt_oracle_mask_of_hash": (c_uint64, [c_uint64]),
     "rpt_oracle_log_num_blocks": (c_int, [c_uint64]),
     "rpt_oracle_needs_resize": (c_int, [c_uint64, c_uint64]),
+    "rpt_oracle_needs_resize_alloc": (c_int, [c_int, c_uint64]),
     "rpt_oracle_murmur64": (c_uint64, [c_uint64]),
     "rpt_oracle_null_hash": (c_uint64, []),
     "rpt_oracle_hash_i64": (None, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p]),
@@ -83,6 +84,11 @@ def log_num_blocks(n: int) -> int:
 
 def needs_resize(sized_for: int, actual: int) -> bool:
     return bool(lib().rpt_oracle_needs_resize(sized_for, actual))
+
+
+def needs_resize_alloc(log_num_blocks: int, actual: int) -> bool:
+    """Resize iff the ALLOCATED filter (2^log_num_blocks blocks) gives fewer than 8 bits per actual row."""
+    return bool(lib().rpt_oracle_needs_resize_alloc(log_num_blocks, actual))
 
 
 def hash_keys(keys: np.ndarray, key_sel=None, validity=None) -> np.ndarray:

@@ -151,3 +151,43 @@ def test_bucketed_skewed_keys(rpt):
     probe = np.concatenate([keys, base])
     sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
     assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
+
+
+def test_c5_geometry_8gib_filter_vs_oracle(rpt):
+    """BASELINE C5's single-rank geometry: a filter sized for 8e9 rows = 2^30 blocks
+    (8 GiB), 512 level-1 buckets of 128 slices. Bucketed insert of 1.2e7 keys and bucketed probes of
+    1.2e7 rows (flat, with a NULL pattern, through a row selection), each against the oracle: every word
+    of the 8 GiB filter and every sel entry."""
+    log_nb = 30
+    bf = rpt.BloomFilter(8 * 10**9)
+    assert bf.log_num_blocks == log_nb
+    n_build, n_probe = 12_000_000, 12_000_000
+    build = orc.synth_build_keys(n_build, start=3 * 10**9)
+    bf.insert(dev(build), strategy=INS_BUCKETED)
+    w = oracle_filter(log_nb, build)
+    got = torch.empty(bf.num_blocks, dtype=torch.int64, device="cuda:0")
+    bf.copy_words_to(got)
+    ref_words = torch.from_numpy(w.view(np.int64)).to("cuda:0")
+    assert torch.equal(got, ref_words), "8 GiB filter words differ from the oracle"
+    del got, ref_words
+    torch.cuda.empty_cache()
+    assert bf.minmax() == orc.minmax(build)
+
+    probe = orc.synth_probe_keys(n_probe, n_build, 100, start=5 * 10**8)
+    probe[::7] = build[: probe[::7].size]  # more hits than p = 0.1
+    bf.probe_strategy = BUCKETED
+    assert bf.probe_strategy_for(n_probe) == BUCKETED
+    dprobe = dev(probe)
+    ref = orc.probe_keys(w, log_nb, probe)
+    assert ref.size > n_probe // 7
+    assert np.array_equal(bf.lookup_sel(dprobe).cpu().numpy().astype(np.uint32), ref)
+    rng = np.random.default_rng(30)
+    valid = rng.random(n_probe) > 0.01
+    vw = gu.validity_words(valid)
+    ref_n = orc.probe_keys(w, log_nb, probe, validity=vw)
+    sel_n = bf.lookup_sel(dprobe, validity=dev(vw)).cpu().numpy().astype(np.uint32)
+    assert np.array_equal(sel_n, ref_n)
+    row_sel = np.sort(rng.choice(n_probe, size=n_probe // 3, replace=False)).astype(np.uint32)
+    ref_r = row_sel[orc.probe_keys(w, log_nb, probe, key_sel=row_sel)]
+    sel_r = bf.lookup_sel(dprobe, row_sel=dev(row_sel)).cpu().numpy().astype(np.uint32)
+    assert np.array_equal(sel_r, ref_r)

@@ -1,4 +1,6 @@
 """HIP path (librpt_gpu.so on cuda:0) vs the oracle and the Arrow golden vectors. Bit-exact."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -286,13 +288,27 @@ def test_reinitialize_and_rehash_resize_rule(rpt):
     chunks = [dict(keys=dev(keys[i:i + 2048])) for i in range(0, actual, 2048)]
     for ch in chunks:
         bf.insert(**ch)
-    assert rpt.needs_resize(bf.sized_for_rows(), actual)
+    assert rpt.needs_resize(bf.sized_for_rows(), actual) and bf.needs_resize(actual)
     bf.reinitialize_and_rehash(actual, chunks)
     assert bf.sized_for_rows() == actual and bf.log_num_blocks == orc.log_num_blocks(actual)
     lnb = orc.log_num_blocks(actual)
     w = orc.new_words(lnb)
     orc.insert_keys(w, lnb, keys)
     assert np.array_equal(bf.export_words(), w)
+
+
+def test_resize_predicate_on_allocation_matches_oracle(rpt):
+    """Finalize's resize rule on the real allocation (rpt_bf_needs_resize_alloc) == the oracle's, at the
+    sized_for = 1000 boundary (1024 / 1025 / 2048 actual rows) and over random estimates."""
+    bf = rpt.BloomFilter(1000)
+    assert bf.log_num_blocks == 7
+    assert [bf.needs_resize(a) for a in (0, 1024, 1025, 2048)] == [False, False, True, True]
+    rng = np.random.default_rng(5)
+    for est in [0, 1, 63, 64, 65, 1000, 4096, 10**5, int(rng.integers(1, 10**6))]:
+        f = rpt.BloomFilter(est)
+        for a in [0, 1, est, est * 2, (64 << f.log_num_blocks) // 8, (64 << f.log_num_blocks) // 8 + 1,
+                  int(rng.integers(0, 10**7))]:
+            assert f.needs_resize(a) == orc.needs_resize_alloc(f.log_num_blocks, a), (est, a)
 
 
 def test_synthetic_generators_match_oracle(rpt):
@@ -310,11 +326,36 @@ def _window_check(bf, w, lnb, probe_dev, sel, lo, hi):
     assert np.array_equal(sel[a:b], exp)
 
 
+def _full_check(w, lnb, probe_dev, sel, piece=10**8):
+    """Every row of the probe against the oracle: the column is copied back in `piece`-row slices and
+    each slice's expected survivors (oracle LookupSel + slice offset) must equal the sel entries that
+    fall inside it. Slices are probed on host threads (ctypes releases the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    n = probe_dev.numel()
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+
+    def one(lo_keys):
+        lo, keys = lo_keys
+        return lo, orc.probe_keys(w, lnb, keys).astype(np.int64) + lo
+
+    jobs = ((lo, probe_dev[lo:min(lo + piece, n)].cpu().numpy()) for lo in range(0, n, piece))
+    checked = 0
+    with ThreadPoolExecutor(threads) as ex:
+        for lo, exp in ex.map(one, jobs):
+            hi = min(lo + piece, n)
+            a, b = np.searchsorted(sel, lo), np.searchsorted(sel, hi)
+            assert np.array_equal(sel[a:b], exp), f"rows [{lo}, {hi}) differ from the oracle"
+            checked += b - a
+    assert checked == sel.size
+
+
 @pytest.mark.parametrize("n_probe,n_build,p,strategy", [(10**8, 10**7, 100, "gather"),
                                                          (10**8, 10**7, 1000, "partitioned"),
                                                          (10**9, 10**7, 100, "partitioned")])
 def test_full_size_probe_properties(rpt, n_probe, n_build, p, strategy):
-    """BASELINE sizes: sortedness, count == popcount(find bits), windows vs oracle, no false negatives."""
+    """BASELINE sizes (C2 at 1e9 rows): EVERY row's result against the oracle (1e8-row slices on host
+    threads), sortedness, count == popcount(find bits), no false negatives."""
     build = rpt.synth_build_keys(n_build)
     bf = with_strategy(rpt.BloomFilter(n_build), strategy)
     bf.insert(build)
@@ -334,8 +375,7 @@ def test_full_size_probe_properties(rpt, n_probe, n_build, p, strategy):
     sel = sel_t[:count]  # int32: n_probe < 2^31
     assert bool((sel[1:] > sel[:-1]).all())
     sel_np = sel.cpu().numpy().astype(np.int64)
-    for lo, hi in [(0, 10**6), (n_probe // 2 - 777, n_probe // 2 + 10**6), (n_probe - 10**6, n_probe)]:
-        _window_check(bf, w, lnb, probe, sel_np, lo, hi)
+    _full_check(w, lnb, probe, sel_np)
     rate = count / n_probe
     assert p / 1000 <= rate < p / 1000 + 0.05
     del probe, sel_t, bits, sel

@@ -1,8 +1,15 @@
-"""rpt_bf_allreduce_or (the native RCCL OR all-reduce for C++ callers) on a single-rank RCCL
-communicator: librccl loads, the collective runs, and the filter words, key min/max and has_data come
-back unchanged. World sizes > 1 need one GPU per rank (RCCL refuses two ranks on one device); the
-Python/torch.distributed merge that bench.py uses is covered at world sizes 2-4 with gloo."""
+"""rpt_bf_allreduce_or (the native RCCL OR all-reduce: the product merge, used by bench.py and by C++
+callers) over a communicator from rpt_rccl_comm_init_rank.
+
+* one rank: librccl loads, the collective runs, and the filter words, key min/max and has_data come
+  back unchanged (also with a communicator the caller created itself through librccl);
+* two ranks, one GPU each (skipped on a one-GPU box: RCCL refuses two ranks on one device): every
+  rank inserts its row-range shard, the merged filter equals the oracle's filter of all rows, and the
+  key min/max / has_data are reduced (an empty rank included). The torch.distributed composition used
+  for gloo rehearsals is covered at world sizes 2-4 in tests/test_distributed_gloo.py."""
 import ctypes
+import os
+import tempfile
 
 import numpy as np
 import pytest
@@ -17,18 +24,28 @@ class _UniqueId(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]  # rccl.h NCCL_UNIQUE_ID_BYTES
 
 
-@pytest.fixture(scope="module")
-def comm():
+@pytest.fixture(scope="module", params=["library", "caller"])
+def comm(request):
     if not torch.cuda.is_available():
         pytest.fail("gpu test run without a visible GPU")
     torch.cuda.set_device(0)
-    rccl = ctypes.CDLL("librccl.so.1")
-    uid = _UniqueId()
-    assert rccl.ncclGetUniqueId(ctypes.byref(uid)) == 0
+    from rpt_amd import _lib
+
+    lib = _lib.load()
     c = ctypes.c_void_p()
-    assert rccl.ncclCommInitRank(ctypes.byref(c), 1, uid, 0) == 0
-    yield c
-    rccl.ncclCommDestroy(c)
+    if request.param == "library":  # rpt_rccl_get_unique_id + rpt_rccl_comm_init_rank
+        uid = (ctypes.c_uint8 * 128)()
+        assert lib.rpt_rccl_get_unique_id(uid) == 0, lib.rpt_last_error()
+        assert lib.rpt_rccl_comm_init_rank(0, 1, uid, 0, ctypes.byref(c)) == 0, lib.rpt_last_error()
+        yield c
+        assert lib.rpt_rccl_comm_destroy(c) == 0
+    else:  # a communicator the caller made itself (a DuckDB shim that owns one)
+        rccl = ctypes.CDLL("librccl.so.1")
+        uid = _UniqueId()
+        assert rccl.ncclGetUniqueId(ctypes.byref(uid)) == 0
+        assert rccl.ncclCommInitRank(ctypes.byref(c), 1, uid, 0) == 0
+        yield c
+        rccl.ncclCommDestroy(c)
 
 
 @pytest.fixture(scope="module")
@@ -57,3 +74,52 @@ def test_single_rank_allreduce_is_identity(rpt, comm, n_keys):
     assert (not bf.is_empty()) == before_has
     if n_keys:
         assert before_mm == (int(keys.view(np.int64).min()), int(keys.view(np.int64).max()))
+
+
+def _two_rank_worker(rank, world, store_path, n_build, empty_rank, q):
+    import torch.distributed as dist
+
+    try:
+        torch.cuda.set_device(rank)
+        dist.init_process_group("gloo", init_method=f"file://{store_path}", rank=rank, world_size=world)
+        import rpt_amd
+        from rpt_amd.distributed import RcclComm, allreduce_or_native, shard_range
+
+        comm = RcclComm(torch.device("cuda", rank))
+        lo, hi = shard_range(n_build, rank, world)
+        bf = rpt_amd.BloomFilter(n_build, device=f"cuda:{rank}")
+        if rank != empty_rank:
+            bf.insert(rpt_amd.synth_build_keys(hi - lo, start=lo, device=f"cuda:{rank}"))
+        allreduce_or_native(bf, comm)
+        lnb = bf.log_num_blocks
+        ref = orc.new_words(lnb)
+        keys = orc.synth_build_keys(n_build)
+        if empty_rank >= 0:
+            elo, ehi = shard_range(n_build, empty_rank, world)
+            keys = np.concatenate([keys[:elo], keys[ehi:]])
+        orc.insert_keys(ref, lnb, keys)
+        ok = np.array_equal(bf.export_words(), ref) and bf.minmax() == orc.minmax(keys) and not bf.is_empty()
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, bool(ok), ""))
+    except Exception as e:  # reported to the parent
+        q.put((rank, False, repr(e)))
+
+
+@pytest.mark.parametrize("n_build,empty_rank", [(3_000_000, -1), (100_001, 1)])
+def test_two_rank_allreduce_matches_single_build(n_build, empty_rank):
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL allows one rank per device)")
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    with tempfile.TemporaryDirectory() as d:
+        store = os.path.join(d, "store")
+        procs = [ctx.Process(target=_two_rank_worker, args=(r, 2, store, n_build, empty_rank, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=180) for _ in procs]
+        for p in procs:
+            p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
