@@ -17,3 +17,4 @@ for ctr in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAIT_ANY SQ_
   timeout -k 10 240 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$OUT/pmc/p$i" -o run -- python3 bench.py $BENCH_ARGS > "$OUT/pmc/p$i.log" 2>&1 || { echo "pmc pass $i failed"; exit 1; }
 done
 python3 tools/pmc_summary.py "$OUT/pmc" "$OUT/trace/bench_kernel_stats.csv" "profiles/pmc/$CFG.json" "$TAG"
+cp "profiles/pmc/$CFG.json" "$OUT/pmc_summary.json"  # gpurun merges back only gpurun_out/
