@@ -31,7 +31,7 @@ __global__ __launch_bounds__(kTileThreads) void bucket_count_kernel(KeyArgs a, u
     uint64_t hh[8];
     bool oo[8];
     int64_t mm[2] = {kMinInit, kMaxInit};
-    load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
+    load_hashes<K, DENSE, MM, RPT_NT_KEY_LOADS>(a, tile_base + seg_local, n, lane, hh, oo, mm);
     if constexpr (MM && KeyTraits<K>::kValues) {
       wave_minmax(mm[0], mm[1]);
       wmn = min(wmn, mm[0]);

@@ -79,6 +79,22 @@ constexpr int kLdsProbeThreads = 1024;                 // whole-filter LDS probe
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Streamed-once loads, non-temporal where it measured faster (C2 / C5 A/B, tools/ab_cfgs.sh):
+// key columns in the 16 Ki-row partition and the bucketed level-1 count (partition 2.27 -> 2.16 ms,
+// bucket count 1.28 -> 1.20 ms per 1e9 keys); NOT in the 32 Ki-row partition (2.62 -> 3.07 ms) nor for
+// the routing intermediates (slice probe records: 0.93 -> 1.20 ms).
+#ifndef RPT_NT_KEY_LOADS
+#define RPT_NT_KEY_LOADS 1
+#endif
+#ifndef RPT_NT_REC_LOADS
+#define RPT_NT_REC_LOADS 0
+#endif
+template <bool NT, typename T>
+__device__ __forceinline__ T stream_load(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 struct KeyArgs {
   const void* keys;
   const uint32_t* key_sel;
@@ -97,7 +113,7 @@ __device__ __forceinline__ bool valid_at(const uint64_t* validity, uint64_t idx)
 //  GENERAL (dictionary key_sel and/or row_sel):        row(c) = base + c*64 + lane.
 // MM: also fold the valid (non-NULL, in-range) key values into mm[0] = min, mm[1] = max (the build's
 // min/max dynamic filter, physical_create_bf.cpp:82-119, fused into the key read).
-template <int K, bool DENSE, bool MM = false>
+template <int K, bool DENSE, bool MM = false, bool NT = false>
 __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uint64_t n, uint32_t lane,
                                             uint64_t (&h)[8], bool (&ok)[8], int64_t* mm = nullptr) {
   using Tr = KeyTraits<K>;
@@ -115,11 +131,11 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
       T v[V];
       if (off + V <= rem) {
         if constexpr (V == 2) {
-          const u64x2 x = *reinterpret_cast<const u64x2*>(kb + off);
+          const u64x2 x = stream_load<NT>(reinterpret_cast<const u64x2*>(kb + off));
           v[0] = static_cast<T>(x[0]);
           v[1] = static_cast<T>(x[1]);
         } else {
-          const u32x4 x = *reinterpret_cast<const u32x4*>(kb + off);
+          const u32x4 x = stream_load<NT>(reinterpret_cast<const u32x4*>(kb + off));
 #pragma unroll
           for (int e = 0; e < V; e++) v[e] = static_cast<T>(x[e]);
         }

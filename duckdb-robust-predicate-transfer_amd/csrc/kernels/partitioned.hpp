@@ -146,7 +146,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
       uint64_t hh[8];
       bool oo[8];
       int64_t mm[2] = {kMinInit, kMaxInit};
-      load_hashes<K, DENSE, MM>(a, tile_base + seg_local, n, lane, hh, oo, mm);
+      load_hashes<K, DENSE, MM, TM == 1 && RPT_NT_KEY_LOADS>(a, tile_base + seg_local, n, lane, hh, oo, mm);
       if constexpr (MM && KeyTraits<K>::kValues) {
         wave_minmax(mm[0], mm[1]);
         wmn = min(wmn, mm[0]);
@@ -431,8 +431,8 @@ __device__ __forceinline__ void probe_slice_runs_tbl(const uint64_t* s_slice, co
         off[u] = slot < total ? rel * kRunPad : ~0u;
         rec[u][0] = rec[u][1] = u32x4{0, 0, 0, 0};
         if (w0 + u * 64 < total && off[u] != ~0u) {  // (first test uniform: the window's tail steps)
-          rec[u][0] = *reinterpret_cast<const u32x4*>(brecs + off[u]);
-          rec[u][1] = *reinterpret_cast<const u32x4*>(brecs + off[u] + 4);
+          rec[u][0] = stream_load<RPT_NT_REC_LOADS>(reinterpret_cast<const u32x4*>(brecs + off[u]));
+          rec[u][1] = stream_load<RPT_NT_REC_LOADS>(reinterpret_cast<const u32x4*>(brecs + off[u] + 4));
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -731,7 +731,8 @@ __global__ __launch_bounds__(kUnpermuteSelThreads<TM>) void unpermute_sel_kernel
 #pragma unroll
   for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
     pv[sg] = u32x4{0, 0, 0, 0};
-    if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos + (seg0 + sg) * kSegRows + lane * 8);
+    if (seg0 + sg < n_segs)
+      pv[sg] = stream_load<RPT_NT_REC_LOADS>(reinterpret_cast<const u32x4*>(pos + (seg0 + sg) * kSegRows + lane * 8));
   }
   {
     const u32x4* src = reinterpret_cast<const u32x4*>(passbits + tile * (tile_cap / 8));
