@@ -506,15 +506,25 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 }
 
 // ---- partitioned build: OR each slice's records into an LDS copy, then merge into the filter ----
-// Same flattened run walk as slice_probe_kernel. The slice starts from zero in LDS (ds_or_b64 per
-// record) and is merged into the filter with coalesced 64-bit device-scope atomic ORs of its non-zero
-// words, so concurrent inserts and several workgroups per slice compose (OR is idempotent).
+// Same flattened run walk as slice_probe_kernel. Records are ORed into an LDS copy of the slice
+// (ds_or_b64 per record), which is then merged into the filter by one of (`mode`):
+//   kSliceMergeAtomic    LDS starts at zero; coalesced 64-bit device-scope atomic ORs of its non-zero
+//                        words (several workgroups per slice compose: OR is idempotent)
+//   kSliceMergeStore     the filter is all zero (rpt_bf::pristine) and this workgroup owns the slice:
+//                        LDS starts at zero, non-zero 16-B pieces leave as plain stores
+//   kSliceMergeAdaptive  this workgroup owns the slice: with >= kSliceWords/2 records it loads the slice
+//                        into LDS first and stores it back whole (read + write at the streaming rate),
+//                        with fewer it merges with atomics as above
+// Memory-side atomics run at ~1.3 TB/s against ~6 TB/s for plain stores (MI355X_MICROARCH.md, Global
+// atomics): the C5 build's merge of an 8 GiB filter took 5.8 ms with atomics. Plain writes are safe
+// because the host orders every word-writing operation on a filter (rpt_bf::order_mu).
+constexpr int kSliceMergeAtomic = 0, kSliceMergeStore = 1, kSliceMergeAdaptive = 2;
 __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* __restrict__ words, uint32_t splits,
                                                                     uint64_t n_tiles,
                                                                     const uint32_t* __restrict__ recs,
                                                                     const uint32_t* __restrict__ runs,
                                                                     uint32_t tile_cap,
-                                                                    const uint32_t* __restrict__ bucket_tiles) {
+                                                                    const uint32_t* __restrict__ bucket_tiles, int mode) {
   // one LDS array, table first: the slice's base offset folds into the ds_read immediate
   __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
   uint64_t* const s_rmasks = s_lds;
@@ -524,12 +534,32 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   const uint32_t slice = sw.slice;
   const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
   if (t_lo >= t_hi) return;  // no rows reach this slice (uniform)
-  for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) s_slice[i] = 0;
-  fill_rot_mask_table(s_rmasks);
-  __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
+  uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
+  u64x2* const s_slice2 = reinterpret_cast<u64x2*>(s_slice);
+  u64x2* const dst2 = reinterpret_cast<u64x2*>(dst);
+  constexpr uint32_t kPieces = kSliceWords / 2;  // 16-B pieces of a slice
+  bool rmw = false;
+  if (mode == kSliceMergeAdaptive) {  // uniform: records this workgroup ORs into the slice
+    uint32_t r = 0;
+    for (uint64_t t = t_lo + threadIdx.x; t < t_hi; t += kSliceThreads) r += my_runs[t] & 0xFFFFu;
+    r = wave_sum(r);
+    if (lane == 0) s_win[wave] = r;
+    __syncthreads();
+    uint32_t tot = 0;
+    for (uint32_t w = 0; w < kWaves; w++) tot += s_win[w];
+    rmw = tot >= kSliceWords / 2;
+    __syncthreads();
+  }
+  if (rmw) {
+    for (uint32_t i = threadIdx.x; i < kPieces; i += kSliceThreads) s_slice2[i] = dst2[i];
+  } else {
+    for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) s_slice[i] = 0;
+  }
+  fill_rot_mask_table(s_rmasks);
+  __syncthreads();
   const uint32_t bt = batch_tiles(t_hi - t_lo);  // as slice_probe_kernel
   // slot -> run through the wave's LDS window, as probe_slice_runs_tbl
   constexpr uint32_t kWin = 64 * RPT_SLICE_UNROLL;
@@ -589,10 +619,18 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
     }
   }
   __syncthreads();
-  uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
-  for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
-    const uint64_t v = s_slice[i];
-    if (v) __hip_atomic_fetch_or(dst + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (rmw) {
+    for (uint32_t i = threadIdx.x; i < kPieces; i += kSliceThreads) dst2[i] = s_slice2[i];
+  } else if (mode == kSliceMergeStore) {
+    for (uint32_t i = threadIdx.x; i < kPieces; i += kSliceThreads) {
+      const u64x2 v = s_slice2[i];
+      if ((v[0] | v[1]) != 0) dst2[i] = v;
+    }
+  } else {
+    for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
+      const uint64_t v = s_slice[i];
+      if (v) __hip_atomic_fetch_or(dst + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

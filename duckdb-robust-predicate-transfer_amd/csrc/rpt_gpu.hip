@@ -55,6 +55,15 @@ struct rpt_bf {
   std::atomic<int> finalized{0};
   std::atomic<int> probe_strategy{RPT_PROBE_AUTO};
   std::atomic<int> insert_strategy{RPT_INSERT_AUTO};
+  // Device order of the operations that write the words (inserts, clear, merges, copies): each waits
+  // for the previous one's event, whatever host thread or stream enqueued it, so concurrent inserts
+  // compose (OR) even where the slice insert updates words with plain read-modify-write stores.
+  // `pristine`: every word is zero once the last ordered write completes (create / clear /
+  // reinitialize, no write since): the next slice insert may then store its slices outright.
+  std::mutex order_mu;
+  hipEvent_t order_ev = nullptr;
+  bool order_pending = false;
+  bool pristine = true;
 };
 
 namespace {
@@ -175,6 +184,24 @@ const char* inst_name(const char* base) {
   names.emplace_back(base, std::move(s));
   return names.back().second.c_str();
 }
+
+// Scope of one word-writing operation on a filter (see rpt_bf::order_mu): waits on `s` for the previous
+// write's completion event, and records this one's when done() is called (after the launches).
+struct WriteOrder {
+  rpt_bf* bf;
+  hipStream_t s;
+  std::unique_lock<std::mutex> lk;
+  WriteOrder(rpt_bf* b, hipStream_t st) : bf(b), s(st), lk(b->order_mu) {
+    if (bf->order_pending) (void)hipStreamWaitEvent(s, bf->order_ev, 0);
+  }
+  // pristine_after: every word is zero once this operation completes
+  void done(bool pristine_after) {
+    if (!bf->order_ev && hipEventCreateWithFlags(&bf->order_ev, hipEventDisableTiming) != hipSuccess) bf->order_ev = nullptr;
+    bf->order_pending = bf->order_ev != nullptr && hipEventRecord(bf->order_ev, s) == hipSuccess;
+    if (!bf->order_pending) (void)hipStreamSynchronize(s);  // no event: order by waiting here
+    bf->pristine = pristine_after;
+  }
+};
 
 int num_cus(int device) {
   static std::mutex mu;
@@ -816,6 +843,7 @@ int rpt_bf_destroy(rpt_bf* bf) {
     DeviceGuard g(bf->device);
     if (bf->words) (void)hipFree(bf->words);
     if (bf->stats) (void)hipFree(bf->stats);
+    if (bf->order_ev) (void)hipEventDestroy(bf->order_ev);
   }
   delete bf;
   return RPT_OK;
@@ -844,6 +872,9 @@ int rpt_bf_reinitialize(rpt_bf* bf, uint64_t actual_rows) {
   bf->sized_for_rows = actual_rows;
   bf->has_data.store(0);
   RPT_HIP(hipMemcpy(bf->stats, kStatsInit, sizeof kStatsInit, hipMemcpyHostToDevice));
+  std::lock_guard<std::mutex> lk(bf->order_mu);
+  bf->order_pending = false;  // the device is idle
+  bf->pristine = true;
   return RPT_OK;
 }
 
@@ -862,8 +893,11 @@ int rpt_bf_set_has_data(rpt_bf* bf, int value) {
 int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
   RPT_ON_DEVICE(bf->device);
-  RPT_HIP(hipMemsetAsync(bf->words, 0, (1ULL << bf->log_num_blocks) * 8, as_stream(stream)));
+  WriteOrder order(bf, as_stream(stream));
+  const hipError_t e = hipMemsetAsync(bf->words, 0, (1ULL << bf->log_num_blocks) * 8, as_stream(stream));
   hipLaunchKernelGGL(stats_reset_kernel, dim3(1), dim3(1), 0, as_stream(stream), bf->stats);
+  order.done(e == hipSuccess);
+  if (e != hipSuccess) return fail(RPT_ERR_HIP, "hipMemsetAsync failed: %s", hipGetErrorString(e));
   RPT_LAUNCHED("stats_reset_kernel");
   bf->has_data.store(0);
   return RPT_OK;
@@ -903,7 +937,9 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const unsigned grid = persistent_grid(bf->device, n_segs);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
+  WriteOrder order(bf, as_stream(stream));
   RPT_DISPATCH_KD(launch_insert_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n, n_segs);
+  order.done(false);
   RPT_LAUNCHED("insert_kernel");
   return RPT_OK;
 }
@@ -998,10 +1034,16 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   if (st != RPT_OK) return st;
   const uint32_t splits = static_cast<uint32_t>(
       std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) / grid_slices)));
+  // only the slice merge writes the words: it alone is ordered after the filter's previous writes
+  WriteOrder order(bf, s);
+  // one workgroup per slice: plain stores (a pristine filter) or a per-slice choice of read-modify-write
+  // vs atomic ORs; several workgroups per slice must merge with atomics
+  const int mode = splits > 1 ? rpt::kSliceMergeAtomic : (bf->pristine ? rpt::kSliceMergeStore : rpt::kSliceMergeAdaptive);
   ProfScope prof_i("slice_insert_kernel", s);
   hipLaunchKernelGGL(rpt::slice_insert_kernel, dim3(grid_slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words, splits,
-                     n_tiles, ws.recs, ws.runs, static_cast<uint32_t>(rpt::tile_cap_for(tile_slices, tm)), bucket_tiles);
+                     n_tiles, ws.recs, ws.runs, static_cast<uint32_t>(rpt::tile_cap_for(tile_slices, tm)), bucket_tiles, mode);
   prof_i.end();
+  order.done(false);
   RPT_LAUNCHED("slice_insert_kernel");
   return RPT_OK;
 }
@@ -1283,7 +1325,9 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
     return fail(RPT_ERR_SHAPE_MISMATCH, "merge of log_num_blocks %d (dev %d) with %d (dev %d)", dst->log_num_blocks,
                 dst->device, src->log_num_blocks, src->device);
   RPT_ON_DEVICE(dst->device);
+  WriteOrder order(dst, as_stream(stream));
   int st = rpt_words_or(dst->words, src->words, 1ULL << dst->log_num_blocks, stream);
+  order.done(false);
   if (st != RPT_OK) return st;
   hipLaunchKernelGGL(stats_merge_kernel, dim3(1), dim3(1), 0, as_stream(stream), dst->stats, src->stats);
   RPT_LAUNCHED("stats_merge_kernel");
@@ -1393,6 +1437,7 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
     return fail(RPT_ERR_OUT_OF_MEMORY, "allreduce staging of %zu bytes", tmp_bytes);
   }
   tmp = reinterpret_cast<uint64_t*>(v + 4);
+  WriteOrder order(bf, s);
   auto run = [&]() -> int {
     if (world > 1) {
       // reduce-scatter by OR: rank `me` owns words [lo(me), lo(me + 1)); peers' copies land in tmp
@@ -1430,6 +1475,7 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
     return RPT_OK;
   };
   const int st = run();
+  order.done(false);
   if (st == RPT_OK) {
     (void)hipFree(v);
   } else {
@@ -1497,6 +1543,11 @@ int rpt_bf_fold(rpt_bf* bf, int* out_new_log_num_blocks) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
   RPT_ON_DEVICE(bf->device);
   RPT_HIP(hipDeviceSynchronize());
+  {
+    std::lock_guard<std::mutex> lk(bf->order_mu);
+    bf->order_pending = false;  // the device is idle; fold writes synchronously below
+    bf->pristine = false;
+  }
   constexpr int kMinLog = 4;  // bloom_filter.h Fold: log_num_blocks_min
   for (;;) {
     if (bf->log_num_blocks <= kMinLog) break;
@@ -1541,6 +1592,11 @@ int rpt_bf_import_words(rpt_bf* bf, const uint64_t* host_words, uint64_t n_words
                 (unsigned long long)(1ULL << bf->log_num_blocks));
   RPT_ON_DEVICE(bf->device);
   RPT_HIP(hipDeviceSynchronize());
+  {
+    std::lock_guard<std::mutex> lk(bf->order_mu);
+    bf->order_pending = false;
+    bf->pristine = false;
+  }
   RPT_HIP(hipMemcpy(bf->words, host_words, n_words * 8, hipMemcpyHostToDevice));
   int any = 0;
   for (uint64_t i = 0; i < n_words && !any; i++) any = host_words[i] != 0;
@@ -1564,7 +1620,10 @@ int rpt_bf_copy_words_from(rpt_bf* bf, const uint64_t* src_dev, uint64_t n_words
     return fail(RPT_ERR_SHAPE_MISMATCH, "copy of %llu words into a %llu-word filter", (unsigned long long)n_words,
                 (unsigned long long)(1ULL << bf->log_num_blocks));
   RPT_ON_DEVICE(bf->device);
-  RPT_HIP(hipMemcpyAsync(bf->words, src_dev, n_words * 8, hipMemcpyDeviceToDevice, as_stream(stream)));
+  WriteOrder order(bf, as_stream(stream));
+  const hipError_t e = hipMemcpyAsync(bf->words, src_dev, n_words * 8, hipMemcpyDeviceToDevice, as_stream(stream));
+  order.done(false);
+  if (e != hipSuccess) return fail(RPT_ERR_HIP, "hipMemcpyAsync failed: %s", hipGetErrorString(e));
   return RPT_OK;
 }
 

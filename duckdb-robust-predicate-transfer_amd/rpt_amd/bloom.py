@@ -211,6 +211,8 @@ class BloomFilter:
         ws_bytes = int(self._lib.rpt_bf_insert_workspace_bytes(self._h, n))  # 0: atomic insert
         if ws_bytes:
             ws = torch.empty(ws_bytes, dtype=torch.uint8, device=self.device)
+            if isinstance(stream, torch.cuda.Stream):
+                ws.record_stream(stream)  # freed below while the insert may still run on `stream`
             check(self._lib.rpt_bf_insert_ws(self._h, ctypes.byref(col), n, ws.data_ptr(), ws_bytes,
                                              _stream(self.device, stream)))
         else:

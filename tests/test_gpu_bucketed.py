@@ -191,3 +191,37 @@ def test_c5_geometry_8gib_filter_vs_oracle(rpt):
     ref_r = row_sel[orc.probe_keys(w, log_nb, probe, key_sel=row_sel)]
     sel_r = bf.lookup_sel(dprobe, row_sel=dev(row_sel)).cpu().numpy().astype(np.uint32)
     assert np.array_equal(sel_r, ref_r)
+
+
+@pytest.mark.parametrize("strategy", [INS_PARTITIONED, INS_BUCKETED])
+def test_slice_merge_modes_vs_oracle(rpt, strategy):
+    """The slice insert's merges into a 2^22-block filter (256 slices, one workgroup each): plain stores
+    into the pristine filter, read-modify-write of slices receiving >= 8192 records, atomic ORs for a
+    small insert, and two large inserts racing on two streams from two host threads (the filter orders
+    its word writes): every word equals the oracle's."""
+    import threading
+
+    log_nb = 22
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    a, b, c = (keys_of(np.int64, n, seed) for n, seed in ((3_000_000, 41), (3_000_000, 42), (1000, 43)))
+    w = orc.new_words(log_nb)
+    for keys in (a, b, c):  # pristine -> stores; ~11.7k records per slice -> RMW; 1000 keys -> atomics
+        bf.insert(dev(keys), strategy=strategy)
+        orc.insert_keys(w, log_nb, keys)
+        assert np.array_equal(bf.export_words(), w)
+    bf.clear()
+    assert bf.export_words().sum() == 0
+    da, db = dev(a), dev(b)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    threads = [threading.Thread(target=bf.insert, args=(k,), kwargs=dict(strategy=strategy, stream=st))
+               for k, st in zip((da, db), streams)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    torch.cuda.synchronize()
+    w2 = orc.new_words(log_nb)
+    orc.insert_keys(w2, log_nb, a)
+    orc.insert_keys(w2, log_nb, b)
+    assert np.array_equal(bf.export_words(), w2)
