@@ -152,7 +152,7 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
     const uint64_t sbase = tile_base + seg_local;
     uint64_t hh[8];
     bool oo[8];
-    load_hashes<K, DENSE>(a, sbase, n, lane, hh, oo);
+    load_hashes<K, DENSE, false, false, true>(a, sbase, n, lane, hh, oo);
     uint16_t pv[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) {

@@ -113,7 +113,7 @@ __device__ __forceinline__ bool valid_at(const uint64_t* validity, uint64_t idx)
 //  GENERAL (dictionary key_sel and/or row_sel):        row(c) = base + c*64 + lane.
 // MM: also fold the valid (non-NULL, in-range) key values into mm[0] = min, mm[1] = max (the build's
 // min/max dynamic filter, physical_create_bf.cpp:82-119, fused into the key read).
-template <int K, bool DENSE, bool MM = false, bool NT = false>
+template <int K, bool DENSE, bool MM = false, bool NT = false, bool BATCH = false>
 __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uint64_t n, uint32_t lane,
                                             uint64_t (&h)[8], bool (&ok)[8], int64_t* mm = nullptr) {
   using Tr = KeyTraits<K>;
@@ -121,7 +121,75 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
   // rows left from `base` (uniform), so per-row bounds checks are 32-bit and addresses are
   // uniform-base + 32-bit lane offset
   const uint32_t rem = n > base ? static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows) : 0u;
-  if constexpr (DENSE) {
+  if constexpr (DENSE && BATCH) {
+    constexpr int V = Tr::kVec;
+    constexpr int C = 8 / V;
+    const T* kb = static_cast<const T*>(a.keys) + base;
+    const uint64_t* vb = a.validity ? a.validity + (base >> 6) : nullptr;  // base is a multiple of 512
+    [[maybe_unused]] const uint8_t* hb = K == kKeySplit ? a.hi8 + base : nullptr;
+    T v[8];
+    uint32_t vbits[C], hi4[C];  // validity bits of the lane's V rows (bits 0..V-1); kKeySplit hash bits 32..39
+    if (rem == static_cast<uint32_t>(kSegRows)) {
+      // A full segment (uniform branch): every load is issued back to back (with one per-lane "full
+      // vector or tail" branch per 16-B load, both paths write the same registers and the compiler
+      // waits for each load before issuing the next). Measured: bucketed level-1 scatter (one
+      // workgroup per CU) 3.55 -> 3.38 ms; the partition and count kernels 1-3 % slower, so they keep
+      // the per-load form.
+#pragma unroll
+      for (int c = 0; c < C; c++) {
+        const uint32_t off = static_cast<uint32_t>(c * 64 * V) + lane * V;
+        if constexpr (V == 2) {
+          const u64x2 x = stream_load<NT>(reinterpret_cast<const u64x2*>(kb + off));
+          v[c * 2] = static_cast<T>(x[0]);
+          v[c * 2 + 1] = static_cast<T>(x[1]);
+        } else {
+          const u32x4 x = stream_load<NT>(reinterpret_cast<const u32x4*>(kb + off));
+#pragma unroll
+          for (int e = 0; e < V; e++) v[c * V + e] = static_cast<T>(x[e]);
+        }
+        hi4[c] = 0;
+        if constexpr (K == kKeySplit) hi4[c] = *reinterpret_cast<const uint32_t*>(hb + off);
+        vbits[c] = (1u << V) - 1;
+      }
+      if (Tr::kValues && vb != nullptr) {
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+          const uint32_t off = static_cast<uint32_t>(c * 64 * V) + lane * V;
+          vbits[c] = static_cast<uint32_t>(vb[off >> 6] >> (off & 63));  // V | 64: one word
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; c++) {
+        const uint32_t off = static_cast<uint32_t>(c * 64 * V) + lane * V;
+#pragma unroll
+        for (int e = 0; e < V; e++) v[c * V + e] = (off + e < rem) ? kb[off + e] : T(0);
+        vbits[c] = (1u << V) - 1;
+        if (Tr::kValues && vb != nullptr && off < rem) vbits[c] = static_cast<uint32_t>(vb[off >> 6] >> (off & 63));
+        hi4[c] = 0;
+        if constexpr (K == kKeySplit)
+          for (int e = 0; e < V; e++) hi4[c] |= (off + e < rem ? static_cast<uint32_t>(hb[off + e]) : 0u) << (8 * e);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      const uint32_t off = static_cast<uint32_t>(c * 64 * V) + lane * V;
+#pragma unroll
+      for (int e = 0; e < V; e++) {
+        ok[c * V + e] = off + e < rem;
+        uint64_t hv = Tr::hash(v[c * V + e]);
+        if constexpr (K == kKeySplit) hv |= static_cast<uint64_t>((hi4[c] >> (8 * e)) & 0xFFu) << 32;
+        if (Tr::kValues && !((vbits[c] >> e) & 1u)) hv = kNullHash;
+        h[c * V + e] = hv;
+        if constexpr (MM && Tr::kValues) {
+          if (off + e < rem && ((vbits[c] >> e) & 1u)) {
+            mm[0] = min(mm[0], static_cast<int64_t>(v[c * V + e]));
+            mm[1] = max(mm[1], static_cast<int64_t>(v[c * V + e]));
+          }
+        }
+      }
+    }
+  } else if constexpr (DENSE) {
     constexpr int V = Tr::kVec;
     const T* kb = static_cast<const T*>(a.keys) + base;
     const uint64_t* vb = a.validity ? a.validity + (base >> 6) : nullptr;  // base is a multiple of 512
