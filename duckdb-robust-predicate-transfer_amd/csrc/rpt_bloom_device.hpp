@@ -41,9 +41,14 @@ __device__ __forceinline__ uint64_t murmur64(uint64_t x) {
 }
 
 // DuckDB CombineHash for composite keys (HashColumns, reference src/bloom_filter.cpp:15-17):
-// hashes = CombineHashScalar(hashes, Hash(col_j)) = (a * 0xbf58476d1ce4e5b9) ^ b. Restated from
-// DuckDB (vector_hash.cpp), not in this container: parity unpinned, as for the key hash itself.
-__device__ __forceinline__ uint64_t combine_hash(uint64_t a, uint64_t b) { return (a * 0xbf58476d1ce4e5b9ULL) ^ b; }
+// hashes = CombineHashScalar(hashes, Hash(col_j)) with DuckDB v1.1+'s form: a ^= a >> 32;
+// a *= 0xd6e8feb86659fd93; a ^ b (v0.x-1.0: (a * 0xbf58476d1ce4e5b9) ^ b). Restated from DuckDB
+// (vector_hash.cpp), not in this container: parity unpinned, as for the key hash itself.
+__device__ __forceinline__ uint64_t combine_hash(uint64_t a, uint64_t b) {
+  a ^= a >> 32;
+  a *= 0xd6e8feb86659fd93ULL;
+  return a ^ b;
+}
 
 __device__ __forceinline__ uint64_t rotl64(uint64_t x, uint32_t r) {
   return (x << r) | (x >> ((64u - r) & 63u));

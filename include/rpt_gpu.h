@@ -214,7 +214,8 @@ int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, ui
 /* Key hashes exactly as the filter sees them (DuckDB HashColumns restatement). */
 int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, rpt_stream_t stream);
 /* HashColumns' CombineHash step for composite keys (bloom_filter.cpp:15-17): inout_hashes[i] =
- * (inout_hashes[i] * 0xbf58476d1ce4e5b9) ^ Hash(row i of col). rpt_hash_keys(col_0) followed by
+ * CombineHashScalar(inout_hashes[i], Hash(row i of col)) with DuckDB v1.1+'s form (a ^= a >> 32;
+ * a *= 0xd6e8feb86659fd93; a ^ b; restated, parity unpinned). rpt_hash_keys(col_0) followed by
  * rpt_hash_combine(col_j) for j = 1, 2, ... is the composite-key hash; insert / probe it as an
  * RPT_KEY_HASH column. */
 int rpt_hash_combine(const rpt_key_column* col, uint64_t n, uint64_t* inout_hashes, rpt_stream_t stream);

@@ -180,7 +180,14 @@ void insert_keys(uint64_t* words, int log_nb, const T* keys, const uint32_t* key
 
 }  // namespace
 
-inline uint64_t combine_hash(uint64_t a, uint64_t b) { return (a * 0xbf58476d1ce4e5b9ULL) ^ b; }
+// DuckDB CombineHashScalar as of v1.1+ (the hash rework that also introduced this MurmurHash64
+// finalizer): a ^= a >> 32; a *= 0xd6e8feb86659fd93; return a ^ b. Restated from memory (v0.x-1.0 used
+// (a * 0xbf58476d1ce4e5b9) ^ b); no DuckDB source in the image: parity unpinned.
+inline uint64_t combine_hash(uint64_t a, uint64_t b) {
+  a ^= a >> 32;
+  a *= 0xd6e8feb86659fd93ULL;
+  return a ^ b;
+}
 
 // TypedUpdateMinMax (reference physical_create_bf.cpp:86-119) for INTEGER / BIGINT: min and max of
 // the valid rows (row -> physical index through key_sel, validity by physical index). Returns 0 and
@@ -255,8 +262,8 @@ void rpt_oracle_hash_i32(const int32_t* keys, const uint32_t* key_sel, const uin
 }
 
 // HashColumns' CombineHash (reference src/bloom_filter.cpp:15-17) for composite keys: DuckDB
-// CombineHashScalar(a, b) = (a * 0xbf58476d1ce4e5b9) ^ b with b = Hash(row of col_j). Restated from
-// DuckDB (vector_hash.cpp; source absent): UNPINNED, like the key hash.
+// CombineHashScalar(a, b) (combine_hash above, the v1.1+ form) with b = Hash(row of col_j). Restated
+// from DuckDB (vector_hash.cpp; source absent): UNPINNED, like the key hash.
 void rpt_oracle_hash_combine_i64(const int64_t* keys, const uint32_t* key_sel, const uint64_t* validity, uint64_t n,
                                  uint64_t* inout) {
   for (uint64_t i = 0; i < n; i++) inout[i] = combine_hash(inout[i], key_hash(keys, key_sel, validity, i));
