@@ -382,6 +382,41 @@ def test_full_size_probe_properties(rpt, n_probe, n_build, p, strategy):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("config,n_build,n_filter", [("C3", 10**8, 10**8), ("C5 share", 10**9, 8 * 10**9)])
+def test_full_size_configs_every_row(rpt, config, n_build, n_filter):
+    """BASELINE C3 (1e8-key build, 128 MiB filter: partitioned, 32 Ki-row tiles) and one rank's share of
+    C5 (1e9 keys into the 8 GiB filter sized for 8e9: bucketed insert and probe) at full size, as
+    bench.py runs them (AUTO strategies): the filter word for word and every one of the 1e9 probe rows
+    against the oracle (built with host threads from the same synthetic streams)."""
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    n_probe = 10**9
+    build = rpt.synth_build_keys(n_build)
+    bf = rpt.BloomFilter(n_filter)
+    bf.insert(build)
+    del build
+    lnb = bf.log_num_blocks
+    assert bf.probe_strategy_for(n_probe) == (3 if config == "C3" else 4)
+    ow = orc.new_words(lnb)
+    orc.build_mt(ow, lnb, orc.synth_build_keys(n_build), threads)
+    got = torch.empty(bf.num_blocks, dtype=torch.int64, device="cuda:0")
+    bf.copy_words_to(got)
+    assert torch.equal(got, torch.from_numpy(ow.view(np.int64)).to("cuda:0")), "filter words differ from the oracle"
+    del got
+    torch.cuda.empty_cache()
+    probe = rpt.synth_probe_keys(n_probe, n_build, 100)
+    sel_t, cnt = bf.probe_async(probe)
+    count = int(cnt.item())
+    sel = sel_t[:count].cpu().numpy().astype(np.int64)
+    del sel_t
+    torch.cuda.empty_cache()
+    assert np.all(sel[1:] > sel[:-1])
+    _full_check(ow, lnb, probe, sel)
+    assert 0.1 <= count / n_probe < 0.15
+    del probe
+    torch.cuda.empty_cache()
+
+
 @pytest.mark.parametrize("strategy", ["partitioned", "gather"])
 def test_row_ids_beyond_int32(rpt, strategy):
     """n > 2^31 rows (sel_t is uint32): ids past 2^31 stay exact, ascending, and match the oracle."""
