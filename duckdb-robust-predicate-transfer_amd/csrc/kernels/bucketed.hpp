@@ -215,7 +215,10 @@ __global__ __launch_bounds__(kBlockThreads) void bucket_pad_kernel(const uint32_
 // B6: level-1 unpermute. Per level-1 tile: gather the pass bits of its bucket runs out of the level-2
 // result bits (bits2, level-2 array order) into LDS in the tile's bucket-sorted order, 64-bit pieces
 // per item (run, piece), then map every row through its position (pos1) -> result bits + counts.
-constexpr int kBucketUnpermuteThreads = 256;
+#ifndef RPT_BUCKET_UNPERMUTE_THREADS
+#define RPT_BUCKET_UNPERMUTE_THREADS 256
+#endif
+constexpr int kBucketUnpermuteThreads = RPT_BUCKET_UNPERMUTE_THREADS;
 __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kernel(
     const uint16_t* __restrict__ pos1, const uint64_t* __restrict__ bits2, uint64_t n, uint32_t bucket_mask,
     const uint32_t* __restrict__ counts_tm, const uint32_t* __restrict__ pre_tm, const uint64_t* __restrict__ base,

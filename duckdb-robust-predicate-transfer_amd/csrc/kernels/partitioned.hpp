@@ -494,7 +494,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
     if (nitem < n_items) {
       const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(nxt.slice) * kSliceWords);
 #pragma unroll
-      for (uint32_t i = 0; i < kPre; i++) pre[i] = src[threadIdx.x + i * kSliceThreads];
+      for (uint32_t i = 0; i < kPre; i++) pre[i] = stream_load<RPT_NT_SLICE_LOADS>(src + threadIdx.x + i * kSliceThreads);
     }
     probe_slice_runs_tbl(s_slice, s_rmasks, s_win, cur, n_tiles, recs, runs, passbits, tile_cap);
     if (nitem >= n_items) break;
