@@ -6,9 +6,10 @@
 namespace rpt {
 
 // ---- bucketed strategy (filters of 2^22..2^31 blocks) ----------------------------------------------
-// Level 1 cuts the rows by 16 MiB filter region ("bucket": 128 slices) into one contiguous hash array
+// Level 1 cuts the rows by 32 MiB filter region ("bucket": 256 slices) into one contiguous hash array
 // per bucket, each padded to whole 16 Ki-row tiles; level 2 is the partitioned pipeline above over
-// those arrays, every bucket against its own 128 slices. bucket = block id >> 21 = hash bits 37...
+// those arrays, every bucket against its own 256 slices. bucket = block id >> 22 = hash bits 38...
+static_assert(kLogNumMasks + 6 + kSliceLog + kBucketSliceLog <= 40, "level-2 split hashes carry bits 0..39");
 __device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t bucket_mask) {
   return static_cast<uint32_t>(h >> (kLogNumMasks + 6 + kSliceLog + kBucketSliceLog)) & bucket_mask;
 }

@@ -40,11 +40,18 @@ __host__ __device__ constexpr uint64_t tile_cap_for(uint32_t n_slices, uint32_t 
 // per slice would otherwise average under 64 records and the slice probe's reads fragment. Measured
 // (probe ms per 1e9 keys, 16 Ki -> 32 Ki rows): 1024 slices 6.25 -> 5.12, 512 slices 5.05 -> 4.6,
 // 256 slices 4.31 -> 4.30 (build 0.26 -> 0.22 ms), 128 slices 3.95 -> 4.22 (one workgroup per CU
-// costs the partition more than the longer runs save). The bucketed strategy's level 2 (128 slices
+// costs the partition more than the longer runs save). The bucketed strategy's level 2 (256 slices
 // per bucket) keeps tm = 1.
 __host__ __device__ constexpr uint32_t tile_mult(uint32_t n_slices) { return n_slices > 128 ? 2u : 1u; }
-// Bucketed strategy (filters > 128 MiB): 16 MiB buckets of 128 slices, at most 1024 buckets (16 GiB).
-constexpr int kBucketSliceLog = 7;
+// Bucketed strategy (filters > 128 MiB): 32 MiB buckets of 256 slices, at most 512 buckets (16 GiB).
+// Bucket size (C5 probe / build ms per 1e9 keys, 8 GiB filter; level-2 tiles of 16 Ki rows): 128 slices
+// 10.5 / 12.3, 256 slices 9.8 / 11.7, 512 slices 10.5 / 12.3, 1024 slices 11.0 / 12.5 -- longer level-1
+// runs (a faster scatter and unpermute) against shorter level-2 runs (a slower partition and slice probe).
+#ifndef RPT_BUCKET_SLICE_LOG
+#define RPT_BUCKET_SLICE_LOG 8
+#endif
+constexpr int kBucketSliceLog = RPT_BUCKET_SLICE_LOG;
+constexpr int kMaxBucketedLog = 31;  // 16 GiB
 constexpr uint32_t kBucketSlices = 1u << kBucketSliceLog;
 constexpr uint32_t kMaxBuckets = 1024;
 constexpr int kTileThreads = 1024;                     // 16 waves
@@ -279,7 +286,43 @@ __device__ __forceinline__ uint32_t seg_row(int j, uint32_t lane) {
 }
 
 // Wave-wide (min, max) of per-lane values, returned wave-uniform (scalar registers).
+#ifndef RPT_DPP_MINMAX
+#define RPT_DPP_MINMAX 1
+#endif
+// One DPP step on both 32-bit halves of an int64; lanes the row mask disables keep their own value.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ int64_t dpp_i64(int64_t v) {
+  const uint64_t u = static_cast<uint64_t>(v);
+  const int lo = static_cast<int>(static_cast<uint32_t>(u)), hi = static_cast<int>(static_cast<uint32_t>(u >> 32));
+  const uint32_t rlo = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(lo, lo, CTRL, ROW_MASK, 0xf, false));
+  const uint32_t rhi = static_cast<uint32_t>(__builtin_amdgcn_update_dpp(hi, hi, CTRL, ROW_MASK, 0xf, false));
+  return static_cast<int64_t>((static_cast<uint64_t>(rhi) << 32) | rlo);
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ void minmax_step(int64_t& mn, int64_t& mx) {
+  mn = min(mn, dpp_i64<CTRL, ROW_MASK>(mn));
+  mx = max(mx, dpp_i64<CTRL, ROW_MASK>(mx));
+}
 __device__ __forceinline__ void wave_minmax(int64_t& mn, int64_t& mx) {
+#if RPT_DPP_MINMAX
+  // quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: every lane holds its row's value;
+  // row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3): lane 63 holds the wave's. All VALU (DPP),
+  // where __shfl_xor costs 24 ds_bpermute per call (the level-1 count: +0.28 ms per 1e9 build keys).
+  minmax_step<0xB1, 0xf>(mn, mx);
+  minmax_step<0x4E, 0xf>(mn, mx);
+  minmax_step<0x141, 0xf>(mn, mx);
+  minmax_step<0x140, 0xf>(mn, mx);
+  minmax_step<0x142, 0xa>(mn, mx);
+  minmax_step<0x143, 0xc>(mn, mx);
+  auto lane63 = [](int64_t v) {
+    const uint64_t u = static_cast<uint64_t>(v);
+    const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(u)), 63));
+    const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(u >> 32)), 63));
+    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+  };
+  mn = lane63(mn);
+  mx = lane63(mx);
+#else
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     mn = min(mn, static_cast<int64_t>(__shfl_xor(static_cast<long long>(mn), d, 64)));
@@ -293,6 +336,7 @@ __device__ __forceinline__ void wave_minmax(int64_t& mn, int64_t& mx) {
   };
   mn = uniform(mn);
   mx = uniform(mx);
+#endif
 }
 // Fold a wave's uniform (min, max) into stats[0..1] (int64, device). A wave whose values cannot lower
 // the min or raise the max — the common case once a few waves have reported — skips the atomics.

@@ -255,20 +255,21 @@ uint32_t slice_count(int log_num_blocks) {
   return log_num_blocks <= rpt::kSliceLog ? 1u : (1u << (log_num_blocks - rpt::kSliceLog));
 }
 
-// 16 MiB buckets of the bucketed strategy (1 for smaller filters).
+// 32 MiB buckets of the bucketed strategy (1 for smaller filters).
 uint32_t bucket_count(int log_num_blocks) {
   return 1u << std::max(0, log_num_blocks - rpt::kSliceLog - rpt::kBucketSliceLog);
 }
 
 int strategy_supported(int strategy, int log_num_blocks) {
-  constexpr int kBucketLog = rpt::kSliceLog + rpt::kBucketSliceLog;  // log2 blocks per bucket (21)
+  constexpr int kBucketLog = rpt::kSliceLog + rpt::kBucketSliceLog;  // log2 blocks per bucket (22)
   switch (strategy) {
     case RPT_PROBE_GATHER: return 1;
     case RPT_PROBE_LDS: return log_num_blocks <= rpt::kLdsDirectMaxLog;
     case RPT_PROBE_PARTITIONED:
       return log_num_blocks >= rpt::kSliceLog && slice_count(log_num_blocks) <= static_cast<uint32_t>(rpt::kMaxSliceCount);
-    case RPT_PROBE_BUCKETED:  // 2..1024 buckets of 16 MiB
-      return log_num_blocks > kBucketLog && bucket_count(log_num_blocks) <= rpt::kMaxBuckets;
+    case RPT_PROBE_BUCKETED:  // 1..512 buckets of 32 MiB (filters of 32 MiB..16 GiB)
+      return log_num_blocks >= kBucketLog && log_num_blocks <= rpt::kMaxBucketedLog &&
+             bucket_count(log_num_blocks) <= rpt::kMaxBuckets;
     default: return 0;
   }
 }
@@ -312,7 +313,7 @@ uint32_t tile_mult_of(uint32_t n_slices) {
 
 // Layout (all 256-aligned): bits | seg_counts | group_sums | group_offs, then for the partitioned
 // strategy recs | pos | passb | runs | runs_tm (whole 16 Ki-row tiles), and for the bucketed one the
-// same level-2 arrays over level2_tiles_max tiles of 128 slices plus the level-1 arrays.
+// same level-2 arrays over level2_tiles_max tiles of 256 slices plus the level-1 arrays.
 size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base, ProbeWorkspace* ws) {
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
@@ -1106,7 +1107,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     RPT_LAUNCHED("probe_bits_kernel<lds>");
   } else {
     // PARTITIONED: the key column, tiles of slice_count(L) slices. BUCKETED: level 1 first, then the
-    // same pipeline over the level-2 hash array (tiles of 128 slices, bucket by bucket), then level 1's
+    // same pipeline over the level-2 hash array (tiles of 256 slices, bucket by bucket), then level 1's
     // unpermute.
     const bool buck = strategy == RPT_PROBE_BUCKETED;
     uint32_t tile_slices = slice_count(L), grid_slices = tile_slices, tm = tile_mult_of(tile_slices);

@@ -59,7 +59,7 @@ typedef enum rpt_probe_strategy {
   RPT_PROBE_LDS = 2,         /* whole filter staged in each workgroup's LDS (filters <= 128 KiB) */
   RPT_PROBE_PARTITIONED = 3, /* rows bucketed per 16 Ki-row tile by 128 KiB filter slice; each slice is
                                 probed from LDS, then row order is restored (filters 128 KiB..128 MiB) */
-  RPT_PROBE_BUCKETED = 4     /* two levels: rows first bucketed by 16 MiB filter region into contiguous
+  RPT_PROBE_BUCKETED = 4     /* two levels: rows first bucketed by 32 MiB filter region into contiguous
                                 hash arrays, then PARTITIONED per region (filters 32 MiB..16 GiB) */
 } rpt_probe_strategy;
 

@@ -86,7 +86,7 @@ def test_workspace_size_grows_with_rows():
     assert lib.rpt_insert_workspace_bytes(10**6, 10) == 0 and lib.rpt_insert_workspace_bytes(10**6, 32) == 0
     # bucketed (filters > 128 MiB): level-1 hash arrays (8 B/row) + level-2 records (4 B/row)
     assert lib.rpt_insert_workspace_bytes(10**6, 26) >= 12 * 10**6
-    assert lib.rpt_probe_workspace_bytes(10**6, 26) >= 18 * 10**6 > lib.rpt_probe_workspace_bytes(10**6, 32)
+    assert lib.rpt_probe_workspace_bytes(10**6, 26) >= 16 * 10**6 > lib.rpt_probe_workspace_bytes(10**6, 32)
 
 
 def test_argument_errors_are_reported():
@@ -110,7 +110,7 @@ def test_strategy_support_rules():
     # partitioned: at least one full LDS slice, at most 1024 slices (128 KiB .. 128 MiB)
     part = [L for L in range(0, 34) if lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_PARTITIONED, L)]
     assert part == list(range(14, 25))
-    # bucketed: 2 .. 1024 buckets of 16 MiB (32 MiB .. 16 GiB), overlapping the partitioned range
+    # bucketed: 1 .. 512 buckets of 32 MiB (32 MiB .. 16 GiB), overlapping the partitioned range
     buck = [L for L in range(0, 40) if lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_BUCKETED, L)]
     assert buck == list(range(22, 32))
     assert lib.rpt_probe_strategy_supported(99, 10) == 0
