@@ -515,10 +515,13 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 //   kSliceMergeAdaptive  this workgroup owns the slice: with >= kSliceWords/2 records it loads the slice
 //                        into LDS first and stores it back whole (read + write at the streaming rate),
 //                        with fewer it merges with atomics as above
+//   kSliceMergeStoreAll  the filter's words are still to be zeroed (rpt_bf_clear is deferred) and this
+//                        workgroup owns the slice: every 16-B piece is stored, zero or not, so the
+//                        insert is the clear (one pass over the filter instead of a memset and a store)
 // Memory-side atomics run at ~1.3 TB/s against ~6 TB/s for plain stores (MI355X_MICROARCH.md, Global
 // atomics): the C5 build's merge of an 8 GiB filter took 5.8 ms with atomics. Plain writes are safe
 // because the host orders every word-writing operation on a filter (rpt_bf::order_mu).
-constexpr int kSliceMergeAtomic = 0, kSliceMergeStore = 1, kSliceMergeAdaptive = 2;
+constexpr int kSliceMergeAtomic = 0, kSliceMergeStore = 1, kSliceMergeAdaptive = 2, kSliceMergeStoreAll = 3;
 __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* __restrict__ words, uint32_t splits,
                                                                     uint64_t n_tiles,
                                                                     const uint32_t* __restrict__ recs,
@@ -533,14 +536,18 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   const SliceWork sw = slice_work(xcd_item(blockIdx.x, gridDim.x), splits, n_tiles, bucket_tiles);
   const uint32_t slice = sw.slice;
   const uint64_t t_lo = sw.t_lo, t_hi = sw.t_hi;
-  if (t_lo >= t_hi) return;  // no rows reach this slice (uniform)
+  uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
+  u64x2* const dst2 = reinterpret_cast<u64x2*>(dst);
+  constexpr uint32_t kPieces = kSliceWords / 2;  // 16-B pieces of a slice
+  if (t_lo >= t_hi) {  // no rows reach this slice (uniform)
+    if (mode == kSliceMergeStoreAll)
+      for (uint32_t i = threadIdx.x; i < kPieces; i += kSliceThreads) dst2[i] = u64x2{0, 0};
+    return;
+  }
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kSliceThreads / 64;
   const uint32_t* my_runs = runs + static_cast<uint64_t>(sw.run_row) * n_tiles;
-  uint64_t* dst = words + static_cast<uint64_t>(slice) * kSliceWords;
   u64x2* const s_slice2 = reinterpret_cast<u64x2*>(s_slice);
-  u64x2* const dst2 = reinterpret_cast<u64x2*>(dst);
-  constexpr uint32_t kPieces = kSliceWords / 2;  // 16-B pieces of a slice
   bool rmw = false;
   if (mode == kSliceMergeAdaptive) {  // uniform: records this workgroup ORs into the slice
     uint32_t r = 0;
@@ -626,6 +633,8 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
       const u64x2 v = s_slice2[i];
       if ((v[0] | v[1]) != 0) dst2[i] = v;
     }
+  } else if (mode == kSliceMergeStoreAll) {
+    for (uint32_t i = threadIdx.x; i < kPieces; i += kSliceThreads) dst2[i] = s_slice2[i];
   } else {
     for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
       const uint64_t v = s_slice[i];

@@ -95,7 +95,8 @@ typedef struct rpt_bf_info {
   uint64_t sized_for_rows; /* PTBloomFilter::SizedForRows (bloom_filter.hpp:41-43) */
   int32_t has_data;        /* !PTBloomFilter::IsEmpty (bloom_filter.hpp:45-47) */
   int32_t finalized;       /* PTBloomFilter::finalized_ (bloom_filter.hpp:30) */
-  uint64_t* words;         /* device pointer to the blocks */
+  uint64_t* words;         /* device pointer to the blocks (after rpt_bf_clear they read as zero only once
+                              another operation on the filter has run: see rpt_bf_clear) */
 } rpt_bf_info;
 
 /* ---- library ---------------------------------------------------------------------------- */
@@ -147,7 +148,11 @@ int rpt_bf_probe_strategy(const rpt_bf* bf);
 int rpt_bf_probe_strategy_for(const rpt_bf* bf, uint64_t n_rows);
 int rpt_bf_insert_strategy_for(const rpt_bf* bf, uint64_t n_rows);
 size_t rpt_bf_probe_workspace_bytes(const rpt_bf* bf, uint64_t n_rows);
-/* Zero every block and clear has_data (stream-ordered). */
+/* Zero every block and clear has_data (stream-ordered). The zeroing is deferred to the next operation on
+ * the filter: a partitioned / bucketed insert that owns every slice stores the slices whole (so a rebuild
+ * is one pass over the filter, not a memset and then the insert's stores); any other insert, merge,
+ * probe, copy or export zeroes the words first, ordered like any other write. Only a direct read through
+ * rpt_bf_info::words can see the words before that. */
 int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
 
 /* ---- build ------------------------------------------------------------------------------- */
