@@ -217,6 +217,7 @@ def main():
 
     import rpt_amd
     from rpt_amd import _lib as rpt_lib
+    from rpt_amd._lib import RptError
     from rpt_amd.distributed import RcclComm, allreduce_or_filter, allreduce_or_native, shard_range
 
     cfg = args.config or ("C2" if args.build_rows is None and args.filter_rows is None else None)
@@ -256,7 +257,23 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     del build_keys
-    comm = RcclComm(device) if world > 1 and backend == "nccl" else None
+    comm, merge_path = None, "none (one GPU)" if world == 1 else "torch.distributed all_to_all + all_gather (gloo rehearsal)"
+    if world > 1 and backend == "nccl":
+        err = None
+        try:
+            comm = RcclComm(device)
+        except RptError as e:  # a rank-0 id failure raises on every rank together (RcclComm)
+            err = str(e)
+        ok = torch.tensor([0 if err else 1], dtype=torch.int64, device=device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same merge path
+        if ok.item():
+            merge_path = "rpt_bf_allreduce_or (C-ABI: RCCL grouped send/recv reduce-scatter, OR kernel, all-gather)"
+        else:
+            if comm is not None:
+                comm.close()
+                comm = None
+            merge_path = f"torch.distributed fallback: the native RCCL communicator failed ({err or 'on another rank'})"
+            print(f"[rank {rank}] {merge_path}", file=sys.stderr, flush=True)
     barrier()
     t1 = time.perf_counter() if world > 1 else t1
     if comm is not None:
@@ -418,6 +435,7 @@ def main():
                 "or_merge_GBps_per_gpu": (2 * (world - 1) / world * filter_bytes / merge_s / 1e9
                                           if world > 1 and merge_s > 0 else None),
                 "merge_check": merge_check,
+                "merge_path": merge_path,
             },
         }
         if not args.no_cpu_baseline and world == 1:

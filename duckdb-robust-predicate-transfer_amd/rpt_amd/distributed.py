@@ -78,22 +78,33 @@ class RcclComm:
     ID_BYTES = 128  # RPT_RCCL_UNIQUE_ID_BYTES
 
     def __init__(self, device: torch.device, group=None):
-        from ._lib import check, load
+        from ._lib import RptError, load
 
         self._lib = load()
+        self.handle = None
         self.device = torch.device(device)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        uid = torch.zeros(self.ID_BYTES, dtype=torch.uint8)
+        # id + a status byte: a rank-0 failure (e.g. RCCL not loadable) reaches every rank through the
+        # broadcast, so all ranks raise together instead of the others waiting in the init
+        uid = torch.zeros(self.ID_BYTES + 1, dtype=torch.uint8)
+        err = ""
         if self.rank == 0:
-            check(self._lib.rpt_rccl_get_unique_id(uid.data_ptr()))
+            st = self._lib.rpt_rccl_get_unique_id(uid.data_ptr())
+            if st != 0:
+                err = self._lib.rpt_last_error().decode(errors="replace")
+                uid[self.ID_BYTES] = 1
         on_device = dist.get_backend(group) != "gloo"
         t = uid.to(self.device) if on_device else uid
         dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         uid = t.cpu().contiguous()
+        if int(uid[self.ID_BYTES]) != 0:
+            raise RptError(7, f"rpt_rccl_get_unique_id failed on rank 0{': ' + err if err else ''}")
         h = ctypes.c_void_p()
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
-        check(self._lib.rpt_rccl_comm_init_rank(dev, self.world, uid.data_ptr(), self.rank, ctypes.byref(h)))
+        st = self._lib.rpt_rccl_comm_init_rank(dev, self.world, uid.data_ptr(), self.rank, ctypes.byref(h))
+        if st != 0:
+            raise RptError(st, self._lib.rpt_last_error().decode(errors="replace"))
         self.handle = h
 
     def close(self) -> None:

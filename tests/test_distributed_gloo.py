@@ -133,3 +133,57 @@ def test_minmax_and_flag_allreduce(world):
     else:
         expect = [((int(i64.min), 12), True), (None, True), (None, False), ((int(i64.max), int(i64.max)), True)]
     assert out == expect
+
+
+def _rccl_id_worker(rank, world, port, fail_rank0, q):
+    import sys
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rpt_amd import _lib
+        from rpt_amd.distributed import RcclComm
+
+        if fail_rank0 and rank == 0:
+            lib = _lib.load()
+
+            class Failing:  # rpt_rccl_get_unique_id refusing, as when RCCL cannot be loaded
+                def __getattr__(self, name):
+                    return getattr(lib, name)
+
+                @staticmethod
+                def rpt_rccl_get_unique_id(_ptr):
+                    return _lib.RPT_ERR_COLLECTIVE
+
+            _lib.load = lambda path=None: Failing()
+        try:
+            RcclComm(torch.device("cuda", 0))
+            q.put((rank, "ok"))
+        except _lib.RptError as e:
+            q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank0", [True, False])
+def test_rccl_comm_failure_reaches_every_rank(fail_rank0):
+    """RcclComm's id exchange carries rank 0's status: when rank 0 cannot draw an id every rank raises
+    (none is left waiting in the communicator init); without a GPU the init itself fails on every rank.
+    bench.py then takes the recorded torch.distributed merge on all ranks together."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rccl_id_worker, args=(r, world, port, fail_rank0, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(got) == [0, 1]
+    for msg in got.values():
+        assert msg != "ok"
+        if fail_rank0:
+            assert "failed on rank 0" in msg
