@@ -511,7 +511,9 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 //   kSliceMergeAtomic    LDS starts at zero; coalesced 64-bit device-scope atomic ORs of its non-zero
 //                        words (several workgroups per slice compose: OR is idempotent)
 //   kSliceMergeStore     the filter is all zero (rpt_bf::pristine) and this workgroup owns the slice:
-//                        LDS starts at zero, non-zero 16-B pieces leave as plain stores
+//                        LDS starts at zero, the slice leaves as plain stores (all of it: whole 128-B
+//                        lines; skipping the zero pieces left partial lines: 1e9 keys into a fresh
+//                        8 GiB filter 10.6-11.1 ms vs 9.4 ms, tools/build_modes.py)
 //   kSliceMergeAdaptive  this workgroup owns the slice: with >= kSliceWords/2 records it loads the slice
 //                        into LDS first and stores it back whole (read + write at the streaming rate),
 //                        with fewer it merges with atomics as above
@@ -521,6 +523,9 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 // Memory-side atomics run at ~1.3 TB/s against ~6 TB/s for plain stores (MI355X_MICROARCH.md, Global
 // atomics): the C5 build's merge of an 8 GiB filter took 5.8 ms with atomics. Plain writes are safe
 // because the host orders every word-writing operation on a filter (rpt_bf::order_mu).
+#ifndef RPT_EXP_STORE_SKIP_ZERO
+#define RPT_EXP_STORE_SKIP_ZERO 0
+#endif
 constexpr int kSliceMergeAtomic = 0, kSliceMergeStore = 1, kSliceMergeAdaptive = 2, kSliceMergeStoreAll = 3;
 __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* __restrict__ words, uint32_t splits,
                                                                     uint64_t n_tiles,
@@ -628,13 +633,12 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   __syncthreads();
   if (rmw) {
     for (uint32_t i = threadIdx.x; i < kPieces; i += kSliceThreads) dst2[i] = s_slice2[i];
-  } else if (mode == kSliceMergeStore) {
+  } else if (mode == kSliceMergeStore || mode == kSliceMergeStoreAll) {
     for (uint32_t i = threadIdx.x; i < kPieces; i += kSliceThreads) {
       const u64x2 v = s_slice2[i];
-      if ((v[0] | v[1]) != 0) dst2[i] = v;
+      if (RPT_EXP_STORE_SKIP_ZERO && mode == kSliceMergeStore && (v[0] | v[1]) == 0) continue;  // A/B only
+      dst2[i] = v;
     }
-  } else if (mode == kSliceMergeStoreAll) {
-    for (uint32_t i = threadIdx.x; i < kPieces; i += kSliceThreads) dst2[i] = s_slice2[i];
   } else {
     for (uint32_t i = threadIdx.x; i < kSliceWords; i += kSliceThreads) {
       const uint64_t v = s_slice[i];
