@@ -76,6 +76,15 @@ constexpr int kLdsProbeThreads = 1024;                 // whole-filter LDS probe
 #ifndef RPT_VALU_INTERLEAVE
 #define RPT_VALU_INTERLEAVE 1                          // store_segment_bits: bit interleave on VALU (lanes 0-7)
 #endif
+#ifndef RPT_SEL_BALLOT_EXPAND
+#define RPT_SEL_BALLOT_EXPAND 1                        // dense selection vectors written 64 rows at a time, contiguously
+#endif
+#ifndef RPT_SEL_BALLOT_MIN
+#define RPT_SEL_BALLOT_MIN 192                         // ... from this many survivors per 512 rows (unpermute_sel)
+#endif
+#ifndef RPT_COMPACT_BALLOT_MIN
+#define RPT_COMPACT_BALLOT_MIN 384                     // ... per 512 rows in compact_kernel (its sparse path stages in LDS)
+#endif
 #ifndef RPT_SLICE_UNROLL
 #define RPT_SLICE_UNROLL 4                             // 512-record steps in flight per wave
 #endif

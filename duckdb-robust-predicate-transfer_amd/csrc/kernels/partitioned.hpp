@@ -790,7 +790,7 @@ __global__ __launch_bounds__(kUnpermuteSelThreads<TM>) void unpermute_sel_kernel
     for (uint32_t i = threadIdx.x; i < tile_cap / 128; i += kThreads) reinterpret_cast<u32x4*>(s_pass)[i] = src[i];
   }
   __syncthreads();
-  uint32_t bytes[kSegsPerWave], excl[kSegsPerWave], run = 0;
+  uint32_t bytes[kSegsPerWave], excl[kSegsPerWave], segtot[kSegsPerWave], run = 0;
 #pragma unroll
   for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
     uint32_t byte = 0;
@@ -805,12 +805,48 @@ __global__ __launch_bounds__(kUnpermuteSelThreads<TM>) void unpermute_sel_kernel
     const uint32_t c = __popc(byte);
     const uint32_t inc = wave_inclusive_sum(c);
     excl[sg] = run + inc - c;
-    run += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
+    segtot[sg] = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(inc), 63));
+    run += segtot[sg];
   }
   if (lane == 0) s_wtot[wave] = run;
   __syncthreads();
   uint32_t woff = block_offs[tile / kTileBlock] + tile_pre[tile];
   for (uint32_t w = 0; w < wave; w++) woff += s_wtot[w];
+#if RPT_SEL_BALLOT_EXPAND
+  // Dense segments (>= RPT_SEL_BALLOT_MIN survivors of 512): row-ordered 64-row words (lane 8k + j holds
+  // byte j of word k; the bytes are ORed within each group of 8 lanes by DPP), expanded word by word
+  // so each store writes one contiguous run of survivors. Sparse segments: each lane writes its own
+  // survivors (fewer instructions when a lane has ~1). Measured (C2 unpermute_sel ms, p = 0.1 / 0.5 /
+  // 1.0): per-lane only 0.48 / 1.09 / 2.89, word-by-word only 0.65 / 0.80 / 1.15; C2 step at p = 0.25
+  // with the switch at 64 / 128 / 192 survivors: 4.12 / 4.10 / 4.08 ms (per-lane only 4.08).
+  uint32_t o = woff;
+#pragma unroll
+  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
+    if (segtot[sg] < RPT_SEL_BALLOT_MIN) {  // uniform
+      uint32_t b = bytes[sg], ol = woff + excl[sg];
+      const uint32_t row0 = static_cast<uint32_t>((seg0 + sg) * kSegRows) + lane * 8;
+      while (b) {
+        const uint32_t row = row0 + static_cast<uint32_t>(__builtin_ctz(b));
+        out_sel[ol++] = row_sel ? row_sel[row] : row;
+        b &= b - 1;
+      }
+      o += segtot[sg];
+      continue;
+    }
+    uint64_t v = static_cast<uint64_t>(bytes[sg]) << (8 * (lane & 7));
+    uint32_t lo = static_cast<uint32_t>(v), hi = static_cast<uint32_t>(v >> 32);
+    lo |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(lo), 0xB1, 0xf, 0xf, false));
+    hi |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(hi), 0xB1, 0xf, 0xf, false));
+    lo |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(lo), 0x4E, 0xf, 0xf, false));
+    hi |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(hi), 0x4E, 0xf, 0xf, false));
+    lo |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(lo), 0x141, 0xf, 0xf, false));
+    hi |= static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(hi), 0x141, 0xf, 0xf, false));
+    v = (static_cast<uint64_t>(hi) << 32) | lo;
+    const uint32_t row0 = static_cast<uint32_t>((seg0 + sg) * kSegRows);
+#pragma unroll
+    for (int k = 0; k < 8; k++) o += expand_word_sel(readlane64(v, 8 * k), row0 + 64 * k, lane, row_sel, out_sel + o);
+  }
+#else
 #pragma unroll
   for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
     uint32_t b = bytes[sg], o = woff + excl[sg];
@@ -821,5 +857,6 @@ __global__ __launch_bounds__(kUnpermuteSelThreads<TM>) void unpermute_sel_kernel
       b &= b - 1;
     }
   }
+#endif
 }
 }  // namespace rpt

@@ -129,6 +129,27 @@ __device__ __forceinline__ uint64_t spread4(uint64_t x) {
 __device__ __forceinline__ uint64_t ballot64(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+// Set bits of the wave-uniform mask w below this lane.
+__device__ __forceinline__ uint32_t mask_rank(uint64_t w) {
+  return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(w >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(w), 0u));
+}
+// Lane `src`'s 64-bit value, wave-uniform.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int src) {
+  const uint32_t lo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v)), src));
+  const uint32_t hi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(v >> 32)), src));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+// Selection-vector expansion of 64 rows whose pass bits are the wave-uniform word w (bit i = row
+// row0 + i): lane i writes row i's id at out[rank] if it passes, so one store instruction writes the
+// survivors as ONE contiguous run (full lines at high pass rates). Returns the survivor count.
+__device__ __forceinline__ uint32_t expand_word_sel(uint64_t w, uint32_t row0, uint32_t lane, const uint32_t* row_sel,
+                                                    uint32_t* out) {
+  if ((w >> lane) & 1ULL) {
+    const uint32_t row = row0 + lane;
+    out[mask_rank(w)] = row_sel ? row_sel[row] : row;
+  }
+  return static_cast<uint32_t>(__popcll(w));
+}
 
 // Inclusive wave-wide prefix sum of a 32-bit value (whole wave active). DPP: shifts within rows of 16,
 // then row broadcasts 15 / 31 -- six dependent VALU ops instead of six ds_bpermute round trips.

@@ -611,3 +611,31 @@ def test_direct_probe_pipelined_rounds_vs_oracle(rpt, strategy, dtype, n):
     bf.insert(dev(build))
     sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
     assert np.array_equal(sel, orc.probe_keys(w, lnb, probe))
+
+
+@pytest.mark.parametrize("strategy", ["gather", "partitioned", "bucketed"])
+@pytest.mark.parametrize("p", [400, 800, 1000])
+@pytest.mark.parametrize("use_row_sel", [False, True])
+def test_dense_selection_vectors_vs_oracle(rpt, strategy, p, use_row_sel):
+    """High pass rates take the word-by-word selection-vector expansion (unpermute_sel_kernel from 192
+    survivors per 512 rows, compact_kernel from 384): every sel entry against the oracle, ragged n, with
+    and without an incoming row selection."""
+    n_build, n, lnb = 300_000, 3_000_001, 22
+    bf = rpt.BloomFilter(log_num_blocks=lnb)
+    bf.probe_strategy = {"gather": 1, "partitioned": 3, "bucketed": 4}[strategy]
+    bf.insert(rpt.synth_build_keys(n_build))
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, orc.synth_build_keys(n_build))
+    probe = rpt.synth_probe_keys(n, n_build, p)
+    keys = probe.cpu().numpy()
+    if use_row_sel:
+        rng = np.random.default_rng(p)
+        rows = np.sort(rng.choice(n, size=n // 2, replace=False)).astype(np.uint32)
+        got = bf.lookup_sel(probe, row_sel=torch.from_numpy(rows.view(np.int32)).to("cuda:0"))
+        exp = rows[orc.probe_keys(w, lnb, keys, key_sel=rows)]
+    else:
+        got = bf.lookup_sel(probe)
+        exp = orc.probe_keys(w, lnb, keys)
+    got = got.cpu().numpy().view(np.uint32)
+    assert got.size >= (p / 1000) * (n // 2 if use_row_sel else n) * 0.99
+    assert np.array_equal(got, exp.astype(np.uint32))
