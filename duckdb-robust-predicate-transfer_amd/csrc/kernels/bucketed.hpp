@@ -181,8 +181,11 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
     const uint32_t used = s_cur[nb - 1];
     for (uint32_t i = threadIdx.x; i < used; i += kTileThreads) {
       const uint64_t d = s_dst[s_bk[i]] + i;
-      hash_lo[d] = s_lo[i];
-      hash_hi[d] = s_hi[i];
+#ifndef RPT_EXP_SCATTER_SKIP
+#define RPT_EXP_SCATTER_SKIP 0  // measurement only: 1 = no high-byte stores, 2 = no low-word stores, 3 = neither
+#endif
+      if (!(RPT_EXP_SCATTER_SKIP & 2)) hash_lo[d] = s_lo[i];
+      if (!(RPT_EXP_SCATTER_SKIP & 1)) hash_hi[d] = s_hi[i];
     }
   } else {
     for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {  // LDS only: no global latency in the chain
