@@ -203,6 +203,10 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
         poff += pad_run(c[i]);
       }
     }
+#ifndef RPT_EXP_PART_STOP
+#define RPT_EXP_PART_STOP 0  // measurement only: 1 = stop after pass 1 + the scans, 2 = after the scatter
+#endif
+    if (RPT_EXP_PART_STOP == 1) return;
     // pass 2: pull this thread's records back out of the row-ordered staging ...
     uint32_t rec[kRPT];
 #pragma unroll
@@ -271,6 +275,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
       }
     }
     __syncthreads();
+    if (RPT_EXP_PART_STOP == 2) return;
     // records of the tile in the padded layout, 16 B per thread and step (pad slots hold stale values:
     // probed, never read back); the scatter left s_cur[i] = start_i + count_i
     u32x4* dst = reinterpret_cast<u32x4*>(recs + tile * tile_cap);
