@@ -74,8 +74,8 @@ __device__ __forceinline__ uint64_t block_of(uint64_t h, uint64_t block_mask) {
 }
 
 // Key types (rpt_key_type), plus kKeySplit: the bucketed strategy's level-2 input, the low 32 bits
-// of each row's hash (keys) with hash bits 32..39 in a parallel byte array (KeyArgs::hi8) -- the 37
-// bits a 16 MiB bucket's slices need, in 5 bytes instead of 8.
+// of each row's hash (keys) with hash bits 32..39 in a parallel byte array (KeyArgs::hi8) -- the 38
+// bits a 32 MiB bucket's slices need, in 5 bytes instead of 8.
 enum KeyKind : int { kKeyI64 = 0, kKeyI32 = 1, kKeyHash = 2, kKeySplit = 3 };
 
 template <int K> struct KeyTraits;
