@@ -155,7 +155,7 @@ def test_bucketed_skewed_keys(rpt):
 
 def test_c5_geometry_8gib_filter_vs_oracle(rpt):
     """BASELINE C5's single-rank geometry: a filter sized for 8e9 rows = 2^30 blocks
-    (8 GiB), 512 level-1 buckets of 128 slices. Bucketed insert of 1.2e7 keys and bucketed probes of
+    (8 GiB), 256 level-1 buckets of 256 slices. Bucketed insert of 1.2e7 keys and bucketed probes of
     1.2e7 rows (flat, with a NULL pattern, through a row selection), each against the oracle: every word
     of the 8 GiB filter and every sel entry."""
     log_nb = 30
@@ -191,6 +191,37 @@ def test_c5_geometry_8gib_filter_vs_oracle(rpt):
     ref_r = row_sel[orc.probe_keys(w, log_nb, probe, key_sel=row_sel)]
     sel_r = bf.lookup_sel(dprobe, row_sel=dev(row_sel)).cpu().numpy().astype(np.uint32)
     assert np.array_equal(sel_r, ref_r)
+
+
+@pytest.mark.timeout(300)
+def test_max_bucketed_geometry_16gib_vs_oracle(rpt):
+    """The largest filter the bucketed strategy takes: 2^31 blocks (16 GiB), 512 level-1 buckets. A
+    rebuild (clear, then a bucketed insert that stores every slice whole) of 2e7 keys and a bucketed
+    probe of 2e7 rows, against the oracle: every filter word and every sel entry."""
+    log_nb = 31
+    from rpt_amd import _lib
+
+    assert _lib.load().rpt_probe_strategy_supported(BUCKETED, log_nb) == 1
+    assert _lib.load().rpt_probe_strategy_supported(BUCKETED, log_nb + 1) == 0
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    n_build, n_probe = 20_000_000, 20_000_000
+    bf.insert(dev(orc.synth_build_keys(1000, start=7 * 10**9)))  # then rebuilt: nothing of it may survive
+    bf.clear()
+    build = orc.synth_build_keys(n_build, start=9 * 10**9)
+    bf.insert(dev(build), strategy=INS_BUCKETED)
+    w = oracle_filter(log_nb, build)
+    got = torch.empty(bf.num_blocks, dtype=torch.int64, device="cuda:0")
+    bf.copy_words_to(got)
+    assert torch.equal(got, torch.from_numpy(w.view(np.int64)).to("cuda:0")), "16 GiB filter words differ"
+    del got
+    torch.cuda.empty_cache()
+    probe = orc.synth_probe_keys(n_probe, n_build, 300, start=11 * 10**9)
+    probe[::5] = build[: probe[::5].size]
+    bf.probe_strategy = BUCKETED
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
+    ref = orc.probe_keys(w, log_nb, probe)
+    assert ref.size > n_probe // 5
+    assert np.array_equal(sel, ref)
 
 
 @pytest.mark.parametrize("strategy", [INS_PARTITIONED, INS_BUCKETED])
