@@ -434,6 +434,10 @@ def main():
                 # per-GPU xGMI bytes of the OR all-reduce: 2 (W-1)/W of the filter
                 "or_merge_GBps_per_gpu": (2 * (world - 1) / world * filter_bytes / merge_s / 1e9
                                           if world > 1 and merge_s > 0 else None),
+                # the merge is direct point-to-point (every rank sends its 1/W slices to every peer, twice):
+                # each of a GPU's W-1 xGMI links carries 2 S / W of it (GB/s per link)
+                "or_merge_GBps_per_link": (2 / world * filter_bytes / merge_s / 1e9
+                                           if world > 1 and merge_s > 0 else None),
                 "merge_check": merge_check,
                 "merge_path": merge_path,
             },
