@@ -19,8 +19,9 @@ The build rows are split by row range, each rank's partial filter (sized for the
 is OR-merged through the C-ABI's rpt_bf_allreduce_or over an RCCL communicator the library creates
 (the product path a C++ caller gets), checked bit-identical to a single-GPU build of all rows, and
 every rank probes its own 1e9-row slice of the global probe column (weak scaling, no data-path
-collective in the probe). RPT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (the merge then
-runs the torch.distributed composition over host memory).
+collective in the probe). A communicator that cannot be built ends the run with a non-zero exit on
+every rank. RPT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (the merge then runs the
+torch.distributed composition over host memory, reported as torch_merge_ms).
 
 Prints ONE JSON line on rank 0. `roofline` prices the dominant kernel from HIP events the library
 records on the launch stream (rpt_profiling_*) and its PMC traffic from profiles/pmc/<config>.json
@@ -83,6 +84,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "0")) or None,
                     help="CPU-baseline threads (default: this process's CPU share, see cpu_share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--merge", default="native", choices=["native", "torch"],
+                    help="N > 1: the product merge rpt_bf_allreduce_or_ws over RCCL (default; a failing "
+                         "communicator exits non-zero), or the torch.distributed composition (reported as "
+                         "torch_merge_ms, not or_merge_ms)")
     ap.add_argument("--no-merge-check", action="store_true",
                     help="skip the (untimed) bit-identity check of the OR-merged filter (N > 1)")
     ap.add_argument("--key-type", default="i64", choices=["i64", "i32"],
@@ -218,7 +223,7 @@ def main():
     import rpt_amd
     from rpt_amd import _lib as rpt_lib
     from rpt_amd._lib import RptError
-    from rpt_amd.distributed import RcclComm, allreduce_or_filter, allreduce_or_native, shard_range
+    from rpt_amd.distributed import RcclComm, allreduce_or_filter, allreduce_or_native, allreduce_workspace, shard_range
 
     cfg = args.config or ("C2" if args.build_rows is None and args.filter_rows is None else None)
     n_probe = int(args.probe_rows)
@@ -257,31 +262,34 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     del build_keys
-    comm, merge_path = None, "none (one GPU)" if world == 1 else "torch.distributed all_to_all + all_gather (gloo rehearsal)"
-    if world > 1 and backend == "nccl":
-        err = None
+    # The product merge is rpt_bf_allreduce_or_ws over a library-made RCCL communicator. A failing
+    # communicator ends the run (non-zero exit on every rank): a merge time is only ever reported for
+    # the product path. `--merge torch` (or the gloo rehearsal) times the torch.distributed composition
+    # instead, reported as torch_merge_ms, never as or_merge_ms.
+    comm, merge_ws = None, None
+    native = world > 1 and backend == "nccl" and args.merge == "native"
+    merge_path = ("none (one GPU)" if world == 1 else
+                  "rpt_bf_allreduce_or_ws (C-ABI: RCCL grouped send/recv reduce-scatter in 32 MiB rounds, OR kernel "
+                  "on a helper stream, all-gather)" if native else
+                  f"torch.distributed all_to_all + all_gather ({'--merge torch' if backend == 'nccl' else 'gloo rehearsal'})")
+    if native:
         try:
-            comm = RcclComm(device)
-        except RptError as e:  # a rank-0 id failure raises on every rank together (RcclComm)
-            err = str(e)
-        ok = torch.tensor([0 if err else 1], dtype=torch.int64, device=device)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # every rank takes the same merge path
-        if ok.item():
-            merge_path = "rpt_bf_allreduce_or (C-ABI: RCCL grouped send/recv reduce-scatter, OR kernel, all-gather)"
-        else:
-            if comm is not None:
-                comm.close()
-                comm = None
-            merge_path = f"torch.distributed fallback: the native RCCL communicator failed ({err or 'on another rank'})"
-            print(f"[rank {rank}] {merge_path}", file=sys.stderr, flush=True)
+            comm = RcclComm(device)  # every rank checks RCCL first and all agree: they fail together
+        except RptError as e:
+            print(f"[rank {rank}] native RCCL communicator failed: {e}", file=sys.stderr, flush=True)
+            dist.destroy_process_group()
+            sys.exit(3)
+        merge_ws = allreduce_workspace(bf, comm)  # bounded staging, allocated outside the timed merge
+    torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter() if world > 1 else t1
     if comm is not None:
-        allreduce_or_native(bf, comm)  # rpt_bf_allreduce_or (C-ABI), the product merge
+        allreduce_or_native(bf, comm, workspace=merge_ws)  # rpt_bf_allreduce_or_ws (C-ABI), the product merge
     elif world > 1:
-        allreduce_or_filter(bf)  # gloo rehearsal
+        allreduce_or_filter(bf)  # torch.distributed composition
     torch.cuda.synchronize()
     t2 = time.perf_counter()
+    merge_ws = None
     bf.finalized = True
     merge_check = None
     if world > 1 and not args.no_merge_check:
@@ -430,14 +438,16 @@ def main():
                 "rows": n_build,
                 "insert_ms": insert_s * 1e3,
                 "insert_keys_per_s": (n_build / world) / insert_s if insert_s > 0 else None,
-                "or_merge_ms": merge_s * 1e3,
+                # the product merge only (rpt_bf_allreduce_or_ws; workspace allocated before the timer)
+                "or_merge_ms": merge_s * 1e3 if comm is not None else None,
+                "torch_merge_ms": merge_s * 1e3 if world > 1 and comm is None else None,
                 # per-GPU xGMI bytes of the OR all-reduce: 2 (W-1)/W of the filter
                 "or_merge_GBps_per_gpu": (2 * (world - 1) / world * filter_bytes / merge_s / 1e9
-                                          if world > 1 and merge_s > 0 else None),
+                                          if comm is not None and merge_s > 0 else None),
                 # the merge is direct point-to-point (every rank sends its 1/W slices to every peer, twice):
                 # each of a GPU's W-1 xGMI links carries 2 S / W of it (GB/s per link)
                 "or_merge_GBps_per_link": (2 / world * filter_bytes / merge_s / 1e9
-                                           if world > 1 and merge_s > 0 else None),
+                                           if comm is not None and merge_s > 0 else None),
                 "merge_check": merge_check,
                 "merge_path": merge_path,
             },

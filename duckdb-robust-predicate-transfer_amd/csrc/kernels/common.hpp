@@ -3,6 +3,14 @@
 // stay together without relocatable device code).
 #pragma once
 
+// Measurement-only macros (RPT_EXP_*) make kernels skip work, i.e. return WRONG results: they exist for
+// the A/B variants tools/build_variants.sh builds under other names (build/variants/). The product build
+// (Makefile: RPT_PRODUCT_BUILD, which HIPFLAGS cannot drop) refuses them.
+#if defined(RPT_PRODUCT_BUILD) && (defined(RPT_EXP_PART_STOP) || defined(RPT_EXP_SCATTER_SKIP) || \
+                                   defined(RPT_EXP_STORE_SKIP_ZERO) || defined(RPT_EXP_NO_PASS_WRITE))
+#error "RPT_EXP_* measurement macros are not allowed in the product build (use tools/build_variants.sh)"
+#endif
+
 namespace rpt {
 
 constexpr int kBlockThreads = 256;

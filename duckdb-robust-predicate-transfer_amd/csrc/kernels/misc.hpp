@@ -53,17 +53,19 @@ __global__ __launch_bounds__(kBlockThreads) void hash_kernel(KeyArgs a, uint64_t
 // ---- k4: OR merge --------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlockThreads) void or_slices_kernel(uint64_t* __restrict__ dst,
                                                                  const uint64_t* __restrict__ srcs, uint32_t k,
-                                                                 uint64_t n_words, int accumulate) {
+                                                                 uint64_t n_words, uint64_t src_stride,
+                                                                 int accumulate) {
+  // srcs: k slices of n_words words, slice s at srcs + s * src_stride (dst and every slice 16-B aligned)
   const uint64_t n_pairs = n_words / 2;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_pairs; i += stride) {
     u64x2 acc = accumulate ? reinterpret_cast<const u64x2*>(dst)[i] : u64x2{0, 0};
-    for (uint32_t s = 0; s < k; s++) acc |= reinterpret_cast<const u64x2*>(srcs + s * n_words)[i];
+    for (uint32_t s = 0; s < k; s++) acc |= reinterpret_cast<const u64x2*>(srcs + s * src_stride)[i];
     reinterpret_cast<u64x2*>(dst)[i] = acc;
   }
   if ((n_words & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
     uint64_t acc = accumulate ? dst[n_words - 1] : 0ULL;
-    for (uint32_t s = 0; s < k; s++) acc |= srcs[s * n_words + n_words - 1];
+    for (uint32_t s = 0; s < k; s++) acc |= srcs[s * src_stride + n_words - 1];
     dst[n_words - 1] = acc;
   }
 }

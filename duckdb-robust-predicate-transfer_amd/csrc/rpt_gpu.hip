@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <list>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -33,6 +34,7 @@
 #include "rpt_bloom_device.hpp"
 #include "rpt_gpu.h"
 #include "rpt_gpu_synth.h"
+#include "rpt_gpu_testing.h"  // the RCCL entry-point table type; its setter exists in the test build only
 
 #include "kernels/common.hpp"
 #include "kernels/probe_direct.hpp"
@@ -68,6 +70,10 @@ struct rpt_bf {
   // (settle_for_read / zero_pending_locked; an insert that stores every slice whole does it as part of
   // its stores). Written under order_mu; readers test it without the lock first.
   std::atomic<bool> clear_pending{false};
+  // A reader that settled the clear recorded zero_ev after its memset: readers on other streams wait on
+  // it (no host sync) until it has completed (zero_unsynced then drops).
+  hipEvent_t zero_ev = nullptr;
+  std::atomic<bool> zero_unsynced{false};
 };
 
 namespace {
@@ -216,19 +222,31 @@ hipError_t zero_pending_locked(rpt_bf* bf, hipStream_t s) {
   return e;
 }
 
-// ... and by a reader: zero the words as an ordered write on the reader's stream and wait for it, so a
-// reader on another stream that finds the flag already settled cannot overtake the zeroing. (Reading a
-// cleared filter before any insert is rare: the fast path is one atomic load.)
+// ... and by a reader: zero the words as an ordered write on the reader's stream and record zero_ev after
+// the memset, so a reader on another stream that finds the clear already settled waits for that event
+// instead of overtaking the zeroing (no host synchronization: legal under stream capture). Reading a
+// cleared filter before any insert is rare: the fast path is two atomic loads.
 int settle_for_read(const rpt_bf* cbf, hipStream_t s) {
   rpt_bf* bf = const_cast<rpt_bf*>(cbf);
-  if (!bf->clear_pending.load()) return RPT_OK;
-  WriteOrder order(bf, s);
-  if (!bf->clear_pending.load()) return RPT_OK;  // settled by another thread meanwhile (in order)
-  const hipError_t e = zero_pending_locked(bf, s);
-  order.done(true);
-  if (e != hipSuccess) return fail(RPT_ERR_HIP, "hipMemsetAsync failed: %s", hipGetErrorString(e));
-  const hipError_t e2 = hipStreamSynchronize(s);
-  if (e2 != hipSuccess) return fail(RPT_ERR_HIP, "hipStreamSynchronize failed: %s", hipGetErrorString(e2));
+  if (!bf->clear_pending.load() && !bf->zero_unsynced.load()) return RPT_OK;
+  std::lock_guard<std::mutex> lk(bf->order_mu);
+  if (bf->clear_pending.load()) {
+    if (bf->order_pending) RPT_HIP(hipStreamWaitEvent(s, bf->order_ev, 0));
+    RPT_HIP(hipMemsetAsync(bf->words, 0, (1ULL << bf->log_num_blocks) * 8, s));
+    if (!bf->zero_ev) RPT_HIP(hipEventCreateWithFlags(&bf->zero_ev, hipEventDisableTiming));
+    if (!bf->order_ev) RPT_HIP(hipEventCreateWithFlags(&bf->order_ev, hipEventDisableTiming));
+    RPT_HIP(hipEventRecord(bf->zero_ev, s));
+    RPT_HIP(hipEventRecord(bf->order_ev, s));  // later writes are ordered after the zeroing too
+    bf->order_pending = true;
+    bf->pristine = true;
+    bf->zero_unsynced.store(true);  // before the flag drops: a reader seeing neither may skip both
+    bf->clear_pending.store(false);
+    return RPT_OK;
+  }
+  if (bf->zero_unsynced.load()) {
+    if (hipEventQuery(bf->zero_ev) == hipSuccess) bf->zero_unsynced.store(false);
+    else RPT_HIP(hipStreamWaitEvent(s, bf->zero_ev, 0));
+  }
   return RPT_OK;
 }
 #define RPT_SETTLE(bf, s)                        \
@@ -879,6 +897,7 @@ int rpt_bf_destroy(rpt_bf* bf) {
     if (bf->words) (void)hipFree(bf->words);
     if (bf->stats) (void)hipFree(bf->stats);
     if (bf->order_ev) (void)hipEventDestroy(bf->order_ev);
+    if (bf->zero_ev) (void)hipEventDestroy(bf->zero_ev);
   }
   delete bf;
   return RPT_OK;
@@ -911,6 +930,7 @@ int rpt_bf_reinitialize(rpt_bf* bf, uint64_t actual_rows) {
   bf->order_pending = false;  // the device is idle
   bf->pristine = true;
   bf->clear_pending.store(false);  // alloc_words zeroed the new words
+  bf->zero_unsynced.store(false);
   return RPT_OK;
 }
 
@@ -1032,6 +1052,13 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   InsertWorkspace ws;
   insert_workspace_layout(n, L, strategy, workspace, &ws);
   hipStream_t s = as_stream(stream);
+  // the first kernels below fold the keys' min/max into bf->stats: they must land after the filter's
+  // previous write (e.g. a clear's stats reset enqueued on another stream), so wait for its event now;
+  // only the slice merge at the end takes the write order for the words
+  {
+    std::lock_guard<std::mutex> lk(bf->order_mu);
+    if (bf->order_pending) RPT_HIP(hipStreamWaitEvent(s, bf->order_ev, 0));
+  }
   const int cus = num_cus(bf->device);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
   const bool dense = dense_ok(col, nullptr);
@@ -1354,7 +1381,7 @@ int rpt_words_or_slices(uint64_t* dst, const uint64_t* srcs, uint32_t k, uint64_
   const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n_words / 2, rpt::kBlockThreads), 8192)));
   ProfScope prof12_("or_slices_kernel", as_stream(stream));
   hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), dst, srcs, k,
-                     n_words, 0);
+                     n_words, n_words, 0);
   prof12_.end();
   RPT_LAUNCHED("or_slices_kernel");
   return RPT_OK;
@@ -1366,7 +1393,7 @@ int rpt_words_or(uint64_t* dst, const uint64_t* src, uint64_t n_words, rpt_strea
   const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(n_words / 2, rpt::kBlockThreads), 8192)));
   ProfScope prof13_("or_slices_kernel", as_stream(stream));
   hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, as_stream(stream), dst, src, 1u,
-                     n_words, 1);
+                     n_words, n_words, 1);
   prof13_.end();
   RPT_LAUNCHED("or_slices_kernel");
   return RPT_OK;
@@ -1383,10 +1410,14 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
   const hipError_t ez = zero_pending_locked(dst, as_stream(stream));
   if (ez != hipSuccess) return fail(RPT_ERR_HIP, "hipMemsetAsync failed: %s", hipGetErrorString(ez));
   int st = rpt_words_or(dst->words, src->words, 1ULL << dst->log_num_blocks, stream);
+  if (st == RPT_OK) {
+    // inside the write order: a later clear's stats reset must not be overtaken by this merge
+    hipLaunchKernelGGL(stats_merge_kernel, dim3(1), dim3(1), 0, as_stream(stream), dst->stats, src->stats);
+    const hipError_t el = hipGetLastError();
+    if (el != hipSuccess) st = fail(RPT_ERR_HIP, "launch of stats_merge_kernel failed: %s", hipGetErrorString(el));
+  }
   order.done(false);
   if (st != RPT_OK) return st;
-  hipLaunchKernelGGL(stats_merge_kernel, dim3(1), dim3(1), 0, as_stream(stream), dst->stats, src->stats);
-  RPT_LAUNCHED("stats_merge_kernel");
   if (src->has_data.load()) dst->has_data.store(1);
   return RPT_OK;
 }
@@ -1396,53 +1427,51 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
 namespace {
 // The RCCL entry points rpt_bf_allreduce_or uses, resolved from librccl on first use (rccl.h types:
 // ncclResult_t = int, ncclComm_t = opaque pointer, ncclDataType_t / ncclRedOp_t = int enums).
-struct RcclUniqueId {
-  char internal[RPT_RCCL_UNIQUE_ID_BYTES];  // rccl.h ncclUniqueId (passed by value to ncclCommInitRank)
-};
 struct RcclApi {
-  int (*get_unique_id)(RcclUniqueId*) = nullptr;
-  int (*comm_init_rank)(void**, int, RcclUniqueId, int) = nullptr;
-  int (*comm_destroy)(void*) = nullptr;
-  int (*group_start)() = nullptr;
-  int (*group_end)() = nullptr;
-  int (*send)(const void*, size_t, int, int, void*, hipStream_t) = nullptr;
-  int (*recv)(void*, size_t, int, int, void*, hipStream_t) = nullptr;
-  int (*all_reduce)(const void*, void*, size_t, int, int, void*, hipStream_t) = nullptr;
-  int (*comm_count)(void*, int*) = nullptr;
-  int (*comm_user_rank)(void*, int*) = nullptr;
-  const char* (*error_string)(int) = nullptr;
+  rpt_rccl_api_table fn{};
   std::string load_error;
 };
 constexpr int kNcclInt64 = 4, kNcclUint64 = 5, kNcclMin = 3;  // rccl.h ncclDataType_t / ncclRedOp_t
-const RcclApi& rccl_api() {
-  static const RcclApi api = [] {
-    RcclApi a;
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
-    if (!h) {
-      const char* e = dlerror();
-      a.load_error = e ? e : "dlopen(librccl) failed";
-      return a;
-    }
-    auto sym = [&](auto& fn, const char* name) {
-      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
-      if (!fn && a.load_error.empty()) a.load_error = std::string("librccl lacks ") + name;
-    };
-    sym(a.get_unique_id, "ncclGetUniqueId");
-    sym(a.comm_init_rank, "ncclCommInitRank");
-    sym(a.comm_destroy, "ncclCommDestroy");
-    sym(a.group_start, "ncclGroupStart");
-    sym(a.group_end, "ncclGroupEnd");
-    sym(a.send, "ncclSend");
-    sym(a.recv, "ncclRecv");
-    sym(a.all_reduce, "ncclAllReduce");
-    sym(a.comm_count, "ncclCommCount");
-    sym(a.comm_user_rank, "ncclCommUserRank");
-    sym(a.error_string, "ncclGetErrorString");
+
+std::shared_ptr<const RcclApi> load_librccl() {
+  auto a = std::make_shared<RcclApi>();
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    const char* e = dlerror();
+    a->load_error = e ? e : "dlopen(librccl) failed";
     return a;
-  }();
-  return api;
+  }
+  auto sym = [&](auto& fn, const char* name) {
+    fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+    if (!fn && a->load_error.empty()) a->load_error = std::string("librccl lacks ") + name;
+  };
+  sym(a->fn.get_unique_id, "ncclGetUniqueId");
+  sym(a->fn.comm_init_rank, "ncclCommInitRank");
+  sym(a->fn.comm_destroy, "ncclCommDestroy");
+  sym(a->fn.group_start, "ncclGroupStart");
+  sym(a->fn.group_end, "ncclGroupEnd");
+  sym(a->fn.send, "ncclSend");
+  sym(a->fn.recv, "ncclRecv");
+  sym(a->fn.all_reduce, "ncclAllReduce");
+  sym(a->fn.comm_count, "ncclCommCount");
+  sym(a->fn.comm_user_rank, "ncclCommUserRank");
+  sym(a->fn.error_string, "ncclGetErrorString");
+  return a;
 }
+
+// librccl; the test build (RPT_TESTING_HOOKS, csrc/rpt_gpu_testing.h) can swap in a loopback table.
+std::mutex g_rccl_mu;
+std::shared_ptr<const RcclApi> g_rccl, g_librccl;
+std::shared_ptr<const RcclApi> rccl_api() {
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  if (!g_rccl) {
+    if (!g_librccl) g_librccl = load_librccl();
+    g_rccl = g_librccl;
+  }
+  return g_rccl;
+}
+
 // {min, max, has_data} -> {min, ~max, ~has}: bit complement reverses the order without overflow, so one
 // MIN all-reduce gives the global min, max and has_data (an empty partial holds {INT64_MAX, INT64_MIN}).
 __global__ void minmax_pack_kernel(const int64_t* stats, int has, int64_t* v) {
@@ -1454,6 +1483,67 @@ __global__ void minmax_unpack_kernel(const int64_t* v, int64_t* stats, int* has)
   stats[0] = v[0];
   stats[1] = ~v[1];
   *has = static_cast<int>(~v[2]);
+}
+
+// Word ranges of the OR all-reduce: rank j owns words [lo(j), lo(j + 1)), starts rounded down to 32 words
+// (256 B) so every slice, and every round's piece of it, is 16-B aligned for the OR kernel; the last rank
+// takes the rest. The reduce-scatter runs in rounds of at most `round` words per peer (the staging bound);
+// every rank derives the same round count, so the grouped sends and receives pair up round by round.
+struct MergeGeom {
+  uint64_t nw;
+  int world;
+  uint64_t lo(int j) const { return j >= world ? nw : ((nw * static_cast<uint64_t>(j)) / world) & ~31ULL; }
+  uint64_t len(int j) const { return lo(j + 1) - lo(j); }
+  uint64_t max_len() const {
+    uint64_t m = 0;
+    for (int j = 0; j < world; j++) m = std::max(m, len(j));
+    return m;
+  }
+  uint64_t round_words() const { return std::max<uint64_t>(2, std::min<uint64_t>(RPT_ALLREDUCE_ROUND_WORDS, (max_len() + 1) & ~1ULL)); }
+  uint64_t rounds() const { return ceil_div(max_len(), round_words()); }
+  // words of slice j sent in round r
+  uint64_t piece(int j, uint64_t r) const {
+    const uint64_t R = round_words(), l = len(j);
+    return r * R >= l ? 0 : std::min(R, l - r * R);
+  }
+  // workspace: {min, ~max, ~has, has} scratch, then two staging buffers of (world - 1) round pieces
+  size_t workspace_bytes() const {
+    return 256 + (world > 1 ? 2 * static_cast<size_t>(world - 1) * round_words() * 8 : 0);
+  }
+};
+
+// A helper stream + events per concurrent all-reduce: the OR kernel of round r runs there while the
+// transfers of round r + 1 run on the caller's stream. Pooled per device (never destroyed).
+struct MergeHelper {
+  int device;
+  hipStream_t s = nullptr;
+  hipEvent_t rx[2] = {nullptr, nullptr}, ored[2] = {nullptr, nullptr}, join = nullptr;
+};
+std::mutex g_helper_mu;
+std::vector<MergeHelper*> g_helper_free;
+MergeHelper* take_helper(int device) {
+  {
+    std::lock_guard<std::mutex> lk(g_helper_mu);
+    for (size_t i = 0; i < g_helper_free.size(); i++)
+      if (g_helper_free[i]->device == device) {
+        MergeHelper* h = g_helper_free[i];
+        g_helper_free.erase(g_helper_free.begin() + static_cast<long>(i));
+        return h;
+      }
+  }
+  auto* h = new MergeHelper{device};
+  bool ok = hipStreamCreateWithFlags(&h->s, hipStreamNonBlocking) == hipSuccess;
+  for (hipEvent_t* e : {&h->rx[0], &h->rx[1], &h->ored[0], &h->ored[1], &h->join})
+    ok = ok && hipEventCreateWithFlags(e, hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    (void)hipGetLastError();
+    return nullptr;  // leaks what was created: only after a HIP failure
+  }
+  return h;
+}
+void give_helper(MergeHelper* h) {
+  std::lock_guard<std::mutex> lk(g_helper_mu);
+  g_helper_free.push_back(h);
 }
 }  // namespace
 extern "C" {
@@ -1473,54 +1563,85 @@ extern "C" {
     }                                                                                          \
   } while (0)
 
-int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
+size_t rpt_allreduce_workspace_bytes(int world, int log_num_blocks) {
+  if (world < 1 || log_num_blocks < 0 || log_num_blocks > 40) return 0;
+  return MergeGeom{1ULL << log_num_blocks, world}.workspace_bytes();
+}
+
+int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t workspace_bytes,
+                           rpt_stream_t stream) {
   if (!bf || !nccl_comm) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
-  const RcclApi& api = rccl_api();
-  if (!api.load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api.load_error.c_str());
+  const std::shared_ptr<const RcclApi> api_p = rccl_api();
+  const rpt_rccl_api_table& api = api_p->fn;
+  if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
   RPT_ON_DEVICE(bf->device);
   hipStream_t s = as_stream(stream);
   int world = 1, me = 0;
   RPT_NCCL(api.comm_count(nccl_comm, &world));
   RPT_NCCL(api.comm_user_rank(nccl_comm, &me));
-  const uint64_t nw = 1ULL << bf->log_num_blocks;
-  auto lo = [&](int j) { return nw * static_cast<uint64_t>(j) / static_cast<uint64_t>(world); };
-  uint64_t* tmp = nullptr;
-  int64_t* v = nullptr;  // {min, ~max, ~has} then has_data (as int) in v[3]
-  const uint64_t mine = lo(me + 1) - lo(me);
-  const size_t tmp_bytes = world > 1 ? (static_cast<size_t>(world) - 1) * mine * 8 : 0;
-  if (hipMalloc(&v, 4 * sizeof(int64_t) + tmp_bytes) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(RPT_ERR_OUT_OF_MEMORY, "allreduce staging of %zu bytes", tmp_bytes);
-  }
-  tmp = reinterpret_cast<uint64_t*>(v + 4);
+  const MergeGeom g{1ULL << bf->log_num_blocks, world};
+  if (!workspace || workspace_bytes < g.workspace_bytes())
+    return fail(RPT_ERR_WORKSPACE, "all-reduce workspace %zu bytes < required %zu", workspace_bytes, g.workspace_bytes());
+  int64_t* v = static_cast<int64_t*>(workspace);  // {min, ~max, ~has} then has_data (as int) in v[3]
+  uint64_t* stage = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + 256);
+  MergeHelper* h = nullptr;
   WriteOrder order(bf, s);
   if (zero_pending_locked(bf, s) != hipSuccess) {
     order.done(false);
-    (void)hipFree(v);
     return fail(RPT_ERR_HIP, "hipMemsetAsync failed");
   }
+  bool helper_pending = false;  // OR kernels enqueued on the helper stream and not yet joined into s
+  auto join_helper = [&]() -> hipError_t {
+    if (!helper_pending) return hipSuccess;
+    helper_pending = false;
+    hipError_t e = hipEventRecord(h->join, h->s);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s, h->join, 0);
+    return e;
+  };
   auto run = [&]() -> int {
     if (world > 1) {
-      // reduce-scatter by OR: rank `me` owns words [lo(me), lo(me + 1)); peers' copies land in tmp
-      RPT_NCCL(api.group_start());
-      for (int p = 0, k = 0; p < world; p++) {
-        if (p == me) continue;
-        RPT_NCCL_IN_GROUP(api.send(bf->words + lo(p), lo(p + 1) - lo(p), kNcclUint64, p, nccl_comm, s));
-        RPT_NCCL_IN_GROUP(api.recv(tmp + static_cast<uint64_t>(k++) * mine, mine, kNcclUint64, p, nccl_comm, s));
+      h = take_helper(bf->device);
+      if (!h) return fail(RPT_ERR_HIP, "all-reduce helper stream creation failed");
+      const uint64_t R = g.round_words(), nr = g.rounds();
+      bool ored[2] = {false, false};
+      // reduce-scatter by OR: rank `me` owns words [lo(me), lo(me + 1)); in round r every peer sends its
+      // r-th piece of that range into staging buffer r % 2, and the OR kernel folds the pieces in on the
+      // helper stream while round r + 1 transfers
+      for (uint64_t r = 0; r < nr; r++) {
+        const int b = static_cast<int>(r & 1);
+        uint64_t* buf = stage + static_cast<uint64_t>(b) * (world - 1) * R;
+        const uint64_t cnt = g.piece(me, r), stride = (cnt + 1) & ~1ULL;
+        if (ored[b]) RPT_HIP(hipStreamWaitEvent(s, h->ored[b], 0));  // round r - 2's OR has read buf
+        RPT_NCCL(api.group_start());
+        for (int p = 0, k = 0; p < world; p++) {
+          if (p == me) continue;
+          const uint64_t out = g.piece(p, r);
+          if (out) RPT_NCCL_IN_GROUP(api.send(bf->words + g.lo(p) + r * R, out, kNcclUint64, p, nccl_comm, s));
+          if (cnt) RPT_NCCL_IN_GROUP(api.recv(buf + static_cast<uint64_t>(k) * stride, cnt, kNcclUint64, p, nccl_comm, s));
+          k++;
+        }
+        RPT_NCCL(api.group_end());
+        if (cnt) {
+          RPT_HIP(hipEventRecord(h->rx[b], s));
+          RPT_HIP(hipStreamWaitEvent(h->s, h->rx[b], 0));
+          helper_pending = true;
+          const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(cnt / 2 + 1, rpt::kBlockThreads), 2048)));
+          ProfScope prof_or("or_slices_kernel(allreduce)", h->s);
+          hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, h->s,
+                             bf->words + g.lo(me) + r * R, buf, static_cast<uint32_t>(world - 1), cnt, stride, 1);
+          prof_or.end();
+          RPT_LAUNCHED("or_slices_kernel");
+          RPT_HIP(hipEventRecord(h->ored[b], h->s));
+          ored[b] = true;
+        }
       }
-      RPT_NCCL(api.group_end());
-      if (mine > 0) {
-        const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(mine / 2 + 1, rpt::kBlockThreads), 4096)));
-        hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words + lo(me), tmp,
-                           static_cast<uint32_t>(world - 1), mine, 1);
-        RPT_LAUNCHED("or_slices_kernel");
-      }
-      // all-gather: every rank's merged words to every peer
+      // all-gather: every rank's merged words to every peer, once its OR kernels are done
+      RPT_HIP(join_helper());
       RPT_NCCL(api.group_start());
       for (int p = 0; p < world; p++) {
         if (p == me) continue;
-        RPT_NCCL_IN_GROUP(api.send(bf->words + lo(me), mine, kNcclUint64, p, nccl_comm, s));
-        RPT_NCCL_IN_GROUP(api.recv(bf->words + lo(p), lo(p + 1) - lo(p), kNcclUint64, p, nccl_comm, s));
+        if (g.len(me)) RPT_NCCL_IN_GROUP(api.send(bf->words + g.lo(me), g.len(me), kNcclUint64, p, nccl_comm, s));
+        if (g.len(p)) RPT_NCCL_IN_GROUP(api.recv(bf->words + g.lo(p), g.len(p), kNcclUint64, p, nccl_comm, s));
       }
       RPT_NCCL(api.group_end());
     }
@@ -1536,21 +1657,51 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
     return RPT_OK;
   };
   const int st = run();
-  order.done(false);
-  if (st == RPT_OK) {
-    (void)hipFree(v);
-  } else {
-    (void)hipStreamSynchronize(s);  // nothing may still use the staging buffer
-    (void)hipFree(v);
+  // on an error path the helper may still hold OR kernels: the caller's stream waits for them, so the
+  // workspace is free once `stream` is
+  if (h) {
+    if (join_helper() != hipSuccess) (void)hipStreamSynchronize(h->s);
+    give_helper(h);
   }
+  order.done(false);
   return st;
+}
+
+int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
+  if (!bf || !nccl_comm) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  int world = 1;
+  {
+    const std::shared_ptr<const RcclApi> api_p = rccl_api();
+    const rpt_rccl_api_table& api = api_p->fn;
+    if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
+    RPT_NCCL(api.comm_count(nccl_comm, &world));
+  }
+  RPT_ON_DEVICE(bf->device);
+  const size_t bytes = MergeGeom{1ULL << bf->log_num_blocks, world}.workspace_bytes();
+  void* ws = nullptr;
+  if (hipMalloc(&ws, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(RPT_ERR_OUT_OF_MEMORY, "all-reduce workspace of %zu bytes", bytes);
+  }
+  const int st = rpt_bf_allreduce_or_ws(bf, nccl_comm, ws, bytes, stream);
+  (void)hipStreamSynchronize(as_stream(stream));  // nothing may still use the workspace
+  (void)hipFree(ws);
+  return st;
+}
+
+int rpt_rccl_available(int device) {
+  const std::shared_ptr<const RcclApi> api_p = rccl_api();
+  if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
+  RPT_ON_DEVICE(device);
+  return RPT_OK;
 }
 
 int rpt_rccl_get_unique_id(uint8_t* out_id) {
   if (!out_id) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
-  const RcclApi& api = rccl_api();
-  if (!api.load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api.load_error.c_str());
-  RcclUniqueId id{};
+  const std::shared_ptr<const RcclApi> api_p = rccl_api();
+  const rpt_rccl_api_table& api = api_p->fn;
+  if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
+  rpt_rccl_unique_id id{};
   RPT_NCCL(api.get_unique_id(&id));
   std::memcpy(out_id, id.internal, RPT_RCCL_UNIQUE_ID_BYTES);
   return RPT_OK;
@@ -1559,10 +1710,11 @@ int rpt_rccl_get_unique_id(uint8_t* out_id) {
 int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, void** out_comm) {
   if (!id || !out_comm || world < 1 || rank < 0 || rank >= world)
     return fail(RPT_ERR_INVALID_ARGUMENT, "bad communicator arguments (world %d, rank %d)", world, rank);
-  const RcclApi& api = rccl_api();
-  if (!api.load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api.load_error.c_str());
+  const std::shared_ptr<const RcclApi> api_p = rccl_api();
+  const rpt_rccl_api_table& api = api_p->fn;
+  if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
   RPT_ON_DEVICE(device);
-  RcclUniqueId uid{};
+  rpt_rccl_unique_id uid{};
   std::memcpy(uid.internal, id, RPT_RCCL_UNIQUE_ID_BYTES);
   void* comm = nullptr;
   RPT_NCCL(api.comm_init_rank(&comm, world, uid, rank));
@@ -1572,13 +1724,32 @@ int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, 
 
 int rpt_rccl_comm_destroy(void* comm) {
   if (!comm) return RPT_OK;
-  const RcclApi& api = rccl_api();
-  if (!api.load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api.load_error.c_str());
+  const std::shared_ptr<const RcclApi> api_p = rccl_api();
+  const rpt_rccl_api_table& api = api_p->fn;
+  if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
   RPT_NCCL(api.comm_destroy(comm));
   return RPT_OK;
 }
 #undef RPT_NCCL_IN_GROUP
 #undef RPT_NCCL
+
+#ifdef RPT_TESTING_HOOKS
+// Test build only (rpt_gpu_testing.h): the product library has no such entry point.
+int rpt_testing_set_rccl_api(const rpt_rccl_api_table* table) {
+  std::shared_ptr<const RcclApi> a;
+  if (table) {
+    const void* const* e = reinterpret_cast<const void* const*>(table);
+    for (size_t i = 0; i < sizeof(rpt_rccl_api_table) / sizeof(void*); i++)
+      if (!e[i]) return fail(RPT_ERR_INVALID_ARGUMENT, "RCCL table entry %zu is null", i);
+    auto t = std::make_shared<RcclApi>();
+    t->fn = *table;
+    a = std::move(t);
+  }
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  g_rccl = std::move(a);  // null: rccl_api() returns to librccl
+  return RPT_OK;
+}
+#endif  // RPT_TESTING_HOOKS
 
 int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out) {
   if (!bf || !out) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
@@ -1627,7 +1798,7 @@ int rpt_bf_fold(rpt_bf* bf, int* out_new_log_num_blocks) {
     const unsigned grid = static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(slice / 2, rpt::kBlockThreads), 8192)));
     ProfScope prof14_("or_slices_kernel(fold)", nullptr);
     hipLaunchKernelGGL(rpt::or_slices_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, nullptr, bf->words,
-                       bf->words + slice, static_cast<uint32_t>((1u << folds) - 1), slice, 1);
+                       bf->words + slice, static_cast<uint32_t>((1u << folds) - 1), slice, slice, 1);
     prof14_.end();
     RPT_LAUNCHED("or_slices_kernel(fold)");
     RPT_HIP(hipDeviceSynchronize());

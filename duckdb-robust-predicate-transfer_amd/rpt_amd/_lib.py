@@ -119,6 +119,9 @@ SIGNATURES = {
     "rpt_hash_combine": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_bf_merge_or": (c_int, [c_void_p, c_void_p, c_void_p]),
     "rpt_bf_allreduce_or": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "rpt_bf_allreduce_or_ws": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "rpt_allreduce_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "rpt_rccl_available": (c_int, [c_int]),
     "rpt_rccl_get_unique_id": (c_int, [c_void_p]),
     "rpt_rccl_comm_init_rank": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),
     "rpt_rccl_comm_destroy": (c_int, [c_void_p]),
@@ -141,12 +144,7 @@ SIGNATURES = {
 _lib = None
 
 
-def load(path: str | None = None) -> ctypes.CDLL:
-    """Load (once) and return librpt_gpu.so. Raises if it is missing: there is no CPU fallback."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    p = path or os.environ.get("RPT_GPU_LIB", LIB_PATH)
+def _bind(p: str) -> ctypes.CDLL:
     if not os.path.exists(p):
         raise RptError(-1, f"librpt_gpu.so not found at {p}; build it with `make -C {PKG_DIR}`")
     lib = ctypes.CDLL(p)
@@ -154,8 +152,21 @@ def load(path: str | None = None) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
     return lib
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and return librpt_gpu.so. Raises if it is missing: there is no CPU fallback."""
+    global _lib
+    if _lib is None:
+        _lib = _bind(path or os.environ.get("RPT_GPU_LIB", LIB_PATH))
+    return _lib
+
+
+def load_variant(path: str) -> ctypes.CDLL:
+    """Bind another build of the same C-ABI (the test build tests/loopback/build/librpt_gpu_testing.so)
+    beside the product library; handles from one build must not be passed to the other."""
+    return _bind(path)
 
 
 def check(status: int) -> None:

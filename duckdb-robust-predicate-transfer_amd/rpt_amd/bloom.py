@@ -101,8 +101,8 @@ class BloomFilter:
     """A device-resident blocked Bloom filter (PTBloomFilter)."""
 
     def __init__(self, est_num_rows: Optional[int] = None, *, log_num_blocks: Optional[int] = None,
-                 device=None):
-        lib = load()
+                 device=None, lib=None):
+        lib = lib if lib is not None else load()  # lib: a build bound by _lib.load_variant (tests)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         if self.device.type != "cuda":
             raise RptError(1, "BloomFilter lives on a GPU device")

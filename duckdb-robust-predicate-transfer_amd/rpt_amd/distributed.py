@@ -16,10 +16,11 @@ MI355X-native scale-out of PhysicalCreateBF's parallel sink (physical_create_bf.
     its row offset, concatenated in rank order, is the global ascending sel — no exchange.
 
 Two implementations of the OR all-reduce:
-  * `RcclComm` + `allreduce_or_native`: the product path. librpt_gpu.so's `rpt_bf_allreduce_or`
-    (grouped ncclSend/ncclRecv reduce-scatter by OR + all-gather, in place on the filter words) over a
-    communicator the library creates (`rpt_rccl_comm_init_rank`, unique id broadcast over the
-    torch.distributed group). This is what a C++ / DuckDB caller gets; bench.py uses it on GPUs.
+  * `RcclComm` + `allreduce_or_native`: the product path. librpt_gpu.so's `rpt_bf_allreduce_or_ws`
+    (grouped ncclSend/ncclRecv reduce-scatter by OR in bounded rounds overlapped with the OR kernel,
+    then an all-gather, in place on the filter words) over a communicator the library creates
+    (`rpt_rccl_comm_init_rank`, unique id broadcast over the torch.distributed group). This is what a
+    C++ / DuckDB caller gets; bench.py uses it on GPUs.
   * `allreduce_or_filter`: the same choreography in torch.distributed collectives, used to rehearse
     the multi-rank path on CPU (gloo); `or_slices` is injectable so it runs without a GPU in tests.
 """
@@ -85,8 +86,18 @@ class RcclComm:
         self.device = torch.device(device)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
-        # id + a status byte: a rank-0 failure (e.g. RCCL not loadable) reaches every rank through the
-        # broadcast, so all ranks raise together instead of the others waiting in the init
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        on_device = dist.get_backend(group) != "gloo"
+        # 1. every rank checks that librccl loads and its GPU is usable, and the group agrees before
+        #    anyone enters the collective init (a rank failing there would leave the others blocked in
+        #    ncclCommInitRank)
+        st = self._lib.rpt_rccl_available(dev)
+        err = "" if st == 0 else self._lib.rpt_last_error().decode(errors="replace")
+        ok = torch.tensor([1 if st == 0 else 0], dtype=torch.int64, device=self.device if on_device else "cpu")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if not int(ok.item()):
+            raise RptError(7, f"RCCL unavailable on {'this rank: ' + err if st != 0 else 'another rank'}")
+        # 2. rank 0 draws the id; a status byte rides along, so a failure there reaches every rank
         uid = torch.zeros(self.ID_BYTES + 1, dtype=torch.uint8)
         err = ""
         if self.rank == 0:
@@ -94,14 +105,13 @@ class RcclComm:
             if st != 0:
                 err = self._lib.rpt_last_error().decode(errors="replace")
                 uid[self.ID_BYTES] = 1
-        on_device = dist.get_backend(group) != "gloo"
         t = uid.to(self.device) if on_device else uid
         dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         uid = t.cpu().contiguous()
         if int(uid[self.ID_BYTES]) != 0:
             raise RptError(7, f"rpt_rccl_get_unique_id failed on rank 0{': ' + err if err else ''}")
+        # 3. the collective init
         h = ctypes.c_void_p()
-        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         st = self._lib.rpt_rccl_comm_init_rank(dev, self.world, uid.data_ptr(), self.rank, ctypes.byref(h))
         if st != 0:
             raise RptError(st, self._lib.rpt_last_error().decode(errors="replace"))
@@ -119,13 +129,22 @@ class RcclComm:
             pass
 
 
-def allreduce_or_native(bf, comm: RcclComm, stream=None) -> None:
-    """CREATE_BF Combine across GPUs through the C-ABI (rpt_bf_allreduce_or): words OR-merged in place,
+def allreduce_workspace(bf, comm: RcclComm) -> torch.Tensor:
+    """Staging for rpt_bf_allreduce_or_ws: <= 2 (W-1) x 32 MiB + 256 B whatever the filter size; allocate
+    it once, before a timed merge."""
+    n = int(bf._lib.rpt_allreduce_workspace_bytes(comm.world, bf.log_num_blocks))
+    return torch.empty(n, dtype=torch.uint8, device=bf.device)
+
+
+def allreduce_or_native(bf, comm: RcclComm, stream=None, workspace: Optional[torch.Tensor] = None) -> None:
+    """CREATE_BF Combine across GPUs through the C-ABI (rpt_bf_allreduce_or_ws): words OR-merged in place,
     key min/max and has_data reduced; returns once has_data is known (one stream sync)."""
     from ._lib import check
     from .bloom import _stream
 
-    check(bf._lib.rpt_bf_allreduce_or(bf.handle, comm.handle, _stream(bf.device, stream)))
+    ws = workspace if workspace is not None else allreduce_workspace(bf, comm)
+    check(bf._lib.rpt_bf_allreduce_or_ws(bf.handle, comm.handle, ws.data_ptr(), ws.numel(),
+                                         _stream(bf.device, stream)))
 
 
 def allreduce_or_filter(bf, group=None) -> None:

@@ -236,7 +236,18 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream);
  * ncclRedOp_t. The key min/max and has_data are reduced too, in one ncclAllReduce(MIN). Collective:
  * every rank of the communicator must call it. Stream-ordered on `stream`; returns after has_data is
  * known (one stream sync). librccl is loaded on first use (dlopen), so the library itself does not
- * depend on it. */
+ * depend on it.
+ * Rank j owns words [lo(j), lo(j+1)), lo(j) = (num_blocks * j / world) rounded down to 32 words (W need not
+ * divide the block count). The reduce-scatter runs in rounds of at most RPT_ALLREDUCE_ROUND_WORDS words
+ * per peer through two staging buffers: the OR kernel of round r runs on a library helper stream while
+ * round r + 1 transfers on `stream`. rpt_bf_allreduce_or_ws takes that staging from the caller
+ * (rpt_allreduce_workspace_bytes(world, log_num_blocks) bytes of device memory, exclusively owned until
+ * the call returns; <= 2 (W-1) * 32 MiB + 256 B whatever the filter size); rpt_bf_allreduce_or allocates
+ * and frees it itself. */
+#define RPT_ALLREDUCE_ROUND_WORDS (4ULL << 20)
+size_t rpt_allreduce_workspace_bytes(int world, int log_num_blocks);
+int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t workspace_bytes,
+                           rpt_stream_t stream);
 int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream);
 /* RCCL communicator for callers that bring none (bench.py, tests; a DuckDB shim that owns an
  * ncclComm_t passes it to rpt_bf_allreduce_or directly). Rank 0 calls rpt_rccl_get_unique_id, the
@@ -244,6 +255,10 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream);
  * then every rank calls rpt_rccl_comm_init_rank for its own GPU (collective; blocks until all ranks
  * joined) — ncclGetUniqueId / ncclCommInitRank / ncclCommDestroy of the dlopened librccl. */
 #define RPT_RCCL_UNIQUE_ID_BYTES 128
+/* RPT_OK if librccl loads with every entry point the merge uses and `device` can be made current (no
+ * collective call): every rank checks it, and the ranks agree, before the collective init, so a rank
+ * that cannot join never leaves the others blocked in ncclCommInitRank. */
+int rpt_rccl_available(int device);
 int rpt_rccl_get_unique_id(uint8_t* out_id);
 int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, void** out_comm);
 int rpt_rccl_comm_destroy(void* comm);

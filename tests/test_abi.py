@@ -115,3 +115,25 @@ def test_strategy_support_rules():
     assert buck == list(range(22, 32))
     assert lib.rpt_probe_strategy_supported(99, 10) == 0
     assert lib.rpt_synth_probe_keys(None, 1, 10, 0, 10, None) == _lib.RPT_ERR_INVALID_ARGUMENT
+
+
+def test_testing_hook_absent_from_product():
+    # the RCCL-table seam (csrc/rpt_gpu_testing.h) exists only in the test build (tests/loopback)
+    lib = _lib.load()
+    assert not hasattr(lib, "rpt_testing_set_rccl_api")
+
+
+@pytest.mark.parametrize("world,L", [(1, 30), (2, 3), (2, 20), (3, 25), (8, 24), (8, 30), (8, 31)])
+def test_allreduce_workspace_is_bounded(world, L):
+    lib = _lib.load()
+    b = lib.rpt_allreduce_workspace_bytes(world, L)
+    nw = 1 << L
+    if world == 1:
+        assert b == 256
+    else:
+        # 256 B + two staging buffers of (W-1) round pieces: <= 32 MiB per peer, <= 1 GiB at C5 (W = 8, 2^30)
+        assert b <= 256 + 2 * (world - 1) * (4 << 20) * 8
+        assert b >= 256 + 2 * (world - 1) * 8 * min(4 << 20, nw // world - 32)
+    if (world, L) == (8, 30):
+        assert b <= 1 << 30
+    assert lib.rpt_allreduce_workspace_bytes(0, L) == 0

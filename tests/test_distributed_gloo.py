@@ -135,7 +135,7 @@ def test_minmax_and_flag_allreduce(world):
     assert out == expect
 
 
-def _rccl_id_worker(rank, world, port, fail_rank0, q):
+def _rccl_id_worker(rank, world, port, mode, q):
     import sys
 
     sys.path.insert(0, PKG)
@@ -145,18 +145,24 @@ def _rccl_id_worker(rank, world, port, fail_rank0, q):
         from rpt_amd import _lib
         from rpt_amd.distributed import RcclComm
 
-        if fail_rank0 and rank == 0:
-            lib = _lib.load()
+        lib = _lib.load()
+        fail_avail = mode == "avail_rank1" and rank == 1
+        fail_id = mode == "id_rank0" and rank == 0
 
-            class Failing:  # rpt_rccl_get_unique_id refusing, as when RCCL cannot be loaded
-                def __getattr__(self, name):
-                    return getattr(lib, name)
+        class Patched:  # RCCL / the GPU unusable on one rank, or rank 0 unable to draw an id
+            def __getattr__(self, name):
+                return getattr(lib, name)
 
-                @staticmethod
-                def rpt_rccl_get_unique_id(_ptr):
-                    return _lib.RPT_ERR_COLLECTIVE
+            @staticmethod
+            def rpt_rccl_available(_dev):
+                return _lib.RPT_ERR_COLLECTIVE if fail_avail else _lib.RPT_OK
 
-            _lib.load = lambda path=None: Failing()
+            @staticmethod
+            def rpt_rccl_get_unique_id(ptr):
+                return _lib.RPT_ERR_COLLECTIVE if fail_id else lib.rpt_rccl_get_unique_id(ptr)
+
+        if mode != "none":
+            _lib.load = lambda path=None: Patched()
         try:
             RcclComm(torch.device("cuda", 0))
             q.put((rank, "ok"))
@@ -166,16 +172,17 @@ def _rccl_id_worker(rank, world, port, fail_rank0, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fail_rank0", [True, False])
-def test_rccl_comm_failure_reaches_every_rank(fail_rank0):
-    """RcclComm's id exchange carries rank 0's status: when rank 0 cannot draw an id every rank raises
-    (none is left waiting in the communicator init); without a GPU the init itself fails on every rank.
-    bench.py then takes the recorded torch.distributed merge on all ranks together."""
+@pytest.mark.parametrize("mode", ["avail_rank1", "id_rank0", "none"])
+def test_rccl_comm_failure_reaches_every_rank(mode):
+    """RcclComm never leaves a rank waiting in the collective init: every rank first checks that RCCL
+    loads and its GPU is usable and the group agrees (one rank failing -> every rank raises); rank 0's
+    id draw carries its status to every rank; without a GPU (this container) every rank fails the
+    check. bench.py then exits non-zero on every rank (no silent fallback)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rccl_id_worker, args=(r, world, port, fail_rank0, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rccl_id_worker, args=(r, world, port, mode, q)) for r in range(world)]
     for p in procs:
         p.start()
     got = dict(q.get(timeout=120) for _ in range(world))
@@ -183,7 +190,9 @@ def test_rccl_comm_failure_reaches_every_rank(fail_rank0):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert sorted(got) == [0, 1]
-    for msg in got.values():
+    for r, msg in got.items():
         assert msg != "ok"
-        if fail_rank0:
+        if mode == "id_rank0":
             assert "failed on rank 0" in msg
+        if mode == "avail_rank1":
+            assert ("this rank" if r == 1 else "another rank") in msg

@@ -133,6 +133,8 @@ def test_clear_twice_and_cross_stream(rpt):
     b = keys(1_000_000, 5)
     db = dev(b)
     torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(50_000_000)  # hold s1 back: the clear's stats reset runs late
     bf.clear(stream=s1)
     bf.clear(stream=s1)
     bf.insert(db, strategy=INS_BUCKETED, stream=s2)
@@ -140,7 +142,61 @@ def test_clear_twice_and_cross_stream(rpt):
     w = orc.new_words(log_nb)
     orc.insert_keys(w, log_nb, b)
     assert np.array_equal(bf.export_words(), w)
+    # the insert's min/max (folded in by its first kernels) landed after the clear's reset
+    assert bf.minmax() == orc.minmax(b)
     e = rpt.BloomFilter(log_num_blocks=log_nb)
     e.clear()
     e.insert(db, strategy=INS_BUCKETED)
     assert np.array_equal(e.export_words(), w)
+
+
+@pytest.mark.parametrize("strategy", [INS_PARTITIONED, INS_BUCKETED])
+def test_minmax_ordered_after_cross_stream_clear(rpt, strategy):
+    """after a clear enqueued on a delayed stream, an insert on another stream must fold its
+    key min/max in after the clear's stats reset (partitioned and bucketed inserts fold them in their
+    first kernels, before the slice merge takes the write order), and a merge's stats update stays
+    inside its write order."""
+    log_nb = 24
+    bf = filled(rpt, log_nb)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    b = keys(2_000_000, 11)
+    db = dev(b)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(50_000_000)
+    bf.clear(stream=s1)
+    bf.insert(db, strategy=strategy, stream=s2)
+    torch.cuda.synchronize()
+    assert bf.minmax() == orc.minmax(b)
+    # merge_or: dst cleared on a delayed stream, then merged from src on another stream
+    src = rpt.BloomFilter(log_num_blocks=log_nb)
+    src.insert(db, strategy=strategy)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(50_000_000)
+    bf.clear(stream=s1)
+    bf.merge_or(src, stream=s2)
+    torch.cuda.synchronize()
+    assert bf.minmax() == orc.minmax(b)
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, b)
+    assert np.array_equal(bf.export_words(), w)
+
+
+def test_clear_settled_by_a_reader_orders_other_streams(rpt):
+    """the first reader after a clear zeroes the words on ITS stream without a host sync; a
+    reader on another stream that finds the clear settled must wait for that zeroing (an event), not
+    read the old words."""
+    bf = filled(rpt, 22)
+    da = dev(keys(300_000, 1))
+    out = torch.full((1 << 22,), -1, dtype=torch.int64, device="cuda:0")
+    bf.clear()
+    torch.cuda.synchronize()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    with torch.cuda.stream(s1):
+        torch.cuda._sleep(50_000_000)  # the zeroing enqueued on s1 runs late
+    _sel, cnt = bf.probe_async(da, stream=s1)
+    bf.copy_words_to(out, stream=s2)
+    torch.cuda.synchronize()
+    assert int(cnt.item()) == 0
+    assert not out.any()

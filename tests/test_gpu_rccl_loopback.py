@@ -1,0 +1,272 @@
+"""The product multi-GPU merge, rpt_bf_allreduce_or_ws (CREATE_BF Combine across GPUs; the reference's
+single-node analogue is PhysicalCreateBF::Combine, physical_create_bf.cpp:244-275), run with W = 2..8
+ranks on ONE GPU.
+
+RCCL refuses two ranks on one device, so the ranks here are host threads of this process talking
+through the loopback RCCL of tests/loopback/rccl_loopback.cpp (grouped send/recv matched at
+ncclGroupEnd by device-to-device copies, stream-event ordered; MIN all-reduce through the host). The
+merge code is the product's: the test build of csrc/rpt_gpu.hip (tests/loopback/build/
+librpt_gpu_testing.so, compiled with RPT_TESTING_HOOKS, which only adds the entry point that swaps
+the RCCL table). Every rank's merged words must equal the oracle's filter of all ranks' keys, and the
+key min/max and has_data must be reduced:
+
+* W in {2, 3, 5, 8}: uneven slices (W does not divide the block count), several reduce-scatter rounds
+  (slices over RPT_ALLREDUCE_ROUND_WORDS words), an empty rank, all ranks empty, a filter smaller than
+  one 32-word slice granule;
+* C5's geometry: the 8 GiB / 2^30-block filter sized for 8e9 rows, W = 4;
+* an error injected inside a group: every rank fails with RPT_ERR_COLLECTIVE, every group is closed,
+  and the filters stay usable.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+import rpt_oracle as orc
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+LOOP_DIR = os.path.join(REPO, "tests", "loopback", "build")
+API_FIELDS = ["get_unique_id", "comm_init_rank", "comm_destroy", "group_start", "group_end", "send", "recv",
+              "all_reduce", "comm_count", "comm_user_rank", "error_string"]
+LOOP_SYMBOLS = ["ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclGroupStart", "ncclGroupEnd",
+                "ncclSend", "ncclRecv", "ncclAllReduce", "ncclCommCount", "ncclCommUserRank", "ncclGetErrorString"]
+ROUND_WORDS = 4 << 20  # RPT_ALLREDUCE_ROUND_WORDS
+RPT_ERR_COLLECTIVE = 6
+
+
+class ApiTable(ctypes.Structure):  # rpt_rccl_api_table (csrc/rpt_gpu_testing.h)
+    _fields_ = [(f, ctypes.c_void_p) for f in API_FIELDS]
+
+
+@pytest.fixture(scope="module")
+def env():
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test run without a visible GPU")
+    torch.cuda.set_device(0)
+    from rpt_amd import _lib
+
+    _lib.load()
+    tlib = _lib.load_variant(os.path.join(LOOP_DIR, "librpt_gpu_testing.so"))
+    tlib.rpt_testing_set_rccl_api.restype = ctypes.c_int
+    tlib.rpt_testing_set_rccl_api.argtypes = [ctypes.c_void_p]
+    loop = ctypes.CDLL(os.path.join(LOOP_DIR, "librccl_loopback.so"))
+    loop.rpt_loopback_fail_op.argtypes = [ctypes.c_int, ctypes.c_int]
+    loop.rpt_loopback_group_depth.restype = ctypes.c_int
+    loop.rpt_loopback_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    table = ApiTable(*[ctypes.cast(getattr(loop, s), ctypes.c_void_p) for s in LOOP_SYMBOLS])
+    assert tlib.rpt_testing_set_rccl_api(ctypes.byref(table)) == 0, tlib.rpt_last_error()
+    yield tlib, loop
+    assert tlib.rpt_testing_set_rccl_api(None) == 0
+
+
+def in_threads(world, fn):
+    """Run fn(rank) on `world` threads (ctypes releases the GIL inside the library calls)."""
+    errs = []
+
+    def wrap(r):
+        try:
+            fn(r)
+        except Exception as e:  # surfaced below
+            errs.append((r, repr(e)))
+
+    ts = [threading.Thread(target=wrap, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=600)
+    assert not any(t.is_alive() for t in ts), "a rank thread hung"
+    assert not errs, errs
+
+
+def make_comms(tlib, world):
+    uid = (ctypes.c_uint8 * 128)()
+    assert tlib.rpt_rccl_get_unique_id(uid) == 0, tlib.rpt_last_error()
+    comms = [ctypes.c_void_p() for _ in range(world)]
+    st = [None] * world
+
+    def init(r):
+        st[r] = tlib.rpt_rccl_comm_init_rank(0, world, uid, r, ctypes.byref(comms[r]))
+
+    in_threads(world, init)
+    assert st == [0] * world
+    return comms
+
+
+def destroy_comms(tlib, comms):
+    for c in comms:
+        assert tlib.rpt_rccl_comm_destroy(c) == 0
+
+
+def slices(nw, world):
+    """Rank j's word range (MergeGeom in csrc/rpt_gpu.hip): starts rounded down to 32 words."""
+    lo = [((nw * j) // world) & ~31 for j in range(world)] + [nw]
+    return [(lo[j], lo[j + 1]) for j in range(world)]
+
+
+def expected_rounds(nw, world):
+    mx = max(b - a for a, b in slices(nw, world))
+    r = max(2, min(ROUND_WORDS, (mx + 1) & ~1))
+    return -(-mx // r)
+
+
+def shard(n, rank, world):
+    base, rem = divmod(n, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def build_partials(tlib, world, log_nb, n_build, empty):
+    import rpt_amd
+
+    bfs, keys_used = [], []
+    all_keys = orc.synth_build_keys(n_build) if n_build else np.zeros(0, dtype=np.uint64)
+    for r in range(world):
+        bf = rpt_amd.BloomFilter(log_num_blocks=log_nb, lib=tlib)
+        lo, hi = shard(n_build, r, world)
+        if r not in empty and hi > lo:
+            bf.insert(rpt_amd.synth_build_keys(hi - lo, start=lo, device="cuda:0"))
+            keys_used.append(all_keys[lo:hi])
+        bfs.append(bf)
+    torch.cuda.synchronize()
+    keys = np.concatenate(keys_used) if keys_used else np.zeros(0, dtype=np.uint64)
+    return bfs, keys
+
+
+def allreduce_all(tlib, bfs, comms):
+    world = len(bfs)
+    L = bfs[0].log_num_blocks
+    need = tlib.rpt_allreduce_workspace_bytes(world, L)
+    wss = [torch.empty(need, dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    streams = [torch.cuda.Stream(device="cuda:0") for _ in range(world)]
+    st = [None] * world
+
+    def run(r):
+        st[r] = tlib.rpt_bf_allreduce_or_ws(bfs[r].handle, comms[r], wss[r].data_ptr(), need, streams[r].cuda_stream)
+
+    in_threads(world, run)
+    torch.cuda.synchronize()
+    return st, need
+
+
+@pytest.mark.parametrize("world,log_nb,n_build,empty", [
+    (2, 14, 20_000, ()),
+    (3, 20, 300_000, ()),            # 2^20 words over 3 ranks: uneven slices
+    (5, 25, 3_000_000, (2,)),        # 2^25 / 5 words per slice: 2 rounds, an empty rank
+    (8, 20, 1_000_000, (0, 7)),      # empty first and last rank
+    (8, 3, 40, (1,)),                # 8 words < one 32-word granule: the last rank owns them all
+    (2, 24, 0, (0, 1)),              # every rank empty
+    (3, 26, 4_000_000, ()),          # 2^26 / 3 words per slice: 6 rounds
+])
+def test_loopback_allreduce_matches_single_build(env, world, log_nb, n_build, empty):
+    tlib, loop = env
+    comms = make_comms(tlib, world)
+    bfs, keys = build_partials(tlib, world, log_nb, n_build, set(empty))
+    g0, b0 = ctypes.c_uint64(), ctypes.c_uint64()
+    assert loop.rpt_loopback_stats(comms[0], ctypes.byref(g0), ctypes.byref(b0)) == 0
+    st, need = allreduce_all(tlib, bfs, comms)
+    assert st == [0] * world, tlib.rpt_last_error()
+    nw = 1 << log_nb
+    # bounded staging: 256 B + 2 (W-1) round pieces of <= 32 MiB
+    assert need <= 256 + 2 * (world - 1) * ROUND_WORDS * 8
+    g1, b1 = ctypes.c_uint64(), ctypes.c_uint64()
+    assert loop.rpt_loopback_stats(comms[0], ctypes.byref(g1), ctypes.byref(b1)) == 0
+    assert g1.value - g0.value == expected_rounds(nw, world) + 1  # reduce-scatter rounds + the all-gather
+    # every word crosses W-1 links twice: reduce-scatter pieces in, merged slices out
+    assert b1.value - b0.value == 2 * (world - 1) * nw * 8
+    ref = orc.new_words(log_nb)
+    if keys.size:
+        orc.insert_keys(ref, log_nb, keys)
+    want_mm = orc.minmax(keys) if keys.size else None
+    for r, bf in enumerate(bfs):
+        assert np.array_equal(bf.export_words(), ref), f"rank {r} words"
+        assert bf.minmax() == want_mm, f"rank {r} min/max"
+        assert bf.is_empty() == (keys.size == 0), f"rank {r} has_data"
+    destroy_comms(tlib, comms)
+    for bf in bfs:
+        bf.close()
+
+
+def test_loopback_allreduce_c5_geometry(env):
+    """C5: a filter sized for 8e9 rows (2^30 blocks = 8 GiB) on every rank, W = 4 (4 x 8 GiB on one GPU),
+    1.2e7 build keys over the ranks; every rank's 8 GiB of words against rank 0's on the device, and rank
+    0's against the oracle's."""
+    tlib, _loop = env
+    world, log_nb, n_build = 4, 30, 12_000_000
+    assert tlib.rpt_bf_log_num_blocks_for_rows(8 * 10**9) == log_nb
+    comms = make_comms(tlib, world)
+    bfs, keys = build_partials(tlib, world, log_nb, n_build, set())
+    st, need = allreduce_all(tlib, bfs, comms)
+    assert st == [0] * world, tlib.rpt_last_error()
+    assert need <= 1 << 30  # staging <= 1 GiB (here 2 * 3 * 32 MiB)
+    nw = 1 << log_nb
+    w0 = torch.empty(nw, dtype=torch.int64, device="cuda:0")
+    bfs[0].copy_words_to(w0)
+    wr = torch.empty_like(w0)
+    for r in range(1, world):
+        bfs[r].copy_words_to(wr)
+        assert torch.equal(w0, wr), f"rank {r} differs from rank 0"
+    del wr
+    ref = orc.new_words(log_nb)
+    orc.insert_keys(ref, log_nb, keys)
+    assert np.array_equal(w0.cpu().numpy().view(np.uint64), ref)
+    for bf in bfs:
+        assert bf.minmax() == orc.minmax(keys)
+    destroy_comms(tlib, comms)
+    del w0
+    for bf in bfs:
+        bf.close()
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("fail_rank,fail_op", [(1, 1), (0, 0), (2, 9)])
+def test_loopback_error_inside_group(env, fail_rank, fail_op):
+    """An RCCL call failing inside a group: the failing rank closes its group before returning, every
+    rank's all-reduce returns RPT_ERR_COLLECTIVE (none hangs), no group stays open on any thread, and
+    each filter is still usable afterwards (its write order was released)."""
+    tlib, loop = env
+    world, log_nb = 3, 25  # 2^25 / 3 words per slice: 3 rounds, so op 9 lands in a later round
+    comms = make_comms(tlib, world)
+    bfs, _keys = build_partials(tlib, world, log_nb, 300_000, set())
+    need = tlib.rpt_allreduce_workspace_bytes(world, log_nb)
+    wss = [torch.empty(need, dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    streams = [torch.cuda.Stream(device="cuda:0") for _ in range(world)]
+    st, depth = [None] * world, [None] * world
+
+    def run(r):
+        st[r] = tlib.rpt_bf_allreduce_or_ws(bfs[r].handle, comms[r], wss[r].data_ptr(), need, streams[r].cuda_stream)
+        depth[r] = loop.rpt_loopback_group_depth()
+
+    loop.rpt_loopback_fail_op(fail_rank, fail_op)
+    try:
+        in_threads(world, run)
+    finally:
+        loop.rpt_loopback_fail_op(-1, -1)
+    torch.cuda.synchronize()
+    assert st == [RPT_ERR_COLLECTIVE] * world
+    assert depth == [0] * world
+    for bf in bfs:  # still usable: a write after the failed merge and an export both complete
+        bf.insert(torch.arange(1000, dtype=torch.int64, device="cuda:0"))
+        assert bf.export_words().any()
+    destroy_comms(tlib, comms)
+    for bf in bfs:
+        bf.close()
+
+
+def test_loopback_workspace_is_checked(env):
+    tlib, _loop = env
+    comms = make_comms(tlib, 2)
+    bfs, _ = build_partials(tlib, 2, 20, 1000, set())
+    ws = torch.empty(64, dtype=torch.uint8, device="cuda:0")
+    st = [None, None]
+
+    def run(r):
+        st[r] = tlib.rpt_bf_allreduce_or_ws(bfs[r].handle, comms[r], ws.data_ptr(), 64, None)
+
+    in_threads(2, run)
+    assert st == [4, 4]  # RPT_ERR_WORKSPACE, before any collective call
+    destroy_comms(tlib, comms)
