@@ -6,164 +6,164 @@
 namespace rpt {
 
 // ---- bucketed strategy (filters of 2^22..2^31 blocks) ----------------------------------------------
-// Level 1 cuts the rows by 32 MiB filter region ("bucket": 256 slices) into one contiguous hash array
-// per bucket, each padded to whole 16 Ki-row tiles; level 2 is the partitioned pipeline above over
-// those arrays, every bucket against its own 256 slices. bucket = block id >> 22 = hash bits 38...
+// Level 1 cuts the rows by 32 MiB filter region ("bucket": 256 slices) in ONE pass over the keys; level 2
+// is the partitioned pipeline over the resulting level-2 hash array, every bucket against its own 256
+// slices. bucket = block id >> 22 = hash bits 38...
+//
+// The level-2 array is built without a counting pass (r02 read the keys twice: a count kernel for the
+// bucket totals, then the scatter). Each level-1 tile (16 Ki rows) sorts its rows by bucket in LDS and
+// APPENDS each bucket's run to a list: list (g, b) for bucket b and group g = the workgroup's XCD (8
+// groups, so a list's neighbouring runs leave one L2 and merge there into whole lines; 1 group for
+// small batches, where 8 lists per bucket would pad too much). A list is a sequence of 4 Ki-row chunks
+// taken from a pool on the device: a run's rows [p, p + c) of its list come from one returning atomic
+// on the list's row cursor; the run that covers a chunk's first row takes the chunk (an atomic on its
+// group's pool shard) and publishes its id in chunk_tab; a run starting inside a chunk waits for that
+// id (its taker did its cursor atomic earlier, publishes without waiting for anything, and so
+// finishes; the wait is bounded anyway and flags `error`). bucket_lists_kernel then lays every bucket's
+// lists out as consecutive level-2 tiles of 4 chunks ("w-space": the row order level 2 sees) through
+// chunk_map, and pads each list's last chunk with copies of one of its hashes (re-inserting or
+// re-probing a present hash changes nothing; the pads' results are never read).
 static_assert(kLogNumMasks + 6 + kSliceLog + kBucketSliceLog <= 40, "level-2 split hashes carry bits 0..39");
 __device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t bucket_mask) {
   return static_cast<uint32_t>(h >> (kLogNumMasks + 6 + kSliceLog + kBucketSliceLog)) & bucket_mask;
 }
 
-// B1: rows per bucket of every 16 Ki-row level-1 tile -> counts_tm[tile][bucket] (+ the build's min/max).
+constexpr uint32_t kChunkEmpty = ~0u;
+constexpr uint32_t kMaxRunChunks = static_cast<uint32_t>(kL1TileRows / kChunkRows) + 1;  // chunks one run can touch
+constexpr uint32_t kL1Groups = 8;
+constexpr uint32_t kChunkSpinLimit = 1u << 22;  // ~0.3 s of polling: never reached unless a kernel is broken
+
+struct L1Lists {
+  uint32_t* cursor;     // [groups * nb] rows appended to each list        } zeroed before the scatter
+  uint32_t* pool;       // [groups] chunks taken from each group's shard    }
+  uint32_t* error;      // [1] a bound was hit (never expected)             }
+  uint32_t* chunk_tab;  // [groups * nb][cmax] chunk id of a list's c-th chunk (kChunkEmpty until taken)
+  uint32_t cmax;        // chunks per list: <= 4 * ceil(t1 / groups) + 1
+  uint32_t shard_cap;   // chunks per pool shard: <= 4 * ceil(t1 / groups) + nb
+  uint32_t groups;      // 1 or kL1Groups
+};
+
+// Level-1 tiles are mapped XCD-contiguously (workgroup b runs on XCD b % 8): each XCD gets a contiguous
+// tile range. The list group of a tile is the XCD share of the workgroup that scattered it.
+__device__ __forceinline__ uint64_t l1_tile_of_block(uint32_t blk, uint32_t grid) {
+  const uint32_t per = grid / kL1Groups;
+  return blk < per * kL1Groups ? static_cast<uint64_t>(blk % kL1Groups) * per + blk / kL1Groups : blk;
+}
+__device__ __forceinline__ uint32_t l1_group_of_tile(uint64_t tile, uint32_t grid, uint32_t groups) {
+  if (groups == 1) return 0;
+  const uint32_t per = grid / kL1Groups;
+  return tile < static_cast<uint64_t>(per) * kL1Groups ? static_cast<uint32_t>(tile / per)
+                                                      : static_cast<uint32_t>(tile % kL1Groups);
+}
+
+__device__ __forceinline__ void l1_flag_error(const L1Lists& L) {
+  __hip_atomic_store(L.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// B1: one pass over a 16 Ki-row level-1 tile: hash every row (held in registers), rank it within its
+// bucket (LDS atomic), append each bucket's run to its list (see above), sort the tile's hashes by
+// bucket in LDS and copy them to their list positions as the level-2 kKeySplit layout: hash bits 0..31
+// in hash_lo, bits 32..39 in hash_hi. Probe only: pos_out (u16) = each row's slot in the tile's
+// bucket-sorted order, counts_tm / pre_tm [tile][bucket] = the run's length and its start in its list.
+// Build only (MM): the key min/max is folded into stats.
 template <int K, bool DENSE, bool MM>
-__global__ __launch_bounds__(kTileThreads) void bucket_count_kernel(KeyArgs a, uint64_t n, uint32_t bucket_mask,
-                                                                    uint32_t* __restrict__ counts_tm,
-                                                                    int64_t* __restrict__ stats) {
-  __shared__ uint32_t s_cnt[kMaxBuckets];
+__global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a, uint64_t n, uint32_t bucket_mask, L1Lists L,
+                                                                      uint32_t* __restrict__ hash_lo,
+                                                                      uint8_t* __restrict__ hash_hi,
+                                                                      uint16_t* __restrict__ pos_out,
+                                                                      uint32_t* __restrict__ counts_tm,
+                                                                      uint32_t* __restrict__ pre_tm,
+                                                                      int64_t* __restrict__ stats) {
+  extern __shared__ uint32_t s_lo[];  // kL1TileRows hash words (bits 0..31), bucket-sorted, then
+  uint8_t* s_hi = reinterpret_cast<uint8_t*>(s_lo + kL1TileRows);    // their bits 32..39, then
+  uint16_t* s_bk = reinterpret_cast<uint16_t*>(s_hi + kL1TileRows);  // their bucket
+  __shared__ uint32_t s_cnt[kMaxBuckets], s_start[kMaxBuckets];
+  __shared__ uint64_t s_qc[kMaxBuckets];  // (list position of sorted slot 0) | first chunk index << 32
+  __shared__ uint32_t s_chunk[kMaxRunChunks][kMaxBuckets];  // ids of the chunks the run covers
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t nb = bucket_mask + 1;
+  const uint64_t tile = l1_tile_of_block(blockIdx.x, gridDim.x);
+  const uint32_t grp = L.groups == 1 ? 0u : blockIdx.x % kL1Groups;
+  const uint64_t tile_base = tile * kL1TileRows;
+  // the threads that own a bucket's list (the last kMaxBuckets threads: wave 0 scans meanwhile)
+  const uint32_t own_b = threadIdx.x - (kTileThreads - kMaxBuckets);
+  const bool owner = threadIdx.x >= kTileThreads - kMaxBuckets && own_b < nb;
   for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_cnt[i] = 0;
   __syncthreads();
-  const uint64_t tile = blockIdx.x, tile_base = tile * kL1TileRows;
+  uint64_t hh[kL1SegsPerWave][8];
+  uint32_t rk[kL1SegsPerWave][8];  // rank within the bucket, ~0 for rows past n
   int64_t wmn = kMinInit, wmx = kMaxInit;
 #pragma unroll
   for (int sg = 0; sg < kL1SegsPerWave; sg++) {
-    const uint32_t seg_local = wave * (kL1SegsPerWave * kSegRows) + sg * kSegRows;
-    uint64_t hh[8];
+    const uint64_t sbase = tile_base + wave * (kL1SegsPerWave * kSegRows) + sg * kSegRows;
     bool oo[8];
     int64_t mm[2] = {kMinInit, kMaxInit};
-    load_hashes<K, DENSE, MM, RPT_NT_KEY_LOADS>(a, tile_base + seg_local, n, lane, hh, oo, mm);
+    load_hashes<K, DENSE, MM, false, true>(a, sbase, n, lane, hh[sg], oo, mm);
     if constexpr (MM && KeyTraits<K>::kValues) {
       wave_minmax(mm[0], mm[1]);
       wmn = min(wmn, mm[0]);
       wmx = max(wmx, mm[1]);
     }
 #pragma unroll
-    for (int j = 0; j < 8; j++)
-      if (oo[j]) atomicAdd(&s_cnt[bucket_of(hh[j], bucket_mask)], 1u);
+    for (int j = 0; j < 8; j++) rk[sg][j] = oo[j] ? atomicAdd(&s_cnt[bucket_of(hh[sg][j], bucket_mask)], 1u) : ~0u;
   }
   if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) counts_tm[tile * nb + i] = s_cnt[i];
-}
-
-// B2: in place, each bucket's row of counts_bm[bucket][tile] becomes its exclusive prefix over tiles
-// (where the tile's run starts inside the bucket's array); totals[bucket] = the bucket's rows.
-__global__ __launch_bounds__(1024) void bucket_scan_kernel(uint32_t* __restrict__ counts_bm, uint64_t n_tiles,
-                                                          uint32_t* __restrict__ totals) {
-  __shared__ uint32_t s_wave[16];
-  uint32_t* row = counts_bm + static_cast<uint64_t>(blockIdx.x) * n_tiles;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t carry = 0;
-  for (uint64_t c0 = 0; c0 < n_tiles; c0 += 1024) {
-    const uint64_t i = c0 + threadIdx.x;
-    const uint32_t v = i < n_tiles ? row[i] : 0u;
-    const uint32_t incl = wave_inclusive_sum(v);
-    if (lane == 63) s_wave[wave] = incl;
-    __syncthreads();
-    uint32_t off = carry, chunk = 0;
-    for (uint32_t w = 0; w < 16; w++) {
-      const uint32_t t = s_wave[w];
-      off += w < wave ? t : 0u;
-      chunk += t;
-    }
-    if (i < n_tiles) row[i] = off + incl - v;
-    carry += chunk;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
-}
-
-// B3: bucket bases in the level-2 array (each bucket padded to whole tiles) and its tile ranges:
-// base[b] (rows), bucket_tiles[b] = base[b] / kTileRows; base[nb], bucket_tiles[nb] = the totals.
-__global__ __launch_bounds__(1024) void bucket_base_kernel(const uint32_t* __restrict__ totals, uint32_t nb,
-                                                          uint64_t* __restrict__ base,
-                                                          uint32_t* __restrict__ bucket_tiles) {
-  __shared__ uint32_t s_wave[16];
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t b = threadIdx.x;
-  const uint32_t tiles = b < nb ? static_cast<uint32_t>((totals[b] + kTileRows - 1) / kTileRows) : 0u;
-  const uint32_t incl = wave_inclusive_sum(tiles);
-  if (lane == 63) s_wave[wave] = incl;
-  __syncthreads();
-  uint32_t off = 0, all = 0;
-  for (uint32_t w = 0; w < 16; w++) {
-    off += w < wave ? s_wave[w] : 0u;
-    all += s_wave[w];
-  }
-  const uint32_t first = off + incl - tiles;
-  if (b < nb) {
-    bucket_tiles[b] = first;
-    base[b] = static_cast<uint64_t>(first) * kTileRows;
-  }
-  if (b == 0) {
-    bucket_tiles[nb] = all;
-    base[nb] = static_cast<uint64_t>(all) * kTileRows;
-  }
-}
-
-// B4: hash every row of a level-1 tile again, sort the tile's hashes by bucket in LDS and copy each
-// bucket's run to its place in that bucket's array (index base[b] + pre_tm[tile][b] + i), as the
-// level-2 kKeySplit layout: hash bits 0..31 in hash_lo, bits 32..39 in hash_hi. pos_out (u16, probe
-// only) records each row's position in the tile's bucket-sorted order.
-template <int K, bool DENSE>
-__global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a, uint64_t n, uint32_t bucket_mask,
-                                                                      const uint32_t* __restrict__ counts_tm,
-                                                                      const uint32_t* __restrict__ pre_tm,
-                                                                      const uint64_t* __restrict__ base,
-                                                                      uint32_t* __restrict__ hash_lo,
-                                                                      uint8_t* __restrict__ hash_hi,
-                                                                      uint16_t* __restrict__ pos_out) {
-  extern __shared__ uint32_t s_lo[];  // kL1TileRows hash words (bits 0..31), bucket-sorted, then
-  uint8_t* s_hi = reinterpret_cast<uint8_t*>(s_lo + kL1TileRows);  // their bits 32..39, then
-  uint16_t* s_bk = reinterpret_cast<uint16_t*>(s_hi + kL1TileRows);  // their bucket (RPT_SCATTER_FLAT_COPY)
-  __shared__ uint32_t s_start[kMaxBuckets], s_cur[kMaxBuckets];
-  __shared__ uint64_t s_dst[kMaxBuckets];  // where each bucket's run goes in the level-2 array
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t nb = bucket_mask + 1;
-  // Workgroups go round-robin to the 8 XCDs; give each XCD a contiguous range of tiles, so the runs of
-  // neighbouring tiles (adjacent in each bucket's array) are written through the same L2 and leave it
-  // as whole lines.
-  const uint32_t per_xcd = gridDim.x / 8, xcd = blockIdx.x % 8;
-  const uint64_t tile = blockIdx.x < per_xcd * 8 ? static_cast<uint64_t>(xcd) * per_xcd + blockIdx.x / 8 : blockIdx.x;
-  const uint64_t tile_base = tile * kL1TileRows;
-  const uint32_t* cnt = counts_tm + tile * nb;
-  for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_dst[i] = base[i] + pre_tm[tile * nb + i];
-  if (wave == 0) {  // exclusive scan of this tile's bucket counts, kMaxBuckets / 64 per lane
+  uint32_t run_p = 0, run_c = 0;  // owner: the run's start in its list and its length
+  if (wave == 0) {  // exclusive scan of the bucket counts, kMaxBuckets / 64 per lane
     constexpr int kPer = kMaxBuckets / 64;
     uint32_t c[kPer], t = 0;
 #pragma unroll
     for (int i = 0; i < kPer; i++) {
       const uint32_t idx = lane * kPer + i;
-      c[i] = idx < nb ? cnt[idx] : 0u;
+      c[i] = idx < nb ? s_cnt[idx] : 0u;
       t += c[i];
     }
     uint32_t off = wave_inclusive_sum(t) - t;
 #pragma unroll
     for (int i = 0; i < kPer; i++) {
       const uint32_t idx = lane * kPer + i;
-      if (idx < nb) s_start[idx] = s_cur[idx] = off;
+      if (idx < nb) s_start[idx] = off;
       off += c[i];
+    }
+  } else if (owner) {  // append the run to its list; take the chunks whose first row it covers
+    run_c = s_cnt[own_b];
+    const uint64_t list = static_cast<uint64_t>(grp) * nb + own_b;
+    if (run_c != 0) {
+      run_p = atomicAdd(&L.cursor[list], run_c);
+      const uint32_t c0 = run_p >> kChunkLog, c1 = (run_p + run_c - 1) >> kChunkLog;
+      for (uint32_t cc = (run_p & (kChunkRows - 1)) ? c0 + 1 : c0; cc <= c1; cc++) {
+        const uint32_t local = atomicAdd(&L.pool[grp], 1u);
+        uint32_t id = grp * L.shard_cap + local;
+        if (local >= L.shard_cap || cc >= L.cmax) {
+          l1_flag_error(L);
+          id = 0;
+        } else {
+          __hip_atomic_store(&L.chunk_tab[list * L.cmax + cc], id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        s_chunk[cc - c0][own_b] = id;
+      }
+    }
+    if (counts_tm != nullptr) {
+      counts_tm[tile * nb + own_b] = run_c;
+      pre_tm[tile * nb + own_b] = run_p;
     }
   }
   __syncthreads();
+  // the rows to their bucket-sorted LDS slots; the row map gets the slot
 #pragma unroll
   for (int sg = 0; sg < kL1SegsPerWave; sg++) {
-    const uint32_t seg_local = wave * (kL1SegsPerWave * kSegRows) + sg * kSegRows;
-    const uint64_t sbase = tile_base + seg_local;
-    uint64_t hh[8];
-    bool oo[8];
-    load_hashes<K, DENSE, false, false, true>(a, sbase, n, lane, hh, oo);
+    const uint64_t sbase = tile_base + wave * (kL1SegsPerWave * kSegRows) + sg * kSegRows;
     uint16_t pv[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
       uint32_t p = 0;
-      if (oo[j]) {
-        const uint32_t b = bucket_of(hh[j], bucket_mask);
-        p = atomicAdd(&s_cur[b], 1u);
-        s_lo[p] = static_cast<uint32_t>(hh[j]);
-        s_hi[p] = static_cast<uint8_t>(hh[j] >> 32);
-        if (RPT_SCATTER_FLAT_COPY) s_bk[p] = static_cast<uint16_t>(b);
+      if (rk[sg][j] != ~0u) {
+        const uint32_t b = bucket_of(hh[sg][j], bucket_mask);
+        p = s_start[b] + rk[sg][j];
+        s_lo[p] = static_cast<uint32_t>(hh[sg][j]);
+        s_hi[p] = static_cast<uint8_t>(hh[sg][j] >> 32);
+        s_bk[p] = static_cast<uint16_t>(b);
       }
       pv[j] = static_cast<uint16_t>(p);
     }
@@ -172,47 +172,106 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
       for (int j = 0; j < 8; j++) pos_out[sbase + seg_row<K, DENSE>(j, lane)] = pv[j];
     }
   }
+  if (owner && run_c != 0) {
+    const uint32_t c0 = run_p >> kChunkLog;
+    if (run_p & (kChunkRows - 1)) {  // the run starts inside a chunk an earlier run took: wait for its id
+      const uint64_t list = static_cast<uint64_t>(grp) * nb + own_b;
+      uint32_t id = 0;
+      if (c0 >= L.cmax) {
+        l1_flag_error(L);
+      } else {
+        uint32_t spins = 0;
+        while ((id = __hip_atomic_load(&L.chunk_tab[list * L.cmax + c0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
+               kChunkEmpty) {
+          if (++spins > kChunkSpinLimit) {
+            l1_flag_error(L);
+            id = 0;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      s_chunk[0][own_b] = id;
+    }
+    s_qc[own_b] = static_cast<uint64_t>(run_p - s_start[own_b]) | (static_cast<uint64_t>(c0) << 32);
+  }
   __syncthreads();
-  if (RPT_SCATTER_FLAT_COPY) {
-    // the tile's bucket-sorted rows in order, every lane busy: a wave's 64 rows span ~2 runs, so each
-    // store instruction writes whole pieces of runs (a loop per bucket leaves half the lanes idle)
-    for (uint32_t b = threadIdx.x; b < nb; b += kTileThreads) s_dst[b] -= s_start[b];
-    __syncthreads();
-    const uint32_t used = s_cur[nb - 1];
-    for (uint32_t i = threadIdx.x; i < used; i += kTileThreads) {
-      const uint64_t d = s_dst[s_bk[i]] + i;
+  // copy-out over the tile's bucket-sorted rows, every lane busy: a wave's 64 rows span ~2 runs, so each
+  // store instruction writes whole pieces of runs
+  const uint32_t used = s_start[nb - 1] + s_cnt[nb - 1];
+  for (uint32_t i = threadIdx.x; i < used; i += kTileThreads) {
+    const uint32_t b = s_bk[i];
+    const uint64_t qc = s_qc[b];
+    const uint32_t q = static_cast<uint32_t>(qc) + i;  // the row's position in its list
+    const uint32_t k = (q >> kChunkLog) - static_cast<uint32_t>(qc >> 32);
+    const uint64_t d = static_cast<uint64_t>(s_chunk[k][b]) * kChunkRows + (q & (kChunkRows - 1));
 #ifndef RPT_EXP_SCATTER_SKIP
 #define RPT_EXP_SCATTER_SKIP 0  // measurement only: 1 = no high-byte stores, 2 = no low-word stores, 3 = neither
 #endif
-      if (!(RPT_EXP_SCATTER_SKIP & 2)) hash_lo[d] = s_lo[i];
-      if (!(RPT_EXP_SCATTER_SKIP & 1)) hash_hi[d] = s_hi[i];
-    }
-  } else {
-    for (uint32_t b = wave; b < nb; b += kTileThreads / 64) {  // LDS only: no global latency in the chain
-      const uint32_t c = s_cur[b] - s_start[b], s0 = s_start[b];
-      const uint64_t d = s_dst[b];
-      for (uint32_t i = lane; i < c; i += 64) {
-        hash_lo[d + i] = s_lo[s0 + i];
-        hash_hi[d + i] = s_hi[s0 + i];
-      }
-    }
+    if (!(RPT_EXP_SCATTER_SKIP & 2)) hash_lo[d] = s_lo[i];
+    if (!(RPT_EXP_SCATTER_SKIP & 1)) hash_hi[d] = s_hi[i];
   }
 }
 
-// B5: pad each bucket's array to whole tiles with copies of its first hash (re-inserting or re-probing
-// a present hash changes nothing, and the pads' results are never read).
-__global__ __launch_bounds__(kBlockThreads) void bucket_pad_kernel(const uint32_t* __restrict__ totals,
-                                                                  const uint64_t* __restrict__ base,
-                                                                  uint32_t* __restrict__ hash_lo,
-                                                                  uint8_t* __restrict__ hash_hi) {
-  const uint32_t b = blockIdx.x;
-  const uint64_t t = totals[b], b0 = base[b], end = base[b + 1];
-  if (t == 0) return;
-  const uint32_t lo = hash_lo[b0];
-  const uint8_t hi = hash_hi[b0];
-  for (uint64_t i = b0 + t + threadIdx.x; i < end; i += kBlockThreads) {
-    hash_lo[i] = lo;
-    hash_hi[i] = hi;
+// B2: per bucket (one workgroup each): its level-2 tiles are its lists' chunks in group order, 4 per tile,
+// the last tile completed with copies of the bucket's last chunk (rows past the lists' ends are never
+// read back); list_base[g][b] = the w-space row of list (g, b)'s first row; bucket_tiles[b] = the
+// bucket's first tile, bucket_tiles[nb] = the tile count (0 if the scatter flagged an error, so level 2
+// then runs on nothing and the result is visibly empty). Each list's last chunk is padded with copies of
+// its first row.
+constexpr int kListsThreads = 256;
+__global__ __launch_bounds__(kListsThreads) void bucket_lists_kernel(L1Lists L, uint32_t nb, uint32_t* __restrict__ chunk_map,
+                                                                    uint64_t* __restrict__ list_base,
+                                                                    uint32_t* __restrict__ bucket_tiles,
+                                                                    uint32_t* __restrict__ hash_lo,
+                                                                    uint8_t* __restrict__ hash_hi) {
+  __shared__ uint32_t s_red[kListsThreads / 64];
+  __shared__ uint32_t s_k[kL1Groups + 1];  // prefix over the bucket's lists of their chunk counts
+  const uint32_t b = blockIdx.x, G = L.groups;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t acc = 0;  // tiles of the buckets before b
+  for (uint32_t bb = threadIdx.x; bb < b; bb += kListsThreads) {
+    uint32_t kk = 0;
+    for (uint32_t g = 0; g < G; g++) kk += static_cast<uint32_t>((L.cursor[g * nb + bb] + kChunkRows - 1) >> kChunkLog);
+    acc += (kk + kChunksPerTile - 1) / kChunksPerTile;
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) s_red[wave] = acc;
+  if (threadIdx.x == 0) {
+    uint32_t kk = 0;
+    for (uint32_t g = 0; g < G; g++) {
+      s_k[g] = kk;
+      kk += static_cast<uint32_t>((L.cursor[g * nb + b] + kChunkRows - 1) >> kChunkLog);
+    }
+    s_k[G] = kk;
+  }
+  __syncthreads();
+  uint32_t first = 0;
+  for (uint32_t w = 0; w < kListsThreads / 64; w++) first += s_red[w];
+  const uint32_t nk = s_k[G], tiles = (nk + kChunksPerTile - 1) / kChunksPerTile;
+  const bool err = *L.error != 0;
+  if (threadIdx.x < G) list_base[threadIdx.x * nb + b] = (static_cast<uint64_t>(first) * kChunksPerTile + s_k[threadIdx.x]) * kChunkRows;
+  if (threadIdx.x == 0) {
+    bucket_tiles[b] = err ? 0u : first;
+    if (b == nb - 1) bucket_tiles[nb] = err ? 0u : first + tiles;
+  }
+  for (uint32_t j = threadIdx.x; j < tiles * kChunksPerTile; j += kListsThreads) {
+    const uint32_t jj = min(j, nk - 1);
+    uint32_t g = 0;
+    while (g + 1 < G && s_k[g + 1] <= jj) g++;
+    chunk_map[static_cast<uint64_t>(first) * kChunksPerTile + j] = L.chunk_tab[(static_cast<uint64_t>(g) * nb + b) * L.cmax + (jj - s_k[g])];
+  }
+  if (err) return;
+  for (uint32_t g = 0; g < G; g++) {
+    const uint32_t rows = L.cursor[g * nb + b], r = rows & (kChunkRows - 1);
+    if (r == 0) continue;  // uniform
+    const uint64_t c0 = static_cast<uint64_t>(L.chunk_tab[(static_cast<uint64_t>(g) * nb + b) * L.cmax + (rows >> kChunkLog)]) * kChunkRows;
+    const uint32_t lo = hash_lo[c0];
+    const uint8_t hi = hash_hi[c0];
+    for (uint32_t i = r + threadIdx.x; i < kChunkRows; i += kListsThreads) {
+      hash_lo[c0 + i] = lo;
+      hash_hi[c0 + i] = hi;
+    }
   }
 }
 
@@ -225,8 +284,8 @@ __global__ __launch_bounds__(kBlockThreads) void bucket_pad_kernel(const uint32_
 constexpr int kBucketUnpermuteThreads = RPT_BUCKET_UNPERMUTE_THREADS;
 __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kernel(
     const uint16_t* __restrict__ pos1, const uint64_t* __restrict__ bits2, uint64_t n, uint32_t bucket_mask,
-    const uint32_t* __restrict__ counts_tm, const uint32_t* __restrict__ pre_tm, const uint64_t* __restrict__ base,
-    uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
+    const uint32_t* __restrict__ counts_tm, const uint32_t* __restrict__ pre_tm, const uint64_t* __restrict__ list_base,
+    uint32_t groups, uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
   __shared__ uint32_t s_bits[kL1TileRows / 32];
   __shared__ uint32_t s_start[kMaxBuckets], s_item[kMaxBuckets + 1], s_cnt[kMaxBuckets];
   __shared__ uint64_t s_g[kMaxBuckets];
@@ -234,14 +293,10 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   constexpr uint32_t kWaves = kBucketUnpermuteThreads / 64;
   const uint32_t nb = bucket_mask + 1;
-#if RPT_BUCKET_UNPERMUTE_XCD_MAP
-  // XCD-contiguous tiles, as the scatter: neighbouring tiles' runs are adjacent in every bucket's array,
-  // so the 64-bit pass-bit pieces one tile gathers share lines with its neighbours' in the same L2
-  const uint32_t per_xcd = gridDim.x / 8, xcd = blockIdx.x % 8;
-  const uint64_t tile = blockIdx.x < per_xcd * 8 ? static_cast<uint64_t>(xcd) * per_xcd + blockIdx.x / 8 : blockIdx.x;
-#else
-  const uint64_t tile = blockIdx.x;
-#endif
+  // XCD-contiguous tiles, as the scatter (same grid): neighbouring tiles' runs are adjacent in their
+  // lists, so the 64-bit pass-bit pieces one tile gathers share lines with its neighbours' in the same L2
+  const uint64_t tile = l1_tile_of_block(blockIdx.x, gridDim.x);
+  const uint64_t* lbase = list_base + static_cast<uint64_t>(l1_group_of_tile(tile, gridDim.x, groups)) * nb;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
   constexpr uint32_t kSegsPerWave = (kL1TileRows / kSegRows) / kWaves;
   const uint64_t seg0 = tile * (kL1TileRows / kSegRows) + wave * kSegsPerWave;
@@ -265,7 +320,7 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
     tk += k[i];
     if (b < nb) {
       s_cnt[b] = c[i];
-      s_g[b] = base[b] + pre_tm[tile * nb + b];
+      s_g[b] = lbase[b] + pre_tm[tile * nb + b];
     }
   }
   const uint32_t ic = wave_inclusive_sum(tc), ik = wave_inclusive_sum(tk);

@@ -61,23 +61,23 @@ __host__ __device__ constexpr uint32_t tile_mult(uint32_t n_slices) { return n_s
 constexpr int kBucketSliceLog = RPT_BUCKET_SLICE_LOG;
 constexpr int kMaxBucketedLog = 31;  // 16 GiB
 constexpr uint32_t kBucketSlices = 1u << kBucketSliceLog;
-constexpr uint32_t kMaxBuckets = 1024;
+constexpr uint32_t kMaxBuckets = 512;  // 16 GiB / 32 MiB
 constexpr int kTileThreads = 1024;                     // 16 waves
 constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
 constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave (bucketed level 2 / build)
-// Level-1 tiles of the bucketed strategy (bucket_count / bucket_scatter / bucket_unpermute): 16 Ki rows,
-// independent of the partition tile (the scatter stages 5 B per row in LDS).
+// Level-1 tiles of the bucketed strategy (bucket_scatter / bucket_unpermute): 16 Ki rows, independent of
+// the partition tile (the scatter stages 7 B per row in LDS).
 constexpr uint64_t kL1TileRows = 16384;
 constexpr int kL1SegsPerWave = static_cast<int>(kL1TileRows / kTileThreads / 8);
+// The level-2 hash array is allocated in chunks of 4 Ki rows (bucketed.hpp); a level-2 tile is 4 chunks
+// of one bucket, so a 512-row segment never straddles two chunks.
+constexpr int kChunkLog = 12;
+constexpr uint64_t kChunkRows = 1ULL << kChunkLog;
+constexpr uint32_t kChunksPerTile = static_cast<uint32_t>(kTileRows / kChunkRows);
+static_assert(kChunkRows % kSegRows == 0 && kTileRows % kChunkRows == 0, "chunks hold whole segments, tiles whole chunks");
 constexpr int kSliceThreads = 1024;                    // slice-probe workgroup (16 waves)
 constexpr int kLdsDirectMaxLog = 14;                   // filters <= 128 KiB: whole filter in LDS
 constexpr int kLdsProbeThreads = 1024;                 // whole-filter LDS probe workgroup (16 waves)
-#ifndef RPT_BUCKET_UNPERMUTE_XCD_MAP
-#define RPT_BUCKET_UNPERMUTE_XCD_MAP 1
-#endif
-#ifndef RPT_SCATTER_FLAT_COPY
-#define RPT_SCATTER_FLAT_COPY 1                        // bucketed level-1 scatter: copy-out over sorted rows
-#endif
 #ifndef RPT_PARTITION_SMALL_P
 #define RPT_PARTITION_SMALL_P 1                        // partition of <= 4-slice filters: wave-aggregated counters
 #endif

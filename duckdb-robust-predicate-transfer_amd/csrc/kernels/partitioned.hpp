@@ -113,9 +113,11 @@ template <int K, bool DENSE, bool MM, int TM, int SP = 0>
 __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4) void partition_kernel(
     KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
     uint16_t* __restrict__ pos_out, uint32_t* __restrict__ runs_tm, int64_t* __restrict__ stats,
-    const uint32_t* __restrict__ dev_n_tiles) {
+    const uint32_t* __restrict__ dev_n_tiles, const uint32_t* __restrict__ chunk_map) {
   // dev_n_tiles (bucketed strategy): the tile count is only known on the device; the grid is an upper
   // bound and surplus workgroups leave (their run-table rows are never read).
+  // chunk_map (bucketed strategy, TM = 1): tile t's rows are the kChunksPerTile chunks chunk_map[4t ..]
+  // of the level-2 hash array (every row valid: the lists are padded); otherwise rows tile * kTR ...
   if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;
   constexpr bool PAD = TM == 1;
   constexpr uint64_t kTR = kTileRows * TM;               // rows of this tile
@@ -146,7 +148,13 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
       uint64_t hh[8];
       bool oo[8];
       int64_t mm[2] = {kMinInit, kMaxInit};
-      load_hashes<K, DENSE, MM, TM == 1 && RPT_NT_KEY_LOADS>(a, tile_base + seg_local, n, lane, hh, oo, mm);
+      if (chunk_map != nullptr) {
+        const uint64_t src = static_cast<uint64_t>(chunk_map[tile * kChunksPerTile + (seg_local >> kChunkLog)]) * kChunkRows +
+                             (seg_local & (kChunkRows - 1));
+        load_hashes<K, DENSE, MM, TM == 1 && RPT_NT_KEY_LOADS>(a, src, ~0ULL, lane, hh, oo, mm);
+      } else {
+        load_hashes<K, DENSE, MM, TM == 1 && RPT_NT_KEY_LOADS>(a, tile_base + seg_local, n, lane, hh, oo, mm);
+      }
       if constexpr (MM && KeyTraits<K>::kValues) {
         wave_minmax(mm[0], mm[1]);
         wmn = min(wmn, mm[0]);

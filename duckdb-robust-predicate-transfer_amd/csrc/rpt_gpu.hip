@@ -290,17 +290,18 @@ struct ProbeWorkspace {
   uint8_t* passb;
   uint32_t* runs;     // slice-major [slice][tile]
   uint32_t* runs_tm;  // tile-major [tile][slice] (partition kernel output)
-  // bucketed strategy, level 1
-  uint32_t* counts_tm;     // [tile1][bucket] rows
-  uint32_t* pre_bm;        // [bucket][tile1] run start inside the bucket's array
-  uint32_t* pre_tm;        // [tile1][bucket] the same, tile-major
-  uint32_t* totals;        // [bucket] rows
-  uint64_t* bbase;         // [bucket + 1] first row of the bucket in the level-2 array
+  // bucketed strategy, level 1 (bucketed.hpp)
+  uint32_t* counts_tm;     // [tile1][bucket] rows of the tile's run
+  uint32_t* pre_tm;        // [tile1][bucket] the run's start in its list
+  uint64_t* list_base;     // [group][bucket] w-space row of the list's first row
   uint32_t* bucket_tiles;  // [bucket + 1] first level-2 tile of the bucket; [nb] = level-2 tile count
-  uint32_t* hash_lo;       // level-2 array (kKeySplit): per bucket, its rows' hashes padded to whole
-  uint8_t* hash_hi;        // tiles -- bits 0..31 and bits 32..39
+  uint32_t* chunk_map;     // [level-2 tile][4] chunk ids
+  uint32_t* lists;         // cursors, pool counters, error flag (L1Lists)
+  uint32_t* chunk_tab;     // L1Lists::chunk_tab
+  uint32_t* hash_lo;       // level-2 array (kKeySplit) in 4 Ki-row chunks: hash bits 0..31
+  uint8_t* hash_hi;        // and bits 32..39
   uint16_t* pos1;          // row -> position in its level-1 tile's bucket-sorted order
-  uint64_t* bits2;         // level-2 result bits (level-2 array order)
+  uint64_t* bits2;         // level-2 result bits (w-space order)
 };
 
 uint32_t slice_count(int log_num_blocks) {
@@ -348,10 +349,36 @@ int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
   return RPT_PROBE_GATHER;
 }
 
-// Tile-count bound of the bucketed level-2 array: every non-empty bucket pads < 1 tile.
-uint64_t level2_tiles_max(uint64_t n, int log_num_blocks) {
-  return ceil_div(n, rpt::kTileRows) + std::min<uint64_t>(bucket_count(log_num_blocks), n);
+// Geometry of the bucketed level 1 for a batch of n rows (bucketed.hpp): 8 list groups (one per XCD
+// share) for large batches, 1 below RPT_L1_GROUPS_MIN_ROWS (8 lists per bucket would pad too much);
+// chunk pool shards and the level-2 tile bound.
+constexpr uint64_t kL1GroupsMinRows = 1ULL << 27;
+struct L1Geom {
+  uint64_t t1;          // level-1 tiles
+  uint32_t nb, groups;  // buckets, list groups
+  uint64_t cmax;        // chunks per list (bound)
+  uint64_t shard_cap;   // chunks per pool shard (bound)
+  uint64_t pool_chunks; // groups * shard_cap
+  uint64_t t2max;       // level-2 tiles (bound)
+};
+L1Geom l1_geom(uint64_t n, int log_num_blocks) {
+  static const uint64_t min_rows = [] {
+    const char* e = std::getenv("RPT_L1_GROUPS_MIN_ROWS");  // tuning runs only
+    return e ? static_cast<uint64_t>(std::strtoull(e, nullptr, 10)) : kL1GroupsMinRows;
+  }();
+  L1Geom g;
+  g.t1 = ceil_div(n, rpt::kL1TileRows);
+  g.nb = bucket_count(log_num_blocks);
+  g.groups = n >= min_rows ? rpt::kL1Groups : 1u;
+  const uint64_t tiles_per_group = ceil_div(g.t1, g.groups);  // tiles of workgroups b with b % 8 == g
+  const uint64_t chunks_per_tile = rpt::kL1TileRows / rpt::kChunkRows;
+  g.cmax = tiles_per_group * chunks_per_tile + 1;        // a list holds at most its group's rows
+  g.shard_cap = tiles_per_group * chunks_per_tile + g.nb;  // + one part-filled chunk per list
+  g.pool_chunks = g.groups * g.shard_cap;
+  g.t2max = ceil_div(g.pool_chunks, rpt::kChunksPerTile) + g.nb;  // + one part-filled tile per bucket
+  return g;
 }
+uint64_t level2_tiles_max(uint64_t n, int log_num_blocks) { return l1_geom(n, log_num_blocks).t2max; }
 
 // rpt::tile_mult, with its slice threshold overridable for tuning runs (RPT_TILE_MULT_SLICES: tiles
 // double above that many slices).
@@ -370,7 +397,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
   const uint64_t T = rpt::kTileRows;
-  constexpr int kParts = 19;
+  constexpr int kParts = 20;
   size_t sz[kParts] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
                        align256(n_groups * 4), align256(n_groups * 4)};
   const bool part = strategy == RPT_PROBE_PARTITIONED, buck = strategy == RPT_PROBE_BUCKETED;
@@ -386,16 +413,17 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     sz[8] = sz[7];
   }
   if (buck) {
-    const uint64_t t1 = ceil_div(n, rpt::kL1TileRows), t2 = level2_tiles_max(n, log_num_blocks);
-    const uint64_t nb = bucket_count(log_num_blocks);
-    sz[9] = sz[10] = sz[11] = align256(t1 * nb * 4);
-    sz[12] = align256(nb * 4);
-    sz[13] = align256((nb + 1) * 8);
-    sz[14] = align256((nb + 1) * 4);
-    sz[15] = align256(t2 * T * 4);
-    sz[16] = align256(t1 * rpt::kL1TileRows * 2);
-    sz[17] = align256(t2 * T / 8);
-    sz[18] = align256(t2 * T);
+    const L1Geom g = l1_geom(n, log_num_blocks);
+    sz[9] = sz[10] = align256(g.t1 * g.nb * 4);
+    sz[11] = align256(static_cast<uint64_t>(g.groups) * g.nb * 8);
+    sz[12] = align256((g.nb + 1) * 4);
+    sz[13] = align256(g.t2max * rpt::kChunksPerTile * 4);
+    sz[14] = align256((static_cast<uint64_t>(g.groups) * g.nb + g.groups + 1) * 4);
+    sz[15] = align256(static_cast<uint64_t>(g.groups) * g.nb * g.cmax * 4);
+    sz[16] = align256(g.pool_chunks * rpt::kChunkRows * 4);
+    sz[17] = align256(g.t1 * rpt::kL1TileRows * 2);
+    sz[18] = align256(g.t2max * T / 8);
+    sz[19] = align256(g.pool_chunks * rpt::kChunkRows);
   }
   size_t off[kParts], total = 0;
   for (int i = 0; i < kParts; i++) {
@@ -415,15 +443,16 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     ws->runs = static_cast<uint32_t*>(at(7));
     ws->runs_tm = static_cast<uint32_t*>(at(8));
     ws->counts_tm = static_cast<uint32_t*>(at(9));
-    ws->pre_bm = static_cast<uint32_t*>(at(10));
-    ws->pre_tm = static_cast<uint32_t*>(at(11));
-    ws->totals = static_cast<uint32_t*>(at(12));
-    ws->bbase = static_cast<uint64_t*>(at(13));
-    ws->bucket_tiles = static_cast<uint32_t*>(at(14));
-    ws->hash_lo = static_cast<uint32_t*>(at(15));
-    ws->pos1 = static_cast<uint16_t*>(at(16));
-    ws->bits2 = static_cast<uint64_t*>(at(17));
-    ws->hash_hi = static_cast<uint8_t*>(at(18));
+    ws->pre_tm = static_cast<uint32_t*>(at(10));
+    ws->list_base = static_cast<uint64_t*>(at(11));
+    ws->bucket_tiles = static_cast<uint32_t*>(at(12));
+    ws->chunk_map = static_cast<uint32_t*>(at(13));
+    ws->lists = static_cast<uint32_t*>(at(14));
+    ws->chunk_tab = static_cast<uint32_t*>(at(15));
+    ws->hash_lo = static_cast<uint32_t*>(at(16));
+    ws->pos1 = static_cast<uint16_t*>(at(17));
+    ws->bits2 = static_cast<uint64_t*>(at(18));
+    ws->hash_hi = static_cast<uint8_t*>(at(19));
   }
   return total;
 }
@@ -434,34 +463,38 @@ struct InsertWorkspace {
   uint32_t* recs;
   uint32_t* runs;
   uint32_t* runs_tm;
-  uint32_t* counts_tm;
-  uint32_t* pre_bm;
-  uint32_t* pre_tm;
-  uint32_t* totals;
-  uint64_t* bbase;
   uint32_t* bucket_tiles;
+  uint32_t* chunk_map;
+  uint32_t* lists;
+  uint32_t* chunk_tab;
   uint32_t* hash_lo;
   uint8_t* hash_hi;
+  uint64_t* list_base;
 };
+
+// rpt_bf_insert_ws runs a bucketed insert of more rows in batches of this many
+constexpr uint64_t kBucketedInsertBatch = 1ULL << 31;
 
 size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base, InsertWorkspace* ws) {
   const bool buck = strategy == RPT_INSERT_BUCKETED;
   if (strategy != RPT_INSERT_PARTITIONED && !buck) return 0;
+  if (buck) n = std::min(n, kBucketedInsertBatch);
   const uint64_t T = rpt::kTileRows;
   const uint32_t slices = buck ? rpt::kBucketSlices : slice_count(log_num_blocks);
   const uint32_t tm = buck ? 1u : tile_mult_of(slices);
   const uint64_t tiles = buck ? level2_tiles_max(n, log_num_blocks) : ceil_div(n, T * tm);
-  constexpr int kParts = 11;
+  constexpr int kParts = 10;
   size_t sz[kParts] = {align256(tiles * rpt::tile_cap_for(slices, tm) * 4), align256(static_cast<uint64_t>(slices) * tiles * 4),
                        align256(static_cast<uint64_t>(slices) * tiles * 4)};
   if (buck) {
-    const uint64_t t1 = ceil_div(n, rpt::kL1TileRows), nb = bucket_count(log_num_blocks);
-    sz[3] = sz[4] = sz[5] = align256(t1 * nb * 4);
-    sz[6] = align256(nb * 4);
-    sz[7] = align256((nb + 1) * 8);
-    sz[8] = align256((nb + 1) * 4);
-    sz[9] = align256(tiles * T * 4);
-    sz[10] = align256(tiles * T);
+    const L1Geom g = l1_geom(n, log_num_blocks);
+    sz[3] = align256((g.nb + 1) * 4);
+    sz[4] = align256(g.t2max * rpt::kChunksPerTile * 4);
+    sz[5] = align256((static_cast<uint64_t>(g.groups) * g.nb + g.groups + 1) * 4);
+    sz[6] = align256(static_cast<uint64_t>(g.groups) * g.nb * g.cmax * 4);
+    sz[7] = align256(g.pool_chunks * rpt::kChunkRows * 4);
+    sz[8] = align256(g.pool_chunks * rpt::kChunkRows);
+    sz[9] = align256(static_cast<uint64_t>(g.groups) * g.nb * 8);
   }
   size_t off[kParts], total = 0;
   for (int i = 0; i < kParts; i++) {
@@ -474,14 +507,13 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
     ws->recs = static_cast<uint32_t*>(at(0));
     ws->runs = static_cast<uint32_t*>(at(1));
     ws->runs_tm = static_cast<uint32_t*>(at(2));
-    ws->counts_tm = static_cast<uint32_t*>(at(3));
-    ws->pre_bm = static_cast<uint32_t*>(at(4));
-    ws->pre_tm = static_cast<uint32_t*>(at(5));
-    ws->totals = static_cast<uint32_t*>(at(6));
-    ws->bbase = static_cast<uint64_t*>(at(7));
-    ws->bucket_tiles = static_cast<uint32_t*>(at(8));
-    ws->hash_lo = static_cast<uint32_t*>(at(9));
-    ws->hash_hi = static_cast<uint8_t*>(at(10));
+    ws->bucket_tiles = static_cast<uint32_t*>(at(3));
+    ws->chunk_map = static_cast<uint32_t*>(at(4));
+    ws->lists = static_cast<uint32_t*>(at(5));
+    ws->chunk_tab = static_cast<uint32_t*>(at(6));
+    ws->hash_lo = static_cast<uint32_t*>(at(7));
+    ws->hash_hi = static_cast<uint8_t*>(at(8));
+    ws->list_base = static_cast<uint64_t*>(at(9));
   }
   return total;
 }
@@ -568,10 +600,10 @@ void allow_dynamic_lds(const void* fn) {
 template <int K, bool D, bool MM, int TM, int SP = 0>
 void launch_partition_tm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t slice_mask,
                          uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
-                         const uint32_t* dev_n_tiles) {
+                         const uint32_t* dev_n_tiles, const uint32_t* chunk_map) {
   if constexpr (TM == 1 && SP == 0) {
     if (RPT_PARTITION_SMALL_P && slice_mask + 1 <= 4) {  // few slices: wave-aggregated slice counters
-      launch_partition_tm<K, D, MM, 1, 4>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+      launch_partition_tm<K, D, MM, 1, 4>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles, chunk_map);
       return;
     }
   }
@@ -580,7 +612,7 @@ void launch_partition_tm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, ui
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::partition_kernel<K, D, MM, TM, SP>)); });
   ProfScope prof(inst_name<K, D, MM, TM, SP>("partition_kernel"), s);
   hipLaunchKernelGGL((rpt::partition_kernel<K, D, MM, TM, SP>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n,
-                     slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+                     slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles, chunk_map);
   prof.end();
 }
 
@@ -590,9 +622,9 @@ void launch_partition_mm(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, ui
                          uint64_t n_tiles, uint32_t* recs, uint16_t* pos, uint32_t* runs, int64_t* stats,
                          const uint32_t* dev_n_tiles, uint32_t tm) {
   if (tm == 2)
-    launch_partition_tm<K, D, MM, 2>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+    launch_partition_tm<K, D, MM, 2>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles, nullptr);
   else
-    launch_partition_tm<K, D, MM, 1>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles);
+    launch_partition_tm<K, D, MM, 1>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, stats, dev_n_tiles, nullptr);
 }
 
 // stats == nullptr: probe (no min/max); otherwise the build's key min/max is folded into stats.
@@ -606,6 +638,15 @@ void launch_partition_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uin
     launch_partition_mm<K, D, false>(grid, s, a, n, slice_mask, n_tiles, recs, pos, runs, nullptr, dev_n_tiles, tm);
 }
 
+// Level 2 of the bucketed strategies: the partition over the level-2 hash array, tile t = chunks
+// chunk_map[4t ..] (bucketed.hpp).
+void launch_partition_level2(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint64_t n_tiles,
+                             uint32_t* recs, uint16_t* pos, uint32_t* runs, const uint32_t* dev_n_tiles,
+                             const uint32_t* chunk_map) {
+  launch_partition_tm<rpt::kKeySplit, true, false, 1>(grid, s, a, n, rpt::kBucketSlices - 1, n_tiles, recs, pos, runs,
+                                                      nullptr, dev_n_tiles, chunk_map);
+}
+
 template <int K, bool D>
 void launch_insert_t(unsigned grid, hipStream_t s, rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n, uint64_t n_segs) {
   ProfScope prof(inst_name<K, D>("insert_kernel"), s);
@@ -615,32 +656,25 @@ void launch_insert_t(unsigned grid, hipStream_t s, rpt_bf* bf, const rpt::KeyArg
 }
 
 template <int K, bool D>
-void launch_bucket_count_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
-                           uint32_t* counts_tm, int64_t* stats) {
+void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
+                             const rpt::L1Lists& lists, uint32_t* hash_lo, uint8_t* hash_hi, uint16_t* pos1,
+                             uint32_t* counts_tm, uint32_t* pre_tm, int64_t* stats) {
+  const size_t lds = rpt::kL1TileRows * 7;  // hash words, high bytes, buckets
   if (rpt::KeyTraits<K>::kValues && stats != nullptr) {
-    ProfScope prof(inst_name<K, D, true>("bucket_count_kernel"), s);
-    hipLaunchKernelGGL((rpt::bucket_count_kernel<K, D, true>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n,
-                       bucket_mask, counts_tm, stats);
+    static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into (160 KiB minus the static part)
+    std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D, true>)); });
+    ProfScope prof(inst_name<K, D, true>("bucket_scatter_kernel"), s);
+    hipLaunchKernelGGL((rpt::bucket_scatter_kernel<K, D, true>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n,
+                       bucket_mask, lists, hash_lo, hash_hi, pos1, counts_tm, pre_tm, stats);
     prof.end();
   } else {
-    ProfScope prof(inst_name<K, D, false>("bucket_count_kernel"), s);
-    hipLaunchKernelGGL((rpt::bucket_count_kernel<K, D, false>), dim3(grid), dim3(rpt::kTileThreads), 0, s, a, n,
-                       bucket_mask, counts_tm, static_cast<int64_t*>(nullptr));
+    static std::once_flag once;
+    std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D, false>)); });
+    ProfScope prof(inst_name<K, D, false>("bucket_scatter_kernel"), s);
+    hipLaunchKernelGGL((rpt::bucket_scatter_kernel<K, D, false>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n,
+                       bucket_mask, lists, hash_lo, hash_hi, pos1, counts_tm, pre_tm, static_cast<int64_t*>(nullptr));
     prof.end();
   }
-}
-
-template <int K, bool D>
-void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
-                             const uint32_t* counts_tm, const uint32_t* pre_tm, const uint64_t* bbase, uint32_t* hash_lo,
-                             uint8_t* hash_hi, uint16_t* pos1) {
-  const size_t lds = rpt::kL1TileRows * (RPT_SCATTER_FLAT_COPY ? 7 : 5);
-  static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into (160 KiB minus the static part)
-  std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D>)); });
-  ProfScope prof(inst_name<K, D>("bucket_scatter_kernel"), s);
-  hipLaunchKernelGGL((rpt::bucket_scatter_kernel<K, D>), dim3(grid), dim3(rpt::kTileThreads), lds, s, a, n, bucket_mask,
-                     counts_tm, pre_tm, bbase, hash_lo, hash_hi, pos1);
-  prof.end();
 }
 
 #define RPT_DISPATCH_KD(fn, kt, dense, ...)                  \
@@ -672,44 +706,38 @@ int transpose_u32(hipStream_t s, const uint32_t* in, uint64_t rows, uint64_t col
   return RPT_OK;
 }
 
-// Level 1 of the bucketed strategies: rows per (tile, bucket) [+ the build's min/max], the buckets'
-// prefix tables and bases, every row's hash copied into its bucket's array (+ its position in the
-// tile's bucket-sorted order when pos1 != nullptr), each array padded to whole tiles.
+// Level 1 of the bucketed strategies (bucketed.hpp): one pass over the keys appends every row's hash to
+// its (group, bucket) list of chunks [+ the build's min/max; + the probe's row map and run tables], then
+// the lists are laid out as level-2 tiles (chunk_map, bucket_tiles, list_base) and padded.
 struct BucketLevel1 {
-  uint32_t *counts_tm, *pre_bm, *pre_tm, *totals, *bucket_tiles;
-  uint64_t* bbase;
+  uint32_t* lists;      // cursors | pool counters | error flag
+  uint32_t* chunk_tab;
+  uint32_t* chunk_map;
+  uint32_t* bucket_tiles;
+  uint64_t* list_base;
   uint32_t* hash_lo;
   uint8_t* hash_hi;
-  uint16_t* pos1;
+  uint16_t* pos1;       // probe only
+  uint32_t* counts_tm;  // probe only
+  uint32_t* pre_tm;     // probe only
 };
 int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool dense, uint64_t n, int L,
                       const BucketLevel1& w, int64_t* stats) {
-  const uint32_t nb = bucket_count(L);
-  const uint64_t t1 = ceil_div(n, rpt::kL1TileRows);
-  RPT_DISPATCH_KD(launch_bucket_count_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm, stats);
-  RPT_LAUNCHED("bucket_count_kernel");
-  int st = transpose_u32(s, w.counts_tm, t1, nb, w.pre_bm);
-  if (st != RPT_OK) return st;
-  {
-    ProfScope prof_s("bucket_scan_kernel", s);
-    hipLaunchKernelGGL(rpt::bucket_scan_kernel, dim3(nb), dim3(1024), 0, s, w.pre_bm, t1, w.totals);
-    prof_s.end();
-    ProfScope prof_b("bucket_base_kernel", s);
-    hipLaunchKernelGGL(rpt::bucket_base_kernel, dim3(1), dim3(1024), 0, s, w.totals, nb, w.bbase, w.bucket_tiles);
-    prof_b.end();
-    RPT_LAUNCHED("bucket_scan_kernel");
-  }
-  st = transpose_u32(s, w.pre_bm, nb, t1, w.pre_tm);
-  if (st != RPT_OK) return st;
-  {
-    RPT_DISPATCH_KD(launch_bucket_scatter_t, key_type, dense, static_cast<unsigned>(t1), s, a, n, nb - 1, w.counts_tm,
-                    w.pre_tm, w.bbase, w.hash_lo, w.hash_hi, w.pos1);
-    ProfScope prof_x("bucket_pad_kernel", s);
-    hipLaunchKernelGGL(rpt::bucket_pad_kernel, dim3(nb), dim3(rpt::kBlockThreads), 0, s, w.totals, w.bbase, w.hash_lo,
-                       w.hash_hi);
-    prof_x.end();
-    RPT_LAUNCHED("bucket_scatter_kernel");
-  }
+  const L1Geom g = l1_geom(n, L);
+  const uint64_t n_lists = static_cast<uint64_t>(g.groups) * g.nb;
+  RPT_HIP(hipMemsetAsync(w.lists, 0, (n_lists + g.groups + 1) * 4, s));
+  RPT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.chunk_tab), static_cast<int>(rpt::kChunkEmpty),
+                            n_lists * g.cmax, s));
+  const rpt::L1Lists lists{w.lists, w.lists + n_lists, w.lists + n_lists + g.groups, w.chunk_tab,
+                           static_cast<uint32_t>(g.cmax), static_cast<uint32_t>(g.shard_cap), g.groups};
+  RPT_DISPATCH_KD(launch_bucket_scatter_t, key_type, dense, static_cast<unsigned>(g.t1), s, a, n, g.nb - 1, lists, w.hash_lo,
+                  w.hash_hi, w.pos1, w.counts_tm, w.pre_tm, stats);
+  RPT_LAUNCHED("bucket_scatter_kernel");
+  ProfScope prof("bucket_lists_kernel", s);
+  hipLaunchKernelGGL(rpt::bucket_lists_kernel, dim3(g.nb), dim3(rpt::kListsThreads), 0, s, lists, g.nb, w.chunk_map,
+                     w.list_base, w.bucket_tiles, w.hash_lo, w.hash_hi);
+  prof.end();
+  RPT_LAUNCHED("bucket_lists_kernel");
   return RPT_OK;
 }
 
@@ -1044,6 +1072,21 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
                 buck ? "bucketed" : "partitioned", L);
   int st = check_col(col);
   if (st != RPT_OK) return st;
+  if (buck && n > kBucketedInsertBatch) {  // level-1 list positions are 32-bit: batches of 2^31 rows
+    const size_t elem = col->key_type == RPT_KEY_I32 ? 4 : 8;
+    for (uint64_t off = 0; off < n; off += kBucketedInsertBatch) {
+      rpt_key_column sub = *col;
+      if (col->key_sel) {
+        sub.key_sel = col->key_sel + off;  // dictionary: the selection indexes the whole key array
+      } else {
+        sub.keys = static_cast<const char*>(col->keys) + off * elem;
+        if (col->validity) sub.validity = col->validity + off / 64;  // off is a multiple of 64
+      }
+      st = rpt_bf_insert_ws(bf, &sub, std::min(kBucketedInsertBatch, n - off), workspace, workspace_bytes, stream);
+      if (st != RPT_OK) return st;
+    }
+    return RPT_OK;
+  }
   const size_t need = insert_workspace_layout(n, L, strategy, nullptr, nullptr);
   if (!workspace || workspace_bytes < need)
     return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
@@ -1066,15 +1109,12 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   uint32_t tile_slices = slice_count(L), tm = tile_mult_of(tile_slices);
   uint64_t n_tiles = ceil_div(n, rpt::kTileRows * tm), n_part = n;
   rpt::KeyArgs pa = a;
-  int p_type = col->key_type;
-  bool p_dense = dense;
-  int64_t* p_stats = bf->stats;
   const uint32_t* bucket_tiles = nullptr;
   const uint32_t* dev_n_tiles = nullptr;
   uint32_t grid_slices = tile_slices;
-  if (buck) {
-    const BucketLevel1 l1{ws.counts_tm, ws.pre_bm, ws.pre_tm, ws.totals, ws.bucket_tiles, ws.bbase, ws.hash_lo, ws.hash_hi,
-                          nullptr};
+  if (buck) {  // (the key min/max comes from level 1's key read)
+    const BucketLevel1 l1{ws.lists, ws.chunk_tab, ws.chunk_map, ws.bucket_tiles, ws.list_base, ws.hash_lo, ws.hash_hi,
+                          nullptr, nullptr, nullptr};
     st = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, bf->stats);
     if (st != RPT_OK) return st;
     tile_slices = rpt::kBucketSlices;
@@ -1082,19 +1122,16 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
     n_tiles = level2_tiles_max(n, L);
     n_part = n_tiles * rpt::kTileRows;
     pa = rpt::KeyArgs{ws.hash_lo, nullptr, nullptr, nullptr, ws.hash_hi};
-    p_type = rpt::kKeySplit;
-    p_dense = true;
-    p_stats = nullptr;  // min/max came from the key read of level 1
     bucket_tiles = ws.bucket_tiles;
     dev_n_tiles = ws.bucket_tiles + bucket_count(L);
     grid_slices = bucket_count(L) * rpt::kBucketSlices;
   }
-  if (p_type == rpt::kKeySplit)
-    launch_partition_t<rpt::kKeySplit, true>(static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1, n_tiles,
-                                             ws.recs, nullptr, ws.runs_tm, p_stats, dev_n_tiles, 1u);
+  if (buck)
+    launch_partition_level2(static_cast<unsigned>(n_tiles), s, pa, n_part, n_tiles, ws.recs, nullptr, ws.runs_tm, dev_n_tiles,
+                            ws.chunk_map);
   else
-    RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
-                    n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, p_stats, dev_n_tiles, tm);
+    RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
+                    n_tiles, ws.recs, static_cast<uint16_t*>(nullptr), ws.runs_tm, bf->stats, dev_n_tiles, tm);
   RPT_LAUNCHED("partition_kernel");
   st = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
   if (st != RPT_OK) return st;
@@ -1191,15 +1228,13 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     uint32_t tile_slices = slice_count(L), grid_slices = tile_slices, tm = tile_mult_of(tile_slices);
     uint64_t n_tiles = ceil_div(n, rpt::kTileRows * tm), n_part = n;
     rpt::KeyArgs pa = a;
-    int p_type = col->key_type;
-    bool p_dense = dense;
     const uint32_t* bucket_tiles = nullptr;
     const uint32_t* dev_n_tiles = nullptr;
     uint64_t* part_bits = ws.bits;
     uint32_t* part_counts = ws.seg_counts;
     if (buck) {
-      const BucketLevel1 l1{ws.counts_tm, ws.pre_bm, ws.pre_tm, ws.totals, ws.bucket_tiles, ws.bbase, ws.hash_lo,
-                            ws.hash_hi, ws.pos1};
+      const BucketLevel1 l1{ws.lists, ws.chunk_tab, ws.chunk_map, ws.bucket_tiles, ws.list_base, ws.hash_lo, ws.hash_hi,
+                            ws.pos1, ws.counts_tm, ws.pre_tm};
       int st1 = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, nullptr);
       if (st1 != RPT_OK) return st1;
       tile_slices = rpt::kBucketSlices;
@@ -1208,19 +1243,17 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
       n_tiles = level2_tiles_max(n, L);
       n_part = n_tiles * rpt::kTileRows;
       pa = rpt::KeyArgs{ws.hash_lo, nullptr, nullptr, nullptr, ws.hash_hi};
-      p_type = rpt::kKeySplit;
-      p_dense = true;
       bucket_tiles = ws.bucket_tiles;
       dev_n_tiles = ws.bucket_tiles + bucket_count(L);
       part_bits = ws.bits2;
       part_counts = nullptr;
     }
     const int cus = num_cus(bf->device);
-    if (p_type == rpt::kKeySplit)
-      launch_partition_t<rpt::kKeySplit, true>(static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1, n_tiles,
-                                               ws.recs, ws.pos, ws.runs_tm, nullptr, dev_n_tiles, 1u);
+    if (buck)
+      launch_partition_level2(static_cast<unsigned>(n_tiles), s, pa, n_part, n_tiles, ws.recs, ws.pos, ws.runs_tm, dev_n_tiles,
+                              ws.chunk_map);
     else
-      RPT_DISPATCH_KD(launch_partition_t, p_type, p_dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
+      RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
                       n_tiles, ws.recs, ws.pos, ws.runs_tm, static_cast<int64_t*>(nullptr), dev_n_tiles, tm);
     RPT_LAUNCHED("partition_kernel");
     int st2 = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
@@ -1285,7 +1318,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
       ProfScope prof8b_("bucket_unpermute_kernel", s);
       hipLaunchKernelGGL(rpt::bucket_unpermute_kernel, dim3(static_cast<unsigned>(ceil_div(n, rpt::kL1TileRows))),
                          dim3(rpt::kBucketUnpermuteThreads), 0, s, ws.pos1, ws.bits2, n, bucket_count(L) - 1,
-                         ws.counts_tm, ws.pre_tm, ws.bbase, ws.bits, ws.seg_counts);
+                         ws.counts_tm, ws.pre_tm, ws.list_base, l1_geom(n, L).groups, ws.bits, ws.seg_counts);
       prof8b_.end();
       RPT_LAUNCHED("bucket_unpermute_kernel");
     }
