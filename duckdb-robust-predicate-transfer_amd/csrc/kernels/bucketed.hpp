@@ -14,15 +14,18 @@ namespace rpt {
 // bucket totals, then the scatter). Each level-1 tile (16 Ki rows) sorts its rows by bucket in LDS and
 // APPENDS each bucket's run to a list: list (g, b) for bucket b and group g = the workgroup's XCD (8
 // groups, so a list's neighbouring runs leave one L2 and merge there into whole lines; 1 group for
-// small batches, where 8 lists per bucket would pad too much). A list is a sequence of 4 Ki-row chunks
-// taken from a pool on the device: a run's rows [p, p + c) of its list come from one returning atomic
-// on the list's row cursor; the run that covers a chunk's first row takes the chunk (an atomic on its
-// group's pool shard) and publishes its id in chunk_tab; a run starting inside a chunk waits for that
-// id (its taker did its cursor atomic earlier, publishes without waiting for anything, and so
-// finishes; the wait is bounded anyway and flags `error`). bucket_lists_kernel then lays every bucket's
-// lists out as consecutive level-2 tiles of 4 chunks ("w-space": the row order level 2 sees) through
-// chunk_map, and pads each list's last chunk with copies of one of its hashes (re-inserting or
-// re-probing a present hash changes nothing; the pads' results are never read).
+// small batches, where 8 lists per bucket would pad too much). A list is a sequence of 4 Ki-row chunks: a
+// run's rows [p, p + c) of its list come from one returning atomic on the list's row cursor, whose
+// latency overlaps the LDS sort. The first K chunks of every list have fixed ids (list * K + c; K = 1 by
+// default, rpt_gpu.hip RPT_L1_FIXED_PCT). Beyond K a list grows by extents of kExtentChunks chunks
+// taken from its group's pool shard (one atomic per 64 Ki rows of a list): the run that
+// covers an extent's first row takes it and publishes its first chunk id in ext_dir; a run that starts
+// inside an extent someone else took waits for that id (its taker did its cursor atomic earlier and
+// publishes before waiting for anything, so it finishes; the wait is bounded anyway and flags `error`).
+// bucket_lists_kernel then lays every bucket's lists out as consecutive level-2 tiles of 4 chunks
+// ("w-space": the row order level 2 sees) through chunk_map, and pads each list's last chunk with copies
+// of one of its hashes (re-inserting or re-probing a present hash changes nothing; the pads' results are
+// never read).
 static_assert(kLogNumMasks + 6 + kSliceLog + kBucketSliceLog <= 40, "level-2 split hashes carry bits 0..39");
 __device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t bucket_mask) {
   return static_cast<uint32_t>(h >> (kLogNumMasks + 6 + kSliceLog + kBucketSliceLog)) & bucket_mask;
@@ -31,17 +34,29 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t bucket_mask) 
 constexpr uint32_t kChunkEmpty = ~0u;
 constexpr uint32_t kMaxRunChunks = static_cast<uint32_t>(kL1TileRows / kChunkRows) + 1;  // chunks one run can touch
 constexpr uint32_t kL1Groups = 8;
+constexpr uint32_t kExtentChunks = 16;          // overflow extents: 64 Ki rows
 constexpr uint32_t kChunkSpinLimit = 1u << 22;  // ~0.3 s of polling: never reached unless a kernel is broken
 
 struct L1Lists {
   uint32_t* cursor;     // [groups * nb] rows appended to each list        } zeroed before the scatter
-  uint32_t* pool;       // [groups] chunks taken from each group's shard    }
+  uint32_t* pool;       // [groups] extents taken from each group's shard   }
   uint32_t* error;      // [1] a bound was hit (never expected)             }
-  uint32_t* chunk_tab;  // [groups * nb][cmax] chunk id of a list's c-th chunk (kChunkEmpty until taken)
-  uint32_t cmax;        // chunks per list: <= 4 * ceil(t1 / groups) + 1
-  uint32_t shard_cap;   // chunks per pool shard: <= 4 * ceil(t1 / groups) + nb
+  uint32_t* ext_dir;    // [groups * nb][n_ext] first chunk id of a list's e-th extent (kChunkEmpty until taken)
+  uint32_t k_fixed;     // K: chunks with fixed ids per list
+  uint32_t n_ext;       // extents per list (bound)
+  uint32_t shard_ext;   // extents per pool shard (bound)
   uint32_t groups;      // 1 or kL1Groups
+  uint32_t n_lists;     // groups * nb
 };
+
+// Chunk id of chunk c of list `list` when it is a fixed one or its extent is published (else kChunkEmpty).
+__device__ __forceinline__ uint32_t l1_chunk_id(const L1Lists& L, uint64_t list, uint32_t c) {
+  if (c < L.k_fixed) return static_cast<uint32_t>(list * L.k_fixed + c);
+  const uint32_t x = c - L.k_fixed, e = x / kExtentChunks;
+  if (e >= L.n_ext) return kChunkEmpty;
+  const uint32_t base = __hip_atomic_load(&L.ext_dir[list * L.n_ext + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return base == kChunkEmpty ? kChunkEmpty : base + x % kExtentChunks;
+}
 
 // Level-1 tiles are mapped XCD-contiguously (workgroup b runs on XCD b % 8): each XCD gets a contiguous
 // tile range. The list group of a tile is the XCD share of the workgroup that scattered it.
@@ -110,6 +125,7 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
   if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
   __syncthreads();
   uint32_t run_p = 0, run_c = 0;  // owner: the run's start in its list and its length
+  const uint64_t list = static_cast<uint64_t>(grp) * nb + own_b;
   if (wave == 0) {  // exclusive scan of the bucket counts, kMaxBuckets / 64 per lane
     constexpr int kPer = kMaxBuckets / 64;
     uint32_t c[kPer], t = 0;
@@ -126,28 +142,9 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
       if (idx < nb) s_start[idx] = off;
       off += c[i];
     }
-  } else if (owner) {  // append the run to its list; take the chunks whose first row it covers
+  } else if (owner) {  // append the run to its list (the returned start is used after the LDS sort)
     run_c = s_cnt[own_b];
-    const uint64_t list = static_cast<uint64_t>(grp) * nb + own_b;
-    if (run_c != 0) {
-      run_p = atomicAdd(&L.cursor[list], run_c);
-      const uint32_t c0 = run_p >> kChunkLog, c1 = (run_p + run_c - 1) >> kChunkLog;
-      for (uint32_t cc = (run_p & (kChunkRows - 1)) ? c0 + 1 : c0; cc <= c1; cc++) {
-        const uint32_t local = atomicAdd(&L.pool[grp], 1u);
-        uint32_t id = grp * L.shard_cap + local;
-        if (local >= L.shard_cap || cc >= L.cmax) {
-          l1_flag_error(L);
-          id = 0;
-        } else {
-          __hip_atomic_store(&L.chunk_tab[list * L.cmax + cc], id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        s_chunk[cc - c0][own_b] = id;
-      }
-    }
-    if (counts_tm != nullptr) {
-      counts_tm[tile * nb + own_b] = run_c;
-      pre_tm[tile * nb + own_b] = run_p;
-    }
+    if (run_c != 0) run_p = atomicAdd(&L.cursor[list], run_c);
   }
   __syncthreads();
   // the rows to their bucket-sorted LDS slots; the row map gets the slot
@@ -172,17 +169,31 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
       for (int j = 0; j < 8; j++) pos_out[sbase + seg_row<K, DENSE>(j, lane)] = pv[j];
     }
   }
-  if (owner && run_c != 0) {
-    const uint32_t c0 = run_p >> kChunkLog;
-    if (run_p & (kChunkRows - 1)) {  // the run starts inside a chunk an earlier run took: wait for its id
-      const uint64_t list = static_cast<uint64_t>(grp) * nb + own_b;
-      uint32_t id = 0;
-      if (c0 >= L.cmax) {
-        l1_flag_error(L);
-      } else {
-        uint32_t spins = 0;
-        while ((id = __hip_atomic_load(&L.chunk_tab[list * L.cmax + c0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ==
-               kChunkEmpty) {
+  if (owner) {
+    if (counts_tm != nullptr) {
+      counts_tm[tile * nb + own_b] = run_c;
+      pre_tm[tile * nb + own_b] = run_p;
+    }
+    if (run_c != 0) {
+      const uint32_t c0 = run_p >> kChunkLog, c1 = (run_p + run_c - 1) >> kChunkLog;
+      if (c1 >= L.k_fixed) {
+        // take the extents whose first row this run covers (publishing before any wait) ...
+        for (uint32_t cc = max(c0, L.k_fixed); cc <= c1; cc++) {
+          const uint32_t x = cc - L.k_fixed;
+          if (x % kExtentChunks != 0 || (static_cast<uint64_t>(cc) << kChunkLog) < run_p) continue;
+          const uint32_t e = x / kExtentChunks, local = atomicAdd(&L.pool[grp], 1u);
+          if (e >= L.n_ext || local >= L.shard_ext) {
+            l1_flag_error(L);
+            continue;
+          }
+          const uint32_t first = L.n_lists * L.k_fixed + (grp * L.shard_ext + local) * kExtentChunks;
+          __hip_atomic_store(&L.ext_dir[list * L.n_ext + e], first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      // ... then the ids of the chunks the run covers (fixed, own extents, or an extent an earlier run took)
+      for (uint32_t cc = c0; cc <= c1; cc++) {
+        uint32_t id, spins = 0;
+        while ((id = l1_chunk_id(L, list, cc)) == kChunkEmpty) {
           if (++spins > kChunkSpinLimit) {
             l1_flag_error(L);
             id = 0;
@@ -190,10 +201,10 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
           }
           __builtin_amdgcn_s_sleep(2);
         }
+        s_chunk[cc - c0][own_b] = id;
       }
-      s_chunk[0][own_b] = id;
+      s_qc[own_b] = static_cast<uint64_t>(run_p - s_start[own_b]) | (static_cast<uint64_t>(c0) << 32);
     }
-    s_qc[own_b] = static_cast<uint64_t>(run_p - s_start[own_b]) | (static_cast<uint64_t>(c0) << 32);
   }
   __syncthreads();
   // copy-out over the tile's bucket-sorted rows, every lane busy: a wave's 64 rows span ~2 runs, so each
@@ -259,13 +270,13 @@ __global__ __launch_bounds__(kListsThreads) void bucket_lists_kernel(L1Lists L, 
     const uint32_t jj = min(j, nk - 1);
     uint32_t g = 0;
     while (g + 1 < G && s_k[g + 1] <= jj) g++;
-    chunk_map[static_cast<uint64_t>(first) * kChunksPerTile + j] = L.chunk_tab[(static_cast<uint64_t>(g) * nb + b) * L.cmax + (jj - s_k[g])];
+    chunk_map[static_cast<uint64_t>(first) * kChunksPerTile + j] = l1_chunk_id(L, static_cast<uint64_t>(g) * nb + b, jj - s_k[g]);
   }
   if (err) return;
   for (uint32_t g = 0; g < G; g++) {
     const uint32_t rows = L.cursor[g * nb + b], r = rows & (kChunkRows - 1);
     if (r == 0) continue;  // uniform
-    const uint64_t c0 = static_cast<uint64_t>(L.chunk_tab[(static_cast<uint64_t>(g) * nb + b) * L.cmax + (rows >> kChunkLog)]) * kChunkRows;
+    const uint64_t c0 = static_cast<uint64_t>(l1_chunk_id(L, static_cast<uint64_t>(g) * nb + b, rows >> kChunkLog)) * kChunkRows;
     const uint32_t lo = hash_lo[c0];
     const uint8_t hi = hash_hi[c0];
     for (uint32_t i = r + threadIdx.x; i < kChunkRows; i += kListsThreads) {

@@ -67,7 +67,10 @@ constexpr int kRowsPerThread = static_cast<int>(kTileRows / kTileThreads);
 constexpr int kSegsPerWaveA = kRowsPerThread / 8;      // 512-row segments per wave (bucketed level 2 / build)
 // Level-1 tiles of the bucketed strategy (bucket_scatter / bucket_unpermute): 16 Ki rows, independent of
 // the partition tile (the scatter stages 7 B per row in LDS).
-constexpr uint64_t kL1TileRows = 16384;
+#ifndef RPT_L1_TILE_ROWS
+#define RPT_L1_TILE_ROWS 16384
+#endif
+constexpr uint64_t kL1TileRows = RPT_L1_TILE_ROWS;
 constexpr int kL1SegsPerWave = static_cast<int>(kL1TileRows / kTileThreads / 8);
 // The level-2 hash array is allocated in chunks of 4 Ki rows (bucketed.hpp); a level-2 tile is 4 chunks
 // of one bucket, so a 512-row segment never straddles two chunks.

@@ -297,7 +297,7 @@ struct ProbeWorkspace {
   uint32_t* bucket_tiles;  // [bucket + 1] first level-2 tile of the bucket; [nb] = level-2 tile count
   uint32_t* chunk_map;     // [level-2 tile][4] chunk ids
   uint32_t* lists;         // cursors, pool counters, error flag (L1Lists)
-  uint32_t* chunk_tab;     // L1Lists::chunk_tab
+  uint32_t* ext_dir;       // L1Lists::ext_dir
   uint32_t* hash_lo;       // level-2 array (kKeySplit) in 4 Ki-row chunks: hash bits 0..31
   uint8_t* hash_hi;        // and bits 32..39
   uint16_t* pos1;          // row -> position in its level-1 tile's bucket-sorted order
@@ -350,16 +350,18 @@ int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
 }
 
 // Geometry of the bucketed level 1 for a batch of n rows (bucketed.hpp): 8 list groups (one per XCD
-// share) for large batches, 1 below RPT_L1_GROUPS_MIN_ROWS (8 lists per bucket would pad too much);
-// chunk pool shards and the level-2 tile bound.
+// share) for large batches, 1 below RPT_L1_GROUPS_MIN_ROWS (8 lists per bucket would pad too much); K
+// fixed chunks per list, then overflow extents from per-group pool shards; the level-2 tile bound.
 constexpr uint64_t kL1GroupsMinRows = 1ULL << 27;
 struct L1Geom {
-  uint64_t t1;          // level-1 tiles
-  uint32_t nb, groups;  // buckets, list groups
-  uint64_t cmax;        // chunks per list (bound)
-  uint64_t shard_cap;   // chunks per pool shard (bound)
-  uint64_t pool_chunks; // groups * shard_cap
-  uint64_t t2max;       // level-2 tiles (bound)
+  uint64_t t1;           // level-1 tiles
+  uint32_t nb, groups;   // buckets, list groups
+  uint64_t n_lists;      // groups * nb
+  uint64_t k_fixed;      // chunks with fixed ids per list
+  uint64_t n_ext;        // overflow extents per list (bound)
+  uint64_t shard_ext;    // extents per pool shard (bound)
+  uint64_t pool_chunks;  // chunk ids: n_lists * k_fixed fixed ones, then groups * shard_ext extents
+  uint64_t t2max;        // level-2 tiles (bound)
 };
 L1Geom l1_geom(uint64_t n, int log_num_blocks) {
   static const uint64_t min_rows = [] {
@@ -370,12 +372,22 @@ L1Geom l1_geom(uint64_t n, int log_num_blocks) {
   g.t1 = ceil_div(n, rpt::kL1TileRows);
   g.nb = bucket_count(log_num_blocks);
   g.groups = n >= min_rows ? rpt::kL1Groups : 1u;
-  const uint64_t tiles_per_group = ceil_div(g.t1, g.groups);  // tiles of workgroups b with b % 8 == g
-  const uint64_t chunks_per_tile = rpt::kL1TileRows / rpt::kChunkRows;
-  g.cmax = tiles_per_group * chunks_per_tile + 1;        // a list holds at most its group's rows
-  g.shard_cap = tiles_per_group * chunks_per_tile + g.nb;  // + one part-filled chunk per list
-  g.pool_chunks = g.groups * g.shard_cap;
-  g.t2max = ceil_div(g.pool_chunks, rpt::kChunksPerTile) + g.nb;  // + one part-filled tile per bucket
+  g.n_lists = static_cast<uint64_t>(g.groups) * g.nb;
+  const uint64_t even = ceil_div(ceil_div(n, g.n_lists), rpt::kChunkRows);  // chunks per list of an even split
+#ifndef RPT_L1_FIXED_PCT
+// Fixed chunks per list, in % of an even split's (+ 1). Measured (C5 probe ms, same box): 0 -> 8.70-8.75,
+// 110 / 125 -> 8.82-8.85: fixed ids spare the scatter its extent atomics and waits (3.15 -> 3.06 ms), but
+// the larger workspace (+6 GB at 1e9 rows: the overflow pool stays sized for the worst case) costs the
+// slice probe, partition and unpermute more (slice probe 2.32 -> 2.48 ms).
+#define RPT_L1_FIXED_PCT 0
+#endif
+  g.k_fixed = ceil_div(even * RPT_L1_FIXED_PCT, 100) + 1;
+  const uint64_t group_chunks = ceil_div(g.t1, g.groups) * (rpt::kL1TileRows / rpt::kChunkRows);  // rows of one group
+  const uint64_t cmax = group_chunks + 1;  // chunks of one list
+  g.n_ext = cmax > g.k_fixed ? ceil_div(cmax - g.k_fixed, rpt::kExtentChunks) : 0;
+  g.shard_ext = ceil_div(group_chunks + g.nb, rpt::kExtentChunks) + g.nb;  // + one part-used extent per list
+  g.pool_chunks = g.n_lists * g.k_fixed + g.groups * g.shard_ext * rpt::kExtentChunks;
+  g.t2max = ceil_div(ceil_div(n, rpt::kChunkRows) + g.n_lists, rpt::kChunksPerTile) + g.nb;  // + one part tile per bucket
   return g;
 }
 uint64_t level2_tiles_max(uint64_t n, int log_num_blocks) { return l1_geom(n, log_num_blocks).t2max; }
@@ -418,8 +430,8 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     sz[11] = align256(static_cast<uint64_t>(g.groups) * g.nb * 8);
     sz[12] = align256((g.nb + 1) * 4);
     sz[13] = align256(g.t2max * rpt::kChunksPerTile * 4);
-    sz[14] = align256((static_cast<uint64_t>(g.groups) * g.nb + g.groups + 1) * 4);
-    sz[15] = align256(static_cast<uint64_t>(g.groups) * g.nb * g.cmax * 4);
+    sz[14] = align256((g.n_lists + g.groups + 1) * 4);
+    sz[15] = align256(g.n_lists * g.n_ext * 4);
     sz[16] = align256(g.pool_chunks * rpt::kChunkRows * 4);
     sz[17] = align256(g.t1 * rpt::kL1TileRows * 2);
     sz[18] = align256(g.t2max * T / 8);
@@ -448,7 +460,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     ws->bucket_tiles = static_cast<uint32_t*>(at(12));
     ws->chunk_map = static_cast<uint32_t*>(at(13));
     ws->lists = static_cast<uint32_t*>(at(14));
-    ws->chunk_tab = static_cast<uint32_t*>(at(15));
+    ws->ext_dir = static_cast<uint32_t*>(at(15));
     ws->hash_lo = static_cast<uint32_t*>(at(16));
     ws->pos1 = static_cast<uint16_t*>(at(17));
     ws->bits2 = static_cast<uint64_t*>(at(18));
@@ -466,7 +478,7 @@ struct InsertWorkspace {
   uint32_t* bucket_tiles;
   uint32_t* chunk_map;
   uint32_t* lists;
-  uint32_t* chunk_tab;
+  uint32_t* ext_dir;
   uint32_t* hash_lo;
   uint8_t* hash_hi;
   uint64_t* list_base;
@@ -490,8 +502,8 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
     const L1Geom g = l1_geom(n, log_num_blocks);
     sz[3] = align256((g.nb + 1) * 4);
     sz[4] = align256(g.t2max * rpt::kChunksPerTile * 4);
-    sz[5] = align256((static_cast<uint64_t>(g.groups) * g.nb + g.groups + 1) * 4);
-    sz[6] = align256(static_cast<uint64_t>(g.groups) * g.nb * g.cmax * 4);
+    sz[5] = align256((g.n_lists + g.groups + 1) * 4);
+    sz[6] = align256(g.n_lists * g.n_ext * 4);
     sz[7] = align256(g.pool_chunks * rpt::kChunkRows * 4);
     sz[8] = align256(g.pool_chunks * rpt::kChunkRows);
     sz[9] = align256(static_cast<uint64_t>(g.groups) * g.nb * 8);
@@ -510,7 +522,7 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
     ws->bucket_tiles = static_cast<uint32_t*>(at(3));
     ws->chunk_map = static_cast<uint32_t*>(at(4));
     ws->lists = static_cast<uint32_t*>(at(5));
-    ws->chunk_tab = static_cast<uint32_t*>(at(6));
+    ws->ext_dir = static_cast<uint32_t*>(at(6));
     ws->hash_lo = static_cast<uint32_t*>(at(7));
     ws->hash_hi = static_cast<uint8_t*>(at(8));
     ws->list_base = static_cast<uint64_t*>(at(9));
@@ -711,7 +723,7 @@ int transpose_u32(hipStream_t s, const uint32_t* in, uint64_t rows, uint64_t col
 // the lists are laid out as level-2 tiles (chunk_map, bucket_tiles, list_base) and padded.
 struct BucketLevel1 {
   uint32_t* lists;      // cursors | pool counters | error flag
-  uint32_t* chunk_tab;
+  uint32_t* ext_dir;
   uint32_t* chunk_map;
   uint32_t* bucket_tiles;
   uint64_t* list_base;
@@ -724,12 +736,16 @@ struct BucketLevel1 {
 int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool dense, uint64_t n, int L,
                       const BucketLevel1& w, int64_t* stats) {
   const L1Geom g = l1_geom(n, L);
-  const uint64_t n_lists = static_cast<uint64_t>(g.groups) * g.nb;
+  const uint64_t n_lists = g.n_lists;
+  if (g.pool_chunks >= (1ULL << 32) - rpt::kExtentChunks)
+    return fail(RPT_ERR_INVALID_ARGUMENT, "bucketed batch of %llu rows too large", static_cast<unsigned long long>(n));
   RPT_HIP(hipMemsetAsync(w.lists, 0, (n_lists + g.groups + 1) * 4, s));
-  RPT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.chunk_tab), static_cast<int>(rpt::kChunkEmpty),
-                            n_lists * g.cmax, s));
-  const rpt::L1Lists lists{w.lists, w.lists + n_lists, w.lists + n_lists + g.groups, w.chunk_tab,
-                           static_cast<uint32_t>(g.cmax), static_cast<uint32_t>(g.shard_cap), g.groups};
+  if (g.n_ext)
+    RPT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.ext_dir), static_cast<int>(rpt::kChunkEmpty),
+                              n_lists * g.n_ext, s));
+  const rpt::L1Lists lists{w.lists, w.lists + n_lists, w.lists + n_lists + g.groups, w.ext_dir,
+                           static_cast<uint32_t>(g.k_fixed), static_cast<uint32_t>(g.n_ext),
+                           static_cast<uint32_t>(g.shard_ext), g.groups, static_cast<uint32_t>(n_lists)};
   RPT_DISPATCH_KD(launch_bucket_scatter_t, key_type, dense, static_cast<unsigned>(g.t1), s, a, n, g.nb - 1, lists, w.hash_lo,
                   w.hash_hi, w.pos1, w.counts_tm, w.pre_tm, stats);
   RPT_LAUNCHED("bucket_scatter_kernel");
@@ -1113,7 +1129,7 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   const uint32_t* dev_n_tiles = nullptr;
   uint32_t grid_slices = tile_slices;
   if (buck) {  // (the key min/max comes from level 1's key read)
-    const BucketLevel1 l1{ws.lists, ws.chunk_tab, ws.chunk_map, ws.bucket_tiles, ws.list_base, ws.hash_lo, ws.hash_hi,
+    const BucketLevel1 l1{ws.lists, ws.ext_dir, ws.chunk_map, ws.bucket_tiles, ws.list_base, ws.hash_lo, ws.hash_hi,
                           nullptr, nullptr, nullptr};
     st = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, bf->stats);
     if (st != RPT_OK) return st;
@@ -1233,7 +1249,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     uint64_t* part_bits = ws.bits;
     uint32_t* part_counts = ws.seg_counts;
     if (buck) {
-      const BucketLevel1 l1{ws.lists, ws.chunk_tab, ws.chunk_map, ws.bucket_tiles, ws.list_base, ws.hash_lo, ws.hash_hi,
+      const BucketLevel1 l1{ws.lists, ws.ext_dir, ws.chunk_map, ws.bucket_tiles, ws.list_base, ws.hash_lo, ws.hash_hi,
                             ws.pos1, ws.counts_tm, ws.pre_tm};
       int st1 = run_bucket_level1(s, col->key_type, a, dense, n, L, l1, nullptr);
       if (st1 != RPT_OK) return st1;

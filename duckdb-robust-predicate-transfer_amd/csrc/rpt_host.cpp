@@ -715,9 +715,10 @@ void PTBloomFilter::AllReduceOr(DeviceContext& ctx, void* nccl_comm) {
 
 // ---- CreateBF ------------------------------------------------------------------------------------
 CreateBF::CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices,
-                   uint64_t sink_flush_rows)
+                   uint64_t sink_flush_rows, ResizeRule resize_rule)
     : device_(device),
       estimated_cardinality_(estimated_cardinality),
+      resize_rule_(resize_rule),
       cols_(std::move(bound_column_indices)),
       sink_flush_rows_(std::max<uint64_t>(1, sink_flush_rows)) {
   for (size_t i = 0; i < cols_.size(); i++) {
@@ -794,10 +795,13 @@ void CreateBF::Finalize() {
     DeviceContext ctx(device_);
     for (size_t i = 0; i < filters_.size(); i++) {
       auto& bf = *filters_[i];
-      // physical_create_bf.cpp:383-398: resize iff the allocated filter gives < 8 bits per actual row
-      // (evaluated on this filter's real allocation, rpt_bf_needs_resize_alloc); the rehash reads the
-      // build column from HBM
-      if (bf.NeedsResize(actual_rows)) {
+      // physical_create_bf.cpp:383-398: resize iff the allocated filter gives < 8 bits per actual row,
+      // on this filter's real allocation (default) or by the reference's formula verbatim (ResizeRule);
+      // the rehash reads the build column from HBM
+      const bool resize = resize_rule_ == ResizeRule::kReferenceFormula
+                              ? rpt_bf_needs_resize(bf.SizedForRows(), actual_rows) == 1
+                              : bf.NeedsResize(actual_rows);
+      if (resize) {
         bf.ReinitializeAndRehash(ctx, actual_rows, all_keys_[i]);
         resized_[i] = true;
       }

@@ -216,8 +216,15 @@ class CreateBF {
     size_t chunk_from = 0, chunk_to = 0, current = 0;
   };
 
+  // Finalize's resize predicate (physical_create_bf.cpp:383-398). kOnAllocation (default): the stated
+  // intent "< 8 bits per actual row" on the filter actually allocated (Arrow sizing, 8 bits per estimated
+  // row: rpt_bf_needs_resize_alloc). kReferenceFormula: the reference's formula verbatim, which prices the
+  // allocation as DuckDB's native filter would (NextPow2(max(512, 12 * sized_for)): rpt_bf_needs_resize);
+  // on this filter it keeps e.g. 2048 rows in a filter sized for 1000 (4 bits per key) where the default
+  // resizes. Results differ from the reference's only in which of the two rules decides.
+  enum class ResizeRule { kOnAllocation, kReferenceFormula };
   CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint64_t> bound_column_indices,
-           uint64_t sink_flush_rows = kDefaultSinkFlushRows);
+           uint64_t sink_flush_rows = kDefaultSinkFlushRows, ResizeRule resize_rule = ResizeRule::kOnAllocation);
   std::unique_ptr<LocalState> MakeLocalState() const { return std::make_unique<LocalState>(device_, cols_.size()); }
   void Sink(LocalState& local, const DataChunk& chunk) const;  // physical_create_bf.cpp:201-242
   void Combine(LocalState& local);                             // physical_create_bf.cpp:244-275
@@ -242,6 +249,7 @@ class CreateBF {
 
   int device_;
   uint64_t estimated_cardinality_;
+  ResizeRule resize_rule_;
   std::vector<uint64_t> cols_;
   uint64_t sink_flush_rows_;
   std::vector<std::shared_ptr<PTBloomFilter>> filters_;

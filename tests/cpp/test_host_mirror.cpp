@@ -19,6 +19,8 @@
 #include "rpt_host.hpp"
 
 extern "C" {
+int rpt_oracle_needs_resize(uint64_t sized_for_rows, uint64_t actual_rows);
+int rpt_oracle_needs_resize_alloc(int log_num_blocks, uint64_t actual_rows);
 int rpt_oracle_log_num_blocks(uint64_t n_rows);
 void rpt_oracle_insert_i64(uint64_t* words, int log_nb, const int64_t* keys, const uint32_t* key_sel,
                            const uint64_t* validity, uint64_t n);
@@ -260,6 +262,40 @@ int main() {
       std::sort(rows_in.begin(), rows_in.end());
       EXPECT(empty_threads == 1, "one of 4 source threads finds no range (%zu)", empty_threads);
       EXPECT(rows_out == rows_in, "the source re-emits exactly the sunk rows (%zu vs %zu)", rows_out.size(), rows_in.size());
+    }
+    // the resize predicate (physical_create_bf.cpp:383-398) under both rules, sized for 1000 rows:
+    // 1024 actual rows fill the allocation at 8 bits/row under either; 2048 resize on the allocation
+    // (default) but not by the reference's formula (its 12-bit pricing allocates 16384 bits); 2049 resize
+    // under both. Words == the oracle's filter of the size each rule leaves.
+    for (const uint64_t rows : {1024ull, 2048ull, 2049ull}) {
+      for (const auto rule : {rpt::CreateBF::ResizeRule::kOnAllocation, rpt::CreateBF::ResizeRule::kReferenceFormula}) {
+        rpt::CreateBF c3(dev, /*estimated_cardinality=*/1000, {0}, rpt::CreateBF::kDefaultSinkFlushRows, rule);
+        auto l3 = c3.MakeLocalState();
+        rpt::DataChunk ch = bst.chunks[0];
+        size_t done = 0;
+        for (size_t k = 0; done < rows; k++) {
+          ch = bst.chunks[k];
+          ch.count = std::min<size_t>(ch.count, rows - done);
+          c3.Sink(*l3, ch);
+          done += ch.count;
+        }
+        c3.Combine(*l3);
+        c3.Finalize();
+        const bool ref_rule = rule == rpt::CreateBF::ResizeRule::kReferenceFormula;
+        const bool want = ref_rule ? rows > 2048 : rows > 1024;
+        EXPECT(c3.Resized(0) == want, "rows %llu rule %d: resized %d", (unsigned long long)rows, (int)ref_rule,
+               (int)c3.Resized(0));
+        const int oracle_says = ref_rule ? rpt_oracle_needs_resize(1000, rows)
+                                         : rpt_oracle_needs_resize_alloc(rpt_oracle_log_num_blocks(1000), rows);
+        EXPECT(c3.Resized(0) == (oracle_says > 0),
+               "rows %llu rule %d: oracle predicate", (unsigned long long)rows, (int)ref_rule);
+        const int l = c3.Resized(0) ? rpt_oracle_log_num_blocks(rows) : rpt_oracle_log_num_blocks(1000);
+        std::vector<uint64_t> wr(1ULL << l, 0);
+        std::vector<uint64_t> va = pack(bt.v0, 0, rows);
+        rpt_oracle_insert_i64(wr.data(), l, bt.c0.data(), nullptr, va.data(), rows);
+        EXPECT(c3.GetBloomFilter(0)->LogNumBlocks() == l && c3.GetBloomFilter(0)->ExportWords() == wr,
+               "rows %llu rule %d: filter words", (unsigned long long)rows, (int)ref_rule);
+      }
     }
     // default sink batching (all inserts at Combine), no resize: same filter as the oracle's
     {

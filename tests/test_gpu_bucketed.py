@@ -153,6 +153,59 @@ def test_bucketed_skewed_keys(rpt):
     assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
 
 
+def keys_in_bucket(log_nb, bucket, count, seed):
+    """`count` distinct int64 keys whose hashes fall in level-1 bucket `bucket` (hash bits 38..)."""
+    nb = 1 << (log_nb - 22)
+    cand = keys_of(np.int64, count * nb * 4, seed)
+    h = orc.hash_keys(cand)
+    sel = cand[((h >> np.uint64(38)) & np.uint64(nb - 1)) == bucket][:count]
+    assert sel.size == count
+    return sel
+
+
+@pytest.mark.parametrize("log_nb,n,frac", [(25, 2_000_000, 1.0), (25, 3_000_017, 0.6), (27, 5_000_000, 0.9)])
+def test_bucketed_list_overflow(rpt, log_nb, n, frac):
+    """Rows crowding into one bucket (bucketed.hpp): its list outgrows its fixed chunks and grows by pool
+    extents -- runs of whole 16 Ki-row tiles spanning several chunks, runs starting inside extents other
+    tiles took. Insert (filter words) and probe (sel) vs the oracle."""
+    rng = np.random.default_rng(n)
+    hot = keys_in_bucket(log_nb, 3, 4000, log_nb)
+    keys = np.where(rng.random(n) < frac, hot[rng.integers(0, hot.size, n)], keys_of(np.int64, n, 7))
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.insert(dev(keys), strategy=INS_BUCKETED)
+    w = oracle_filter(log_nb, keys)
+    assert np.array_equal(bf.export_words(), w)
+    assert bf.minmax() == orc.minmax(keys)
+    bf.probe_strategy = BUCKETED
+    probe = np.where(rng.random(n) < frac, hot[rng.integers(0, hot.size, n)], keys_of(np.int64, n, 8))
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
+
+
+@pytest.mark.timeout(300)
+def test_bucketed_grouped_lists_skewed(rpt):
+    """A batch of >= 2^27 rows takes 8 list groups per bucket (one per XCD share); 40 % of its rows in one
+    of 16 buckets, so that bucket's 8 lists overflow while the others stay within their fixed chunks.
+    Insert and probe vs the oracle, every word and sel entry."""
+    log_nb, n = 26, (1 << 27) + 12_345
+    rng = np.random.default_rng(26)
+    hot = keys_in_bucket(log_nb, 11, 3000, 99)
+    keys = orc.synth_build_keys(n, start=10**9)
+    m = rng.random(n) < 0.4
+    keys[m] = hot[rng.integers(0, hot.size, int(m.sum()))]
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.insert(dev(keys), strategy=INS_BUCKETED)
+    w = oracle_filter(log_nb, keys)
+    assert np.array_equal(bf.export_words(), w)
+    bf.probe_strategy = BUCKETED
+    probe = orc.synth_probe_keys(n, n, 10, start=2 * 10**9)
+    probe[m] = keys[m]
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32)
+    ref = orc.probe_keys(w, log_nb, probe)
+    assert ref.size >= int(m.sum())
+    assert np.array_equal(sel, ref)
+
+
 def test_c5_geometry_8gib_filter_vs_oracle(rpt):
     """BASELINE C5's single-rank geometry: a filter sized for 8e9 rows = 2^30 blocks
     (8 GiB), 256 level-1 buckets of 256 slices. Bucketed insert of 1.2e7 keys and bucketed probes of
