@@ -43,6 +43,34 @@
 #include "kernels/compaction.hpp"
 #include "kernels/misc.hpp"
 
+// Host-side tuning macros (the kernels' own are in kernels/*.hpp).
+#ifndef RPT_FUSED_SEL
+#define RPT_FUSED_SEL 1  // rpt_bf_probe, PARTITIONED: the unpermute writes the selection vector itself
+#endif
+#ifndef RPT_L1_FIXED_PCT
+// Fixed chunks per list, in % of an even split's (+ 1). Measured (C5 probe ms, same box): 0 -> 8.70-8.75,
+// 110 / 125 -> 8.82-8.85: fixed ids spare the scatter its extent atomics and waits (3.15 -> 3.06 ms), but
+// the larger workspace (+6 GB at 1e9 rows: the overflow pool stays sized for the worst case) costs the
+// slice probe, partition and unpermute more (slice probe 2.32 -> 2.48 ms).
+#define RPT_L1_FIXED_PCT 0
+#endif
+
+// The product build runs the tuning macros at the defaults the GPU suite tests. Other values exist for
+// A/B timing only (tools/build_variants.sh builds them under other names, without RPT_PRODUCT_BUILD);
+// several were never run through the parity suite (tuning macros).
+#if defined(RPT_PRODUCT_BUILD)
+static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG == 8 && RPT_L1_TILE_ROWS == 16384 &&
+                  RPT_L1_FIXED_PCT == 0 && RPT_BUCKET_UNPERMUTE_THREADS == 256 && RPT_SLICE_UNROLL == 4 &&
+                  RPT_PARTITION_MIN_WAVES == 8 && RPT_PROBE_PREFETCH == 2 && RPT_SEL_BALLOT_MIN == 192 &&
+                  RPT_COMPACT_BALLOT_MIN == 384,
+              "product build: tuning macros must keep their tested defaults (use tools/build_variants.sh)");
+static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
+                  RPT_NT_REC_LOADS == 0 && RPT_NT_SLICE_LOADS == 1 && RPT_PARK_LANE_MAJOR == 1 && RPT_SLICE_XCD_MAP == 1 &&
+                  RPT_PARTITION_SMALL_P == 1 && RPT_VALU_INTERLEAVE == 1 && RPT_SEL_BALLOT_EXPAND == 1 &&
+                  RPT_DPP_MINMAX == 1 && RPT_DPP_SCAN == 1,
+              "product build: tuning switches must keep their tested defaults (use tools/build_variants.sh)");
+#endif
+
 // =================================================================================================
 // Host side
 // =================================================================================================
@@ -374,13 +402,6 @@ L1Geom l1_geom(uint64_t n, int log_num_blocks) {
   g.groups = n >= min_rows ? rpt::kL1Groups : 1u;
   g.n_lists = static_cast<uint64_t>(g.groups) * g.nb;
   const uint64_t even = ceil_div(ceil_div(n, g.n_lists), rpt::kChunkRows);  // chunks per list of an even split
-#ifndef RPT_L1_FIXED_PCT
-// Fixed chunks per list, in % of an even split's (+ 1). Measured (C5 probe ms, same box): 0 -> 8.70-8.75,
-// 110 / 125 -> 8.82-8.85: fixed ids spare the scatter its extent atomics and waits (3.15 -> 3.06 ms), but
-// the larger workspace (+6 GB at 1e9 rows: the overflow pool stays sized for the worst case) costs the
-// slice probe, partition and unpermute more (slice probe 2.32 -> 2.48 ms).
-#define RPT_L1_FIXED_PCT 0
-#endif
   g.k_fixed = ceil_div(even * RPT_L1_FIXED_PCT, 100) + 1;
   const uint64_t group_chunks = ceil_div(g.t1, g.groups) * (rpt::kL1TileRows / rpt::kChunkRows);  // rows of one group
   const uint64_t cmax = group_chunks + 1;  // chunks of one list
@@ -1195,9 +1216,6 @@ int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, ui
   return RPT_OK;
 }
 
-#ifndef RPT_FUSED_SEL
-#define RPT_FUSED_SEL 1  // rpt_bf_probe, PARTITIONED: the unpermute writes the selection vector itself
-#endif
 
 // Phase 1 of rpt_bf_probe. With out_sel (rpt_bf_probe only) the plain PARTITIONED pipeline ends in the
 // fused selection-vector tail instead of the result bits, and *done is set: phase 2 is skipped.

@@ -32,3 +32,18 @@ def test_product_makefile_defines_product_build():
     mk = open(os.path.join(PKG, "Makefile")).read()
     assert "PRODUCT := -DRPT_PRODUCT_BUILD=1" in mk and "$(HIPFLAGS) $(PRODUCT)" in mk
     assert "RPT_TESTING_HOOKS" not in mk.replace("# ", "")
+
+
+def syntax_check(*defines):
+    cmd = [HIPCC, "-fsyntax-only", "--cuda-host-only", "-std=c++17", f"-I{REPO}/include", f"-I{PKG}/csrc", SRC]
+    cmd += [f"-D{d}" for d in defines]
+    return subprocess.run(cmd, capture_output=True, text=True)
+
+
+@pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not installed")
+@pytest.mark.parametrize("macro", ["RPT_SLICE_UNROLL=2", "RPT_L1_TILE_ROWS=8192", "RPT_NT_REC_LOADS=1"])
+def test_product_build_pins_tuning_macros(macro):
+    """Tuning macros other than the defaults the GPU suite runs are for A/B variants only."""
+    r = syntax_check("RPT_PRODUCT_BUILD=1", macro)
+    assert r.returncode != 0 and "must keep their tested defaults" in r.stderr
+    assert syntax_check(macro).returncode == 0
