@@ -95,6 +95,7 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
   __shared__ uint32_t s_cnt[kMaxBuckets], s_start[kMaxBuckets];
   __shared__ uint64_t s_qc[kMaxBuckets];  // (list position of sorted slot 0) | first chunk index << 32
   __shared__ uint32_t s_chunk[kMaxRunChunks][kMaxBuckets];  // ids of the chunks the run covers
+  __shared__ int64_t s_mm[kTileThreads / 64][2];             // MM: each wave's key min / max
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t nb = bucket_mask + 1;
   const uint64_t tile = l1_tile_of_block(blockIdx.x, gridDim.x);
@@ -104,25 +105,34 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
   const uint32_t own_b = threadIdx.x - (kTileThreads - kMaxBuckets);
   const bool owner = threadIdx.x >= kTileThreads - kMaxBuckets && own_b < nb;
   for (uint32_t i = threadIdx.x; i < nb; i += kTileThreads) s_cnt[i] = 0;
+  // MM: the filter's min / max as of now, loaded early and compared at the end (they only ever improve, so
+  // a workgroup whose keys cannot improve the early values cannot improve the current ones either)
+  [[maybe_unused]] int64_t pre_mn = kMinInit, pre_mx = kMaxInit;
+  if constexpr (MM && KeyTraits<K>::kValues) {
+    if (threadIdx.x == 0) {
+      pre_mn = __hip_atomic_load(stats, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pre_mx = __hip_atomic_load(stats + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   __syncthreads();
   uint64_t hh[kL1SegsPerWave][8];
   uint32_t rk[kL1SegsPerWave][8];  // rank within the bucket, ~0 for rows past n
-  int64_t wmn = kMinInit, wmx = kMaxInit;
+  int64_t mm[2] = {kMinInit, kMaxInit};  // MM: this lane's key min / max over the tile
 #pragma unroll
   for (int sg = 0; sg < kL1SegsPerWave; sg++) {
     const uint64_t sbase = tile_base + wave * (kL1SegsPerWave * kSegRows) + sg * kSegRows;
     bool oo[8];
-    int64_t mm[2] = {kMinInit, kMaxInit};
     load_hashes<K, DENSE, MM, false, true>(a, sbase, n, lane, hh[sg], oo, mm);
-    if constexpr (MM && KeyTraits<K>::kValues) {
-      wave_minmax(mm[0], mm[1]);
-      wmn = min(wmn, mm[0]);
-      wmx = max(wmx, mm[1]);
-    }
 #pragma unroll
     for (int j = 0; j < 8; j++) rk[sg][j] = oo[j] ? atomicAdd(&s_cnt[bucket_of(hh[sg][j], bucket_mask)], 1u) : ~0u;
   }
-  if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
+  if constexpr (MM && KeyTraits<K>::kValues) {
+    wave_minmax(mm[0], mm[1]);
+    if (lane == 0) {
+      s_mm[wave][0] = mm[0];
+      s_mm[wave][1] = mm[1];
+    }
+  }
   __syncthreads();
   uint32_t run_p = 0, run_c = 0;  // owner: the run's start in its list and its length
   const uint64_t list = static_cast<uint64_t>(grp) * nb + own_b;
@@ -221,6 +231,17 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
 #endif
     if (!(RPT_EXP_SCATTER_SKIP & 2)) hash_lo[d] = s_lo[i];
     if (!(RPT_EXP_SCATTER_SKIP & 1)) hash_hi[d] = s_hi[i];
+  }
+  if constexpr (MM && KeyTraits<K>::kValues) {
+    if (threadIdx.x == 0) {  // one publish per workgroup; no-return atomics, nothing waits on them
+      int64_t mn = kMinInit, mx = kMaxInit;
+      for (int w = 0; w < kTileThreads / 64; w++) {
+        mn = min(mn, s_mm[w][0]);
+        mx = max(mx, s_mm[w][1]);
+      }
+      if (mn < pre_mn) (void)__hip_atomic_fetch_min(stats, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (mx > pre_mx) (void)__hip_atomic_fetch_max(stats + 1, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 

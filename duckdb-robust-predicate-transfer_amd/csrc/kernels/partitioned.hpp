@@ -130,6 +130,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
   uint32_t* s_cur = s_cnt + n_slices;        // run start (padded if PAD), then scatter cursor (start + count)
   uint32_t* s_delta = s_cur + n_slices;      // !PAD: padded start - unpadded start
   uint16_t* s_gslice = reinterpret_cast<uint16_t*>(s_delta + n_slices);  // slice of each kRunPad group
+  __shared__ int64_t s_mm[kTileThreads / 64][2];  // MM: each wave's key min / max
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   {  // one tile per workgroup (no persistent loop: keeps per-lane invariants out of registers)
     const uint64_t tile = blockIdx.x;
@@ -173,7 +174,12 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
         }
       }
     }
-    if constexpr (MM && KeyTraits<K>::kValues) publish_minmax(wmn, wmx, stats);
+    if constexpr (MM && KeyTraits<K>::kValues) {  // published once per workgroup at the end
+      if (lane == 0) {
+        s_mm[wave][0] = wmn;
+        s_mm[wave][1] = wmx;
+      }
+    }
     [[maybe_unused]] uint32_t lofs[SP > 0 ? SP : 1], wtot[SP > 0 ? SP : 1];
     if constexpr (SP > 0) {  // one atomic per wave and slice
 #pragma unroll
@@ -312,6 +318,19 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
         runs_tm[tile * n_slices + i] = ((s_cur[i] - s_cnt[i] + s_delta[i]) << 16) | s_cnt[i];  // padded start | true count
     }
     __syncthreads();
+  }
+  if constexpr (MM && KeyTraits<K>::kValues) {
+    // one no-return atomic pair per workgroup (a per-wave publish with its load round trip stalled the
+    // wave before pass 1's barrier); a few thousand per build, so no pre-check
+    if (threadIdx.x == 0) {
+      int64_t mn = kMinInit, mx = kMaxInit;
+      for (int w = 0; w < kTileThreads / 64; w++) {
+        mn = min(mn, s_mm[w][0]);
+        mx = max(mx, s_mm[w][1]);
+      }
+      if (mn != kMinInit) (void)__hip_atomic_fetch_min(stats, mn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (mx != kMaxInit) (void)__hip_atomic_fetch_max(stats + 1, mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
