@@ -89,10 +89,8 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
                                                                       uint32_t* __restrict__ counts_tm,
                                                                       uint32_t* __restrict__ pre_tm,
                                                                       int64_t* __restrict__ stats) {
-  extern __shared__ uint32_t s_lo[];  // kL1TileRows hash words (bits 0..31), bucket-sorted, then their
-  uint16_t* s_hi = reinterpret_cast<uint16_t*>(s_lo + kL1TileRows);  // bits 32..47 (hash_hi = the low byte;
-                                                                     // the bucket, bits 38.., is re-derived)
-  static_assert(kLogNumMasks + 6 + kSliceLog + kBucketSliceLog + 9 <= 48, "bits 32..47 hold the bucket id");
+  extern __shared__ uint64_t s_h[];  // kL1TileRows hashes, bucket-sorted (one 8-B LDS write per row; the
+                                     // bucket, bits 38.., is re-derived on the way out)
   __shared__ uint32_t s_cnt[kMaxBuckets], s_start[kMaxBuckets];
   __shared__ uint64_t s_qc[kMaxBuckets];  // (list position of sorted slot 0) | first chunk index << 32
   __shared__ uint32_t s_chunk[kMaxRunChunks][kMaxBuckets];  // ids of the chunks the run covers
@@ -169,8 +167,7 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
       if (rk[sg][j] != ~0u) {
         const uint32_t b = bucket_of(hh[sg][j], bucket_mask);
         p = s_start[b] + rk[sg][j];
-        s_lo[p] = static_cast<uint32_t>(hh[sg][j]);
-        s_hi[p] = static_cast<uint16_t>(hh[sg][j] >> 32);
+        s_h[p] = hh[sg][j];
       }
       pv[j] = static_cast<uint16_t>(p);
     }
@@ -220,9 +217,9 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
   // copy-out over the tile's bucket-sorted rows, every lane busy: a wave's 64 rows span ~2 runs, so each
   // store instruction writes whole pieces of runs
   const uint32_t used = s_start[nb - 1] + s_cnt[nb - 1];
-  constexpr int kBucketShift = kLogNumMasks + 6 + kSliceLog + kBucketSliceLog - 32;
   for (uint32_t i = threadIdx.x; i < used; i += kTileThreads) {
-    const uint32_t hi = s_hi[i], b = (hi >> kBucketShift) & bucket_mask;
+    const uint64_t h = s_h[i];
+    const uint32_t b = bucket_of(h, bucket_mask);
     const uint64_t qc = s_qc[b];
     const uint32_t q = static_cast<uint32_t>(qc) + i;  // the row's position in its list
     const uint32_t k = (q >> kChunkLog) - static_cast<uint32_t>(qc >> 32);
@@ -230,8 +227,8 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
 #ifndef RPT_EXP_SCATTER_SKIP
 #define RPT_EXP_SCATTER_SKIP 0  // measurement only: 1 = no high-byte stores, 2 = no low-word stores, 3 = neither
 #endif
-    if (!(RPT_EXP_SCATTER_SKIP & 2)) hash_lo[d] = s_lo[i];
-    if (!(RPT_EXP_SCATTER_SKIP & 1)) hash_hi[d] = static_cast<uint8_t>(hi);
+    if (!(RPT_EXP_SCATTER_SKIP & 2)) hash_lo[d] = static_cast<uint32_t>(h);
+    if (!(RPT_EXP_SCATTER_SKIP & 1)) hash_hi[d] = static_cast<uint8_t>(h >> 32);
   }
   if constexpr (MM && KeyTraits<K>::kValues) {
     if (threadIdx.x == 0) {  // one publish per workgroup; no-return atomics, nothing waits on them

@@ -692,7 +692,7 @@ template <int K, bool D>
 void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a, uint64_t n, uint32_t bucket_mask,
                              const rpt::L1Lists& lists, uint32_t* hash_lo, uint8_t* hash_hi, uint16_t* pos1,
                              uint32_t* counts_tm, uint32_t* pre_tm, int64_t* stats) {
-  const size_t lds = rpt::kL1TileRows * 6;  // hash words, hash bits 32..47
+  const size_t lds = rpt::kL1TileRows * 8;  // the tile's hashes
   if (rpt::KeyTraits<K>::kValues && stats != nullptr) {
     static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into (160 KiB minus the static part)
     std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::bucket_scatter_kernel<K, D, true>)); });
