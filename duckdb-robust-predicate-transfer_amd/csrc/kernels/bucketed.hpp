@@ -406,10 +406,7 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
     if (seg >= n_segs) break;
     uint32_t byte = 0;
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-      byte |= ((s_bits[p >> 5] >> (p & 31)) & 1u) << e;
-    }
+    for (int c = 0; c < 4; c++) byte |= pass_bits2(s_bits, pv[sg][c]) << (2 * c);
     const uint64_t row0 = seg * kSegRows + lane * 8;
     if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
     out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);

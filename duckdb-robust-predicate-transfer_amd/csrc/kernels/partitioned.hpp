@@ -679,6 +679,17 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
   }
 }
 
+// The pass bits of the two rows whose u16 record positions share the 32-bit row-map word w (bit 0: the
+// low half's row). The unpermute kernels run close to VALU-bound (C2 unpermute_sel: 0.81 VALU instructions
+// per CU cycle), so: the bits are read as 32-bit LDS words from a STATIC array (its base folds into the
+// instruction's offset; a dynamic array's base is a link-time symbol the compiler adds per lookup), and
+// v_bfe_u32 takes the bit offset from the low 5 bits of its operand, so the low position needs no mask.
+template <int TM>
+constexpr uint32_t kPassWordsMax = static_cast<uint32_t>(tile_cap_for(kMaxSliceCount, TM) / 32);
+__device__ __forceinline__ uint32_t pass_bits2(const uint32_t* s_pass32, uint32_t w) {
+  const uint32_t hi = w >> 16;
+  return __builtin_amdgcn_ubfe(s_pass32[(w & 0xFFFFu) >> 5], w, 1) | (__builtin_amdgcn_ubfe(s_pass32[hi >> 5], hi, 1) << 1);
+}
 // ---- partitioned probe, C: restore row order -> result bits + per-segment counts (P1's format) -----
 // One 256-thread workgroup per tile: the tile's pass bits (tile_cap / 8 bytes) are staged in LDS while
 // each wave's row positions are already in flight; a lane owns 8 consecutive rows of a segment (one
@@ -692,7 +703,7 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint
                                                                      uint32_t* __restrict__ seg_counts,
                                                                      const uint32_t* __restrict__ dev_n_tiles) {
   if (dev_n_tiles != nullptr && blockIdx.x >= *dev_n_tiles) return;  // bucketed: grid is an upper bound
-  extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
+  __shared__ uint32_t s_pass[kPassWordsMax<TM>];  // tile_cap / 8 bytes of pass bits (record order)
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
   constexpr uint32_t kSegsPerWave = (kTileRows * TM / kSegRows) / (kUnpermuteThreads / 64);
@@ -716,10 +727,7 @@ __global__ __launch_bounds__(kUnpermuteThreads) void unpermute_kernel(const uint
     if (seg >= n_segs) break;
     uint32_t byte = 0;
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-      byte |= ((static_cast<uint32_t>(s_pass[p >> 3]) >> (p & 7)) & 1u) << e;
-    }
+    for (int c = 0; c < 4; c++) byte |= pass_bits2(s_pass, pv[sg][c]) << (2 * c);
     const uint64_t row0 = seg * kSegRows + lane * 8;  // rows >= n (last segment) carry don't-care positions
     if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
     out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);
@@ -802,7 +810,7 @@ __global__ __launch_bounds__(kUnpermuteSelThreads<TM>) void unpermute_sel_kernel
                                                                          const uint32_t* __restrict__ block_offs,
                                                                          const uint32_t* __restrict__ row_sel,
                                                                          uint32_t* __restrict__ out_sel) {
-  extern __shared__ uint8_t s_pass[];  // tile_cap / 8 bytes of pass bits (record order)
+  __shared__ uint32_t s_pass[kPassWordsMax<TM>];  // tile_cap / 8 bytes of pass bits (record order)
   constexpr int kThreads = kUnpermuteSelThreads<TM>;
   __shared__ uint32_t s_wtot[kThreads / 64];
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -827,10 +835,7 @@ __global__ __launch_bounds__(kUnpermuteSelThreads<TM>) void unpermute_sel_kernel
   for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
     uint32_t byte = 0;
 #pragma unroll
-    for (int e = 0; e < 8; e++) {
-      const uint32_t p = (pv[sg][e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
-      byte |= ((static_cast<uint32_t>(s_pass[p >> 3]) >> (p & 7)) & 1u) << e;
-    }
+    for (int c = 0; c < 4; c++) byte |= pass_bits2(s_pass, pv[sg][c]) << (2 * c);
     const uint64_t row0 = (seg0 + sg) * kSegRows + lane * 8;  // rows >= n carry don't-care positions
     if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
     bytes[sg] = byte;

@@ -1330,10 +1330,10 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
       ProfScope prof7c_(tm == 2 ? "unpermute_sel_kernel<2>" : "unpermute_sel_kernel<1>", s);
       if (tm == 2)
         hipLaunchKernelGGL(rpt::unpermute_sel_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteSelThreads<2>),
-                           cap / 8, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
+                           0, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
       else
         hipLaunchKernelGGL(rpt::unpermute_sel_kernel<1>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteSelThreads<1>),
-                           cap / 8, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
+                           0, s, ws.pos, ws.passb, n, cap, tile_counts, block_offs, row_sel, out_sel);
       prof7c_.end();
       RPT_LAUNCHED("unpermute_sel_kernel");
       *done = true;
@@ -1341,10 +1341,10 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     }
     ProfScope prof7_(tm == 2 ? "unpermute_kernel<2>" : "unpermute_kernel<1>", s);
     if (tm == 2)
-      hipLaunchKernelGGL(rpt::unpermute_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8,
+      hipLaunchKernelGGL(rpt::unpermute_kernel<2>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), 0,
                          s, ws.pos, ws.passb, n_part, cap, part_bits, part_counts, dev_n_tiles);
     else
-      hipLaunchKernelGGL(rpt::unpermute_kernel<1>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), cap / 8,
+      hipLaunchKernelGGL(rpt::unpermute_kernel<1>, dim3(static_cast<unsigned>(n_tiles)), dim3(rpt::kUnpermuteThreads), 0,
                          s, ws.pos, ws.passb, n_part, cap, part_bits, part_counts, dev_n_tiles);
     prof7_.end();
     RPT_LAUNCHED("unpermute_kernel");
