@@ -505,8 +505,13 @@ struct InsertWorkspace {
   uint64_t* list_base;
 };
 
-// rpt_bf_insert_ws runs a bucketed insert of more rows in batches of this many
+// rpt_bf_insert_ws runs a bucketed insert of more rows in batches of this many (level-1 list positions are
+// 32-bit); the test build batches from 2^20 rows so that the batching runs at test sizes
+#ifdef RPT_TESTING_HOOKS
+constexpr uint64_t kBucketedInsertBatch = 1ULL << 20;
+#else
 constexpr uint64_t kBucketedInsertBatch = 1ULL << 31;
+#endif
 
 size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base, InsertWorkspace* ws) {
   const bool buck = strategy == RPT_INSERT_BUCKETED;
@@ -1816,6 +1821,7 @@ int rpt_testing_set_rccl_api(const rpt_rccl_api_table* table) {
   g_rccl = std::move(a);  // null: rccl_api() returns to librccl
   return RPT_OK;
 }
+uint64_t rpt_testing_bucketed_insert_batch(void) { return kBucketedInsertBatch; }
 #endif  // RPT_TESTING_HOOKS
 
 int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out) {

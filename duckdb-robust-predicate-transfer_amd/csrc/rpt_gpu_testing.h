@@ -46,6 +46,9 @@ typedef struct rpt_rccl_api_table {
 /* Test build only: route the library's RCCL calls through `table` (copied) instead of librccl; NULL
  * restores librccl. Communicators made through one table must be used and destroyed through it. */
 int rpt_testing_set_rccl_api(const rpt_rccl_api_table* table);
+/* Test build only: the row count above which rpt_bf_insert_ws runs a bucketed insert in batches (2^31 in
+ * the product, 2^20 here, so the batching runs at test sizes). */
+uint64_t rpt_testing_bucketed_insert_batch(void);
 #endif
 
 #ifdef __cplusplus

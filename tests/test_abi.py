@@ -121,6 +121,7 @@ def test_testing_hook_absent_from_product():
     # the RCCL-table seam (csrc/rpt_gpu_testing.h) exists only in the test build (tests/loopback)
     lib = _lib.load()
     assert not hasattr(lib, "rpt_testing_set_rccl_api")
+    assert not hasattr(lib, "rpt_testing_bucketed_insert_batch")
 
 
 @pytest.mark.parametrize("world,L", [(1, 30), (2, 3), (2, 20), (3, 25), (8, 24), (8, 30), (8, 31)])
