@@ -58,7 +58,7 @@ uint64_t mask_bits(const uint64_t* validity, uint64_t r, uint32_t n) {
   return n >= 64 ? b : b & ((1ULL << n) - 1);
 }
 
-// Flatten one column of `chunk` (FLAT / CONSTANT / DICTIONARY) into `keys` (element size of the
+// Flatten one column of `chunk` (FLAT / CONSTANT / DICTIONARY / SEQUENCE) into `keys` (element size of the
 // column) and clear the bits of its NULL rows at row offset `row0` of `valid_words` (preset to
 // all-valid: a chunk without NULLs touches no validity word), 64 rows per step. Returns true if any
 // row was NULL.
@@ -98,6 +98,19 @@ bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* va
         }
         any_null |= nulls != 0;
         clear_bits(valid_words, row0 + r, nulls, n);
+      }
+      break;
+    }
+    case VectorType::SEQUENCE: {  // start + r * increment in two's complement (wraps as DuckDB's)
+      uint64_t x = static_cast<uint64_t>(v.seq_start);
+      const uint64_t inc = static_cast<uint64_t>(v.seq_increment);
+      if (es == 8) {
+        for (uint64_t r = 0; r < count; r++, x += inc) std::memcpy(keys + r * 8, &x, 8);
+      } else {
+        for (uint64_t r = 0; r < count; r++, x += inc) {
+          const uint32_t y = static_cast<uint32_t>(x);
+          std::memcpy(keys + r * 4, &y, 4);
+        }
       }
       break;
     }
@@ -739,7 +752,7 @@ void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
   m.data.resize(chunk.data.size());
   for (size_t c = 0; c < chunk.data.size(); c++) {
     const Vector& v = chunk.data[c];
-    if (v.data == nullptr) continue;  // a column this mirror does not carry
+    if (v.data == nullptr && v.type != VectorType::SEQUENCE) continue;  // a column this mirror does not carry
     const size_t es = key_size(v.key_type);
     std::vector<uint64_t> keys((chunk.count * es + 7) / 8 + 1, 0);
     std::vector<uint64_t> valid((chunk.count + 63) / 64 + 1, ~0ULL);  // all valid; NULL rows cleared
@@ -875,7 +888,18 @@ uint64_t UseBF::Execute(DeviceContext& ctx, const DataChunk& input, SelectionVec
     const Vector& v = input.data.at(cols_[i]);
     Vector sv = v;
     std::vector<uint32_t> composed;
-    if (v.type == VectorType::FLAT) {
+    std::vector<uint64_t> seq_vals;  // SEQUENCE: the selected rows' values (as FLAT)
+    if (v.type == VectorType::SEQUENCE) {
+      const size_t es = key_size(v.key_type);
+      seq_vals.resize((out.size() * es + 7) / 8 + 1);
+      uint8_t* dst = reinterpret_cast<uint8_t*>(seq_vals.data());
+      for (size_t r = 0; r < out.size(); r++) {
+        const uint64_t x = static_cast<uint64_t>(v.seq_start) + static_cast<uint64_t>(v.seq_increment) * out[r];
+        std::memcpy(dst + r * es, &x, es);  // little-endian: the low 4 bytes are the int32 value
+      }
+      sv.type = VectorType::FLAT;
+      sv.data = seq_vals.data();
+    } else if (v.type == VectorType::FLAT) {
       sv.type = VectorType::DICTIONARY;
       sv.sel = out.data();
       sv.dict_size = n;

@@ -35,14 +35,17 @@ class GpuError : public std::runtime_error {
   int status_;
 };
 
-// DuckDB VectorType subset the hot path sees (HashColumns flattens CONSTANT, bloom_filter.cpp:19-21).
-enum class VectorType { FLAT, CONSTANT, DICTIONARY };
+// DuckDB VectorType subset the hot path sees (HashColumns flattens CONSTANT, bloom_filter.cpp:19-21;
+// VectorOperations::Hash reads the others through their unified format).
+enum class VectorType { FLAT, CONSTANT, DICTIONARY, SEQUENCE };
 enum class KeyType { I32 = RPT_KEY_I32, I64 = RPT_KEY_I64 };
 
 // One key column of a DataChunk.
 //   FLAT:       data[row], validity indexed by row
 //   CONSTANT:   data[0] for every row, validity bit 0 for every row
 //   DICTIONARY: data[sel[row]] (dictionary of dict_size entries), validity indexed by sel[row]
+//   SEQUENCE:   seq_start + row * seq_increment (DuckDB SEQUENCE_VECTOR, e.g. range() keys), never NULL;
+//               no data pointer (INTEGER sequences wrap to int32 as DuckDB's do)
 struct Vector {
   VectorType type = VectorType::FLAT;
   KeyType key_type = KeyType::I64;
@@ -50,6 +53,8 @@ struct Vector {
   const uint32_t* sel = nullptr;       // DICTIONARY only
   uint64_t dict_size = 0;              // DICTIONARY only
   const uint64_t* validity = nullptr;  // DuckDB ValidityMask words; nullptr = all valid
+  int64_t seq_start = 0;               // SEQUENCE only
+  int64_t seq_increment = 1;           // SEQUENCE only
 };
 
 struct DataChunk {

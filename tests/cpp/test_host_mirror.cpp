@@ -297,6 +297,75 @@ int main() {
                "rows %llu rule %d: filter words", (unsigned long long)rows, (int)ref_rule);
       }
     }
+    // SEQUENCE vectors (DuckDB SEQUENCE_VECTOR: start + row * increment, e.g. range() keys): build two
+    // filters from sequence chunks (int64, and int32 wrapping past INT32_MAX as DuckDB's INTEGER sequence),
+    // then a USE_BF chain whose second filter sees the sequence sliced by the first's survivors
+    {
+      const uint64_t rows = 3 * 2048 + 77;
+      std::vector<int64_t> s64(rows);
+      std::vector<int32_t> s32(rows);
+      for (uint64_t r = 0; r < rows; r++) {
+        s64[r] = -500000 + 3 * static_cast<int64_t>(r);
+        s32[r] = static_cast<int32_t>(static_cast<uint32_t>(INT32_MAX - 5000) + 7u * static_cast<uint32_t>(r));
+      }
+      rpt::CreateBF cs(dev, /*estimated_cardinality=*/rows, {0, 1});
+      auto ls = cs.MakeLocalState();
+      for (uint64_t lo = 0; lo < rows; lo += 2048) {
+        rpt::DataChunk ch;
+        ch.count = std::min<uint64_t>(2048, rows - lo);
+        ch.data.resize(2);
+        ch.data[0].type = rpt::VectorType::SEQUENCE;
+        ch.data[0].key_type = rpt::KeyType::I64;
+        ch.data[0].seq_start = s64[lo];
+        ch.data[0].seq_increment = 3;
+        ch.data[1].type = rpt::VectorType::SEQUENCE;
+        ch.data[1].key_type = rpt::KeyType::I32;
+        ch.data[1].seq_start = s32[lo];
+        ch.data[1].seq_increment = 7;
+        cs.Sink(*ls, ch);
+      }
+      cs.Combine(*ls);
+      cs.Finalize();
+      const int ls_nb = rpt_oracle_log_num_blocks(rows);
+      std::vector<uint64_t> q0(1ULL << ls_nb, 0), q1(1ULL << ls_nb, 0);
+      rpt_oracle_insert_i64(q0.data(), ls_nb, s64.data(), nullptr, nullptr, rows);
+      rpt_oracle_insert_i32(q1.data(), ls_nb, s32.data(), nullptr, nullptr, rows);
+      EXPECT(cs.GetBloomFilter(0)->ExportWords() == q0, "int64 sequence filter differs from the oracle");
+      EXPECT(cs.GetBloomFilter(1)->ExportWords() == q1, "int32 sequence filter differs from the oracle");
+      // probe: a sequence over a wider range (half the rows hit), filter 0 then filter 1 on the survivors
+      const uint64_t np_ = 2000;
+      std::vector<int64_t> p64(np_);
+      std::vector<int32_t> p32(np_);
+      for (uint64_t r = 0; r < np_; r++) {
+        p64[r] = -500000 + 3 * 5 * static_cast<int64_t>(r);
+        p32[r] = static_cast<int32_t>(static_cast<uint32_t>(INT32_MAX - 5000) + 7u * 2u * static_cast<uint32_t>(r));
+      }
+      rpt::DataChunk pc;
+      pc.count = np_;
+      pc.data.resize(2);
+      pc.data[0].type = rpt::VectorType::SEQUENCE;
+      pc.data[0].key_type = rpt::KeyType::I64;
+      pc.data[0].seq_start = p64[0];
+      pc.data[0].seq_increment = 15;
+      pc.data[1].type = rpt::VectorType::SEQUENCE;
+      pc.data[1].key_type = rpt::KeyType::I32;
+      pc.data[1].seq_start = p32[0];
+      pc.data[1].seq_increment = 14;
+      std::vector<uint32_t> o0(np_), o1(np_);
+      const uint64_t c0 = rpt_oracle_probe_i64(q0.data(), ls_nb, p64.data(), nullptr, nullptr, np_, o0.data());
+      std::vector<int32_t> p32s(c0);
+      for (uint64_t r = 0; r < c0; r++) p32s[r] = p32[o0[r]];
+      const uint64_t c1 = rpt_oracle_probe_i32(q1.data(), ls_nb, p32s.data(), nullptr, nullptr, c0, o1.data());
+      std::vector<uint32_t> want(c1);
+      for (uint64_t r = 0; r < c1; r++) want[r] = o0[o1[r]];
+      rpt::DeviceContext sctx(dev);
+      rpt::UseBF su({cs.GetBloomFilter(0), cs.GetBloomFilter(1)}, {0, 1});
+      rpt::SelectionVector got;
+      const uint64_t gc = su.Execute(sctx, pc, got);
+      EXPECT(gc == c1 && got == want, "sequence USE_BF chain: %llu survivors vs oracle %llu", (unsigned long long)gc,
+             (unsigned long long)c1);
+      EXPECT(c1 > 0 && c1 < np_, "the sequence probe must keep some rows and drop others (%llu)", (unsigned long long)c1);
+    }
     // default sink batching (all inserts at Combine), no resize: same filter as the oracle's
     {
       rpt::CreateBF c2(dev, /*estimated_cardinality=*/nb, {0});
