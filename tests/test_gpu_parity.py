@@ -533,16 +533,23 @@ def test_double_tile_edges_vs_oracle(rpt, n):
     assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
 
 
-@pytest.mark.parametrize("log_nb", [17, 21, 24])
+@pytest.mark.parametrize("strategy,log_nb,n,dense", [
+    ("partitioned", 17, 3 * 32768 + 777, False), ("partitioned", 21, 3 * 32768 + 777, False),
+    ("partitioned", 24, 3 * 32768 + 777, False), ("bucketed", 22, 5 * 16384 + 333, False),
+    ("bucketed", 24, 9 * 16384 + 4097, False), ("bucketed", 24, 9 * 16384 + 4097, True)])
 @pytest.mark.parametrize("use_row_sel", [False, True])
-def test_fused_sel_tail_equals_two_phase_path(rpt, log_nb, use_row_sel):
+def test_fused_sel_tail_equals_two_phase_path(rpt, strategy, log_nb, n, dense, use_row_sel):
     """rpt_bf_probe's partitioned pipeline ends in the fused tail (tile counts -> offsets -> the unpermute
-    writes the sel); rpt_bf_probe_phase1 + phase2 keep the result-bit path. Both must give the oracle's
-    sel and count, with and without a row selection, for 16 Ki- (2^17, 2^21) and 32 Ki-row (2^24) tiles."""
+    writes the sel); rpt_bf_probe_phase1 + phase2 keep the result-bit path (the bucketed strategy takes it
+    in both). Both must give the oracle's sel and count, with and without a row selection: 16 Ki- (2^17,
+    2^21) and 32 Ki-row (2^24) partition tiles; bucketed with 1 and 4 buckets, several level-1 tiles and a
+    partial last tile, and a probe where every row passes (the dense word-by-word sel expansion)."""
     build = orc.synth_build_keys(200000)
-    n = 3 * 32768 + 777
     probe = orc.synth_probe_keys(n, 200000, 250)
-    bf = with_strategy(rpt.BloomFilter(log_num_blocks=log_nb), "partitioned")
+    if dense:
+        probe = build[np.random.default_rng(7).integers(0, build.size, n)]
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.probe_strategy = {"partitioned": rpt.RPT_PROBE_PARTITIONED, "bucketed": rpt.RPT_PROBE_BUCKETED}[strategy]
     bf.insert(dev(build))
     w = orc.new_words(log_nb)
     orc.insert_keys(w, log_nb, build)
@@ -552,6 +559,7 @@ def test_fused_sel_tail_equals_two_phase_path(rpt, log_nb, use_row_sel):
     exp = ref if row_sel is None else np.intersect1d(row_sel, ref).astype(np.uint32)
     rs = dev(row_sel) if row_sel is not None else None
     m = row_sel.size if row_sel is not None else n
+    assert not dense or exp.size == m  # every row passes: the dense expansion runs
     keys = dev(probe)
     fused = bf.lookup_sel(keys, row_sel=rs).cpu().numpy().view(np.uint32)
     ws = torch.empty(bf.workspace_bytes(m), dtype=torch.uint8, device="cuda:0")
