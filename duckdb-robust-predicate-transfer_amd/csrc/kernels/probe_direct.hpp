@@ -143,6 +143,31 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
 // ascending selection vector. n <= kSmallRows.
 constexpr int kSmallThreads = 1024;
 constexpr uint64_t kSmallRows = RPT_SMALL_PROBE_ROWS;
+// The small kernels' tail: segment counts (<= 32) -> the ascending selection vector. Every wave scans the
+// counts itself (lane i holds segment i's) and expands its own segments' row-ordered result words.
+__device__ __forceinline__ void small_sel_tail(const uint64_t* s_words, const uint32_t* s_cnt, uint32_t n_segs,
+                                               const uint32_t* __restrict__ row_sel, uint32_t* __restrict__ out_sel,
+                                               uint64_t* __restrict__ out_count) {
+  constexpr uint32_t kWaves = kSmallThreads / 64;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t c = lane < n_segs ? s_cnt[lane] : 0u;
+  const uint32_t incl = wave_inclusive_sum(c);
+  if (threadIdx.x == 0) *out_count = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+  for (uint32_t seg = wave; seg < n_segs; seg += kWaves) {
+    // lanes 0..7 own the segment's 8 result words (64 rows each); pc = their survivors
+    uint64_t word = lane < kWordsPerSeg ? s_words[seg * kWordsPerSeg + lane] : 0ULL;
+    const uint32_t pc = __popcll(word);
+    uint32_t p = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl - c), static_cast<int>(seg))) +
+                 wave_inclusive_sum(pc) - pc;
+    const uint32_t row0 = seg * static_cast<uint32_t>(kSegRows) + lane * 64;
+    while (word) {
+      const uint32_t row = row0 + __builtin_ctzll(word);
+      out_sel[p++] = row_sel ? row_sel[row] : row;
+      word &= word - 1;
+    }
+  }
+}
+
 template <int K, bool DENSE>
 __global__ __launch_bounds__(kSmallThreads) void probe_small_kernel(const uint64_t* __restrict__ words,
                                                                    uint64_t block_mask, KeyArgs a, uint64_t n,
@@ -171,22 +196,122 @@ __global__ __launch_bounds__(kSmallThreads) void probe_small_kernel(const uint64
     store_segment_bits<K, DENSE>(pass, lane, seg, s_words, s_cnt);
   }
   __syncthreads();
-  // every wave scans the (<= 32) segment counts itself: lane i holds segment i's
-  const uint32_t c = lane < n_segs ? s_cnt[lane] : 0u;
-  const uint32_t incl = wave_inclusive_sum(c);
-  if (threadIdx.x == 0) *out_count = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
-  for (uint32_t seg = wave; seg < n_segs; seg += kWaves) {
-    // lanes 0..7 own the segment's 8 result words (64 rows each); pc = their survivors
-    uint64_t word = lane < kWordsPerSeg ? s_words[seg * kWordsPerSeg + lane] : 0ULL;
-    const uint32_t pc = __popcll(word);
-    uint32_t p = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl - c), static_cast<int>(seg))) +
-                 wave_inclusive_sum(pc) - pc;
-    const uint32_t row0 = seg * static_cast<uint32_t>(kSegRows) + lane * 64;
-    while (word) {
-      const uint32_t row = row0 + __builtin_ctzll(word);
-      out_sel[p++] = row_sel ? row_sel[row] : row;
-      word &= word - 1;
-    }
+  small_sel_tail(s_words, s_cnt, n_segs, row_sel, out_sel, out_count);
+}
+
+// ---- USE_BF's filter chain in one launch -----------------------------------------------------------
+// PhysicalUseBF::ExecuteInternal (physical_use_bf.cpp:127-179) runs its filters one after another, each
+// LookupSel over the rows the previous ones kept, so its result is the AND of the filters.
+// For a DuckDB-sized batch each LookupSel is latency-bound (launch, sync, and the key loads: the host
+// mirror passes device-mapped pinned host memory, one PCIe round trip), so the whole chain is one
+// single-workgroup launch whose (filter, 512-row segment) probes are independent items spread over the
+// 16 waves: every filter's key loads and gathers are in flight at once instead of one filter after
+// another (rows already failed are probed anyway: a gather costs less than the round trip it would
+// wait for). Each item's pass words land in LDS; their AND per word becomes the sel as in
+// probe_small_kernel. Columns of different key types share the general row mapping (row = base + 64 c +
+// lane). k <= kMaxChain, n <= kSmallRows.
+constexpr uint32_t kMaxChain = RPT_MAX_CHAIN;
+struct ChainArgs {
+  const uint64_t* words[kMaxChain];
+  uint64_t block_mask[kMaxChain];
+  KeyArgs a[kMaxChain];
+  int32_t key_type[kMaxChain];
+  uint32_t k;
+};
+// The hashes of a lane's 8 rows of a segment in the general mapping. Unlike load_hashes' general path
+// (a branch per row around dependent loads), the selection lookups are uniform branches and each level's
+// 8 loads are issued back to back: the keys usually sit in device-mapped host memory, where every
+// dependent load is a PCIe round trip (8 serialized key loads made the chain kernel 17 us, not 3).
+template <int K>
+__device__ __forceinline__ void chain_hashes(const KeyArgs& a, uint64_t base, uint64_t n, uint32_t lane,
+                                             uint64_t (&h)[8], bool (&ok)[8]) {
+  using Tr = KeyTraits<K>;
+  using T = typename Tr::T;
+  const uint32_t rem = static_cast<uint32_t>(n - base < kSegRows ? n - base : kSegRows);  // base < n
+  uint64_t idx[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    const uint32_t off = static_cast<uint32_t>(c * 64) + lane;
+    ok[c] = off < rem;
+    idx[c] = base + (ok[c] ? off : 0u);  // rows past n read row `base` (in range) and are discarded
   }
+  if (a.row_sel != nullptr) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) idx[c] = a.row_sel[idx[c]];
+  }
+  if (a.key_sel != nullptr) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) idx[c] = a.key_sel[idx[c]];
+  }
+  const T* keys = static_cast<const T*>(a.keys);
+  T kv[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) kv[c] = keys[idx[c]];
+  uint64_t vw[8];
+#pragma unroll
+  for (int c = 0; c < 8; c++) vw[c] = ~0ULL;
+  if (Tr::kValues && a.validity != nullptr) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) vw[c] = a.validity[idx[c] >> 6];
+  }
+#pragma unroll
+  for (int c = 0; c < 8; c++) {
+    uint64_t hv = Tr::hash(kv[c]);
+    if (Tr::kValues && !((vw[c] >> (idx[c] & 63)) & 1ULL)) hv = kNullHash;
+    h[c] = hv;
+  }
+}
+template <int K>
+__device__ __forceinline__ void chain_probe(const KeyArgs& a, const uint64_t* __restrict__ words, uint64_t block_mask,
+                                            const uint64_t* s_masks, uint64_t base, uint64_t n, uint32_t lane,
+                                            bool (&pass)[8]) {
+  uint64_t h[8];
+  bool ok[8];
+  chain_hashes<K>(a, base, n, lane, h, ok);
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint64_t m = mask_of(s_masks, h[j]);
+    const uint64_t w = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
+    pass[j] = ok[j] && (w & m) == m;
+  }
+}
+__global__ __launch_bounds__(kSmallThreads) void probe_chain_small_kernel(ChainArgs c, uint64_t n,
+                                                                          const uint32_t* __restrict__ row_sel,
+                                                                          uint32_t* __restrict__ out_sel,
+                                                                          uint64_t* __restrict__ out_count) {
+  constexpr uint32_t kSegs = kSmallRows / kSegRows;
+  constexpr uint32_t kWaves = kSmallThreads / 64;
+  __shared__ uint64_t s_masks[kNumMasks];
+  __shared__ uint64_t s_pass[kMaxChain][kSegs * kWordsPerSeg];  // each filter's row-ordered pass words
+  __shared__ uint64_t s_words[kSegs * kWordsPerSeg];
+  __shared__ uint32_t s_cnt[kSegs];
+  fill_mask_table(s_masks);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t n_segs = static_cast<uint32_t>((n + kSegRows - 1) / kSegRows);
+  for (uint32_t it = wave; it < c.k * n_segs; it += kWaves) {
+    const uint32_t f = it / n_segs, seg = it - f * n_segs;  // uniform
+    const uint64_t base = static_cast<uint64_t>(seg) * kSegRows;
+    bool pass[8];
+    if (c.key_type[f] == kKeyI64) chain_probe<kKeyI64>(c.a[f], c.words[f], c.block_mask[f], s_masks, base, n, lane, pass);
+    else if (c.key_type[f] == kKeyI32) chain_probe<kKeyI32>(c.a[f], c.words[f], c.block_mask[f], s_masks, base, n, lane, pass);
+    else chain_probe<kKeyHash>(c.a[f], c.words[f], c.block_mask[f], s_masks, base, n, lane, pass);
+    store_segment_bits<kKeyI64, false>(pass, lane, seg, s_pass[f], nullptr);
+  }
+  __syncthreads();
+  // the AND over the filters, word by word; then each segment's survivor count
+  for (uint32_t w = threadIdx.x; w < n_segs * kWordsPerSeg; w += kSmallThreads) {
+    uint64_t x = s_pass[0][w];
+    for (uint32_t f = 1; f < c.k; f++) x &= s_pass[f][w];
+    s_words[w] = x;
+  }
+  __syncthreads();
+  for (uint32_t seg = wave; seg < n_segs; seg += kWaves) {
+    const uint32_t pc = lane < kWordsPerSeg ? static_cast<uint32_t>(__popcll(s_words[seg * kWordsPerSeg + lane])) : 0u;
+    const uint32_t t = wave_sum(pc);
+    if (lane == 0) s_cnt[seg] = t;
+  }
+  __syncthreads();
+  small_sel_tail(s_words, s_cnt, n_segs, row_sel, out_sel, out_count);
 }
 }  // namespace rpt

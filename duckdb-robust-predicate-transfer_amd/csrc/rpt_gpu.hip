@@ -1438,6 +1438,42 @@ int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* ro
   return rpt_bf_probe_phase2(bf, row_sel, n, out_sel, out_count_dev, workspace, workspace_bytes, stream);
 }
 
+int rpt_bf_probe_chain(const rpt_bf* const* filters, const rpt_key_column* cols, uint32_t n_filters,
+                       const uint32_t* row_sel, uint64_t n, uint32_t* out_sel, uint64_t* out_count_dev,
+                       rpt_stream_t stream) {
+  if (!filters || !cols || !out_count_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_filters == 0 || n_filters > RPT_MAX_CHAIN)
+    return fail(RPT_ERR_INVALID_ARGUMENT, "n_filters=%u outside 1..%d", n_filters, RPT_MAX_CHAIN);
+  if (n > rpt::kSmallRows)
+    return fail(RPT_ERR_INVALID_ARGUMENT, "n=%llu rows exceeds RPT_SMALL_PROBE_ROWS", (unsigned long long)n);
+  rpt::ChainArgs c{};
+  for (uint32_t f = 0; f < n_filters; f++) {
+    if (!filters[f]) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter %u", f);
+    if (filters[f]->device != filters[0]->device) return fail(RPT_ERR_INVALID_ARGUMENT, "filters on different devices");
+    const int st = check_col(&cols[f]);
+    if (st != RPT_OK) return st;
+    c.words[f] = filters[f]->words;
+    c.block_mask[f] = (1ULL << filters[f]->log_num_blocks) - 1;
+    c.a[f] = rpt::KeyArgs{cols[f].keys, cols[f].key_sel, cols[f].validity, row_sel};
+    c.key_type[f] = cols[f].key_type;
+  }
+  c.k = n_filters;
+  RPT_ON_DEVICE(filters[0]->device);
+  hipStream_t s = as_stream(stream);
+  if (n == 0) {
+    RPT_HIP(hipMemsetAsync(out_count_dev, 0, sizeof(uint64_t), s));
+    return RPT_OK;
+  }
+  if (!out_sel) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_sel");
+  for (uint32_t f = 0; f < n_filters; f++) RPT_SETTLE(filters[f], s);
+  ProfScope prof("probe_chain_small_kernel", s);
+  hipLaunchKernelGGL(rpt::probe_chain_small_kernel, dim3(1), dim3(rpt::kSmallThreads), 0, s, c, n, row_sel, out_sel,
+                     out_count_dev);
+  prof.end();
+  RPT_LAUNCHED("probe_chain_small_kernel");
+  return RPT_OK;
+}
+
 
 int rpt_hash_combine(const rpt_key_column* col, uint64_t n, uint64_t* inout_hashes, rpt_stream_t stream) {
   return launch_hash<true>(col, n, inout_hashes, stream);

@@ -346,11 +346,19 @@ void* DeviceContext::host(int slot, size_t bytes) {
     synchronize();
     if (b.p) check_hip(hipHostFree(b.p), "hipHostFree");
     b.p = nullptr;
+    b.dp = nullptr;
     const size_t cap = std::max(bytes, 2 * b.cap);
     check_hip(hipHostMalloc(&b.p, cap, hipHostMallocDefault), "hipHostMalloc");
     b.cap = cap;
   }
   return b.p;
+}
+
+void* DeviceContext::host_device_ptr(int slot) {
+  Buf& b = host_[slot];
+  if (!b.p) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "host slot not allocated");
+  if (!b.dp) check_hip(hipHostGetDevicePointer(&b.dp, b.p, 0), "hipHostGetDevicePointer");
+  return b.dp;
 }
 
 void* DeviceContext::dev(int slot, size_t bytes) {
@@ -454,14 +462,11 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
     // small batch, atomic insert: the kernel reads the flattened keys from the pinned staging buffer
     // through device-mapped pointers (no copy)
     const Flattened f = flatten_pinned(ctx, chunks.data(), chunks.size(), cols[0], total, 0);
-    void *d_keys = nullptr, *d_valid = nullptr;
-    check_hip(hipHostGetDevicePointer(&d_keys, const_cast<uint8_t*>(f.keys), 0), "hipHostGetDevicePointer");
-    if (f.any_null) check_hip(hipHostGetDevicePointer(&d_valid, const_cast<uint64_t*>(f.valid), 0), "hipHostGetDevicePointer");
     rpt_key_column kc;
     kc.key_type = static_cast<int32_t>(f.key_type);
-    kc.keys = d_keys;
+    kc.keys = ctx.host_device_ptr(0);  // flatten_pinned: keys at the start of slot 0, validity of slot 1
     kc.key_sel = nullptr;
-    kc.validity = static_cast<const uint64_t*>(d_valid);
+    kc.validity = f.any_null ? static_cast<const uint64_t*>(ctx.host_device_ptr(1)) : nullptr;
     check(rpt_bf_insert(bf_, &kc, total, ctx.stream()));
     ctx.synchronize();  // the staging buffer is reused by the next call
     return;
@@ -570,10 +575,9 @@ void PTBloomFilter::LookupSelMapped(DeviceContext& ctx, const std::vector<const 
                                     std::vector<SelectionVector>& sels, uint64_t col, uint64_t total) const {
   const Flattened f = flatten_pinned(ctx, chunks.data(), chunks.size(), col, total, 0);
   auto* h_out = static_cast<uint8_t*>(ctx.host(2, 8 + total * 4));
-  void *d_keys = nullptr, *d_valid = nullptr, *d_out = nullptr;
-  check_hip(hipHostGetDevicePointer(&d_keys, const_cast<uint8_t*>(f.keys), 0), "hipHostGetDevicePointer");
-  check_hip(hipHostGetDevicePointer(&d_out, h_out, 0), "hipHostGetDevicePointer");
-  if (f.any_null) check_hip(hipHostGetDevicePointer(&d_valid, const_cast<uint64_t*>(f.valid), 0), "hipHostGetDevicePointer");
+  void* d_keys = ctx.host_device_ptr(0);  // flatten_pinned: keys at the start of slot 0, validity of slot 1
+  void* d_valid = f.any_null ? ctx.host_device_ptr(1) : nullptr;
+  void* d_out = ctx.host_device_ptr(2);
   rpt_key_column kc;
   kc.key_type = static_cast<int32_t>(f.key_type);
   kc.keys = d_keys;
@@ -874,13 +878,48 @@ uint64_t UseBF::Execute(DeviceContext& ctx, const DataChunk& input, SelectionVec
     rows_out_ += n;
     return n;
   }
+  // The filters that apply (cpp:139-155): not finalized -> skipped; an empty one -> no rows. The AND of
+  // the rest over a DuckDB-sized chunk is one launch (its result equals the loop below: each LookupSel
+  // sees the previous survivors, and stopping at 0 survivors changes nothing).
+  std::vector<size_t> act;
   for (size_t i = 0; i < filters_.size(); i++) {
     const auto& bf = filters_[i];
-    if (!bf || !bf->finalized_) continue;  // cpp:139-142
-    if (bf->IsEmpty()) {                   // cpp:145-155
+    if (!bf || !bf->finalized_) continue;
+    if (bf->IsEmpty()) {
       out.clear();
       return 0;
     }
+    act.push_back(i);
+  }
+  if (!act.empty() && act.size() <= RPT_MAX_CHAIN && n <= RPT_SMALL_PROBE_ROWS) {
+    const DataChunk* in = &input;
+    std::vector<const rpt_bf*> bfs;
+    std::vector<rpt_key_column> kcs;
+    for (size_t k = 0; k < act.size(); k++) {
+      const int slot = DeviceContext::kSlots / 2 + 2 * static_cast<int>(k);
+      const Flattened f = flatten_pinned(ctx, &in, 1, cols_[act[k]], n, slot);
+      rpt_key_column kc;
+      kc.key_type = static_cast<int32_t>(f.key_type);
+      kc.keys = ctx.host_device_ptr(slot);
+      kc.key_sel = nullptr;
+      kc.validity = f.any_null ? static_cast<const uint64_t*>(ctx.host_device_ptr(slot + 1)) : nullptr;
+      kcs.push_back(kc);
+      bfs.push_back(filters_[act[k]]->native());
+    }
+    auto* h_out = static_cast<uint8_t*>(ctx.host(2, 8 + n * 4));
+    void* d_out = ctx.host_device_ptr(2);
+    check(rpt_bf_probe_chain(bfs.data(), kcs.data(), static_cast<uint32_t>(act.size()), nullptr, n,
+                             reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_out) + 8), static_cast<uint64_t*>(d_out),
+                             ctx.stream()));
+    ctx.synchronize();
+    const uint64_t cnt = *reinterpret_cast<const volatile uint64_t*>(h_out);
+    const uint32_t* h_sel = reinterpret_cast<const uint32_t*>(h_out + 8);
+    out.assign(h_sel, h_sel + cnt);
+    rows_out_ += cnt;
+    return cnt;
+  }
+  for (size_t i : act) {
+    const auto& bf = filters_[i];
     // LookupSel over the current slice of the input (physical_use_bf.cpp:163,176-179)
     DataChunk sliced;
     sliced.count = out.size();

@@ -29,6 +29,7 @@ from .bloom import (  # noqa: F401
     log_num_blocks_for_rows,
     make_column,
     needs_resize,
+    probe_chain,
     synth_build_keys,
     synth_probe_keys,
     validity_from_mask,

@@ -108,6 +108,9 @@ SIGNATURES = {
         c_int,
         [c_void_p, POINTER(KeyColumn), c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p],
     ),
+    "rpt_bf_probe_chain": (
+        c_int, [c_void_p, POINTER(KeyColumn), ctypes.c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p]
+    ),
     "rpt_bf_probe_phase1": (
         c_int, [c_void_p, POINTER(KeyColumn), c_void_p, c_uint64, c_void_p, c_size_t, c_void_p]
     ),

@@ -50,6 +50,33 @@ def key_type_of(keys: torch.Tensor, key_type: Optional[int]) -> int:
     raise RptError(1, f"unsupported key dtype {keys.dtype}; pass key_type=RPT_KEY_HASH for hashes")
 
 
+def probe_chain(filters, columns, *, row_sel: Optional[torch.Tensor] = None, n: Optional[int] = None,
+                out_sel: Optional[torch.Tensor] = None, out_count: Optional[torch.Tensor] = None,
+                stream=None) -> torch.Tensor:
+    """USE_BF's filter chain in one launch (rpt_bf_probe_chain): ascending ids (int32) of the rows passing
+    every filters[i] on its own key column. columns[i]: a device key tensor, or a dict of make_column's
+    arguments (keys, key_type, key_sel, validity). n <= RPT_SMALL_PROBE_ROWS, 1..RPT_MAX_CHAIN filters."""
+    if not filters or len(filters) != len(columns):
+        raise RptError(1, "one key column per filter, at least one filter")
+    cols = [make_column(**c) if isinstance(c, dict) else make_column(c) for c in columns]
+    if n is None:
+        c0 = columns[0] if isinstance(columns[0], dict) else {"keys": columns[0]}
+        n = (row_sel.numel() if row_sel is not None else
+             (c0["key_sel"].numel() if c0.get("key_sel") is not None else c0["keys"].numel()))
+    if row_sel is not None and (row_sel.element_size() != 4 or not row_sel.is_cuda):
+        raise RptError(1, "row_sel must be a 32-bit device tensor")
+    device = filters[0].device
+    if out_sel is None:
+        out_sel = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    if out_count is None:
+        out_count = torch.zeros(1, dtype=torch.int64, device=device)
+    handles = (ctypes.c_void_p * len(filters))(*[f._h for f in filters])
+    arr = (KeyColumn * len(cols))(*cols)
+    check(filters[0]._lib.rpt_bf_probe_chain(handles, arr, len(filters), _ptr(row_sel), n, out_sel.data_ptr(),
+                                              out_count.data_ptr(), _stream(device, stream)))
+    return out_sel[: int(out_count.item())]
+
+
 def make_column(keys: torch.Tensor, key_type: Optional[int] = None, key_sel: Optional[torch.Tensor] = None,
                 validity: Optional[torch.Tensor] = None) -> KeyColumn:
     """rpt_key_column for a FLAT (key_sel None) or DICTIONARY (key_sel uint32/int32) key vector."""

@@ -202,6 +202,18 @@ int rpt_bf_probe_is_fused(const rpt_bf* bf, uint64_t n_rows);
 int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
                  uint32_t* out_sel, uint64_t* out_count_dev, void* workspace, size_t workspace_bytes,
                  rpt_stream_t stream);
+/* PhysicalUseBF::ExecuteInternal's filter chain (physical_use_bf.cpp:127-179: each LookupSel over the rows
+ * the previous filters kept, i.e. the AND of the filters) over one small batch in ONE launch: out_sel gets
+ * the ascending ids of the rows that pass every filters[i], probed on its own key column cols[i] (each
+ * column may have its own key type, dictionary, validity), and *out_count_dev their count. Rows are
+ * 0..n-1, or row_sel[0..n) as in rpt_bf_probe. 1 <= n_filters <= RPT_MAX_CHAIN, n <= RPT_SMALL_PROBE_ROWS,
+ * every filter on one device; no workspace. The skips and early exits of the reference loop (a filter not
+ * yet finalized is skipped, an empty filter passes nothing) are the caller's: pass the filters that
+ * apply. Buffers may be device-mapped pinned host memory, as for the fused rpt_bf_probe. */
+#define RPT_MAX_CHAIN 8
+int rpt_bf_probe_chain(const rpt_bf* const* filters, const rpt_key_column* cols, uint32_t n_filters,
+                       const uint32_t* row_sel, uint64_t n, uint32_t* out_sel, uint64_t* out_count_dev,
+                       rpt_stream_t stream);
 /* rpt_bf_probe in its two stream-ordered phases (same filter, workspace and stream), for callers that
  * time or overlap them. GATHER / LDS: phase 1 = hash + gather + result bits + per-segment counts,
  * phase 2 = scan + expansion into out_sel. PARTITIONED: phase 1 = partition rows by filter slice +

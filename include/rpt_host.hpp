@@ -75,10 +75,13 @@ class DeviceContext {
   void* stream() const { return stream_; }
   void synchronize();  // both streams
 
-  // internal: grow-on-demand buffers
-  static constexpr int kSlots = 16;
+  // internal: grow-on-demand buffers (host slots 16..31: UseBF's chained key columns)
+  static constexpr int kSlots = 32;
   void* host(int slot, size_t bytes);
   void* dev(int slot, size_t bytes);
+  // the device address of host slot `slot`'s pinned buffer (kernels read / write it in place), cached
+  // until the slot grows
+  void* host_device_ptr(int slot);
   // internal: the device-to-host stream of pipelined batches (created on first use) and its events
   void* copy_stream();
   void* event(int i);
@@ -97,6 +100,7 @@ class DeviceContext {
   struct Buf {
     void* p = nullptr;
     size_t cap = 0;
+    void* dp = nullptr;  // host slots: device address of p (0 until asked for)
   };
   Buf host_[kSlots], dev_[kSlots];
   void* events_[8] = {};
@@ -268,7 +272,9 @@ class CreateBF {
 
 // PhysicalUseBF::ExecuteInternal (physical_use_bf.cpp:60-198): AND of the filters over the chunk,
 // in filter order, with its early exits (empty filter -> 0 rows, 0 survivors -> stop) and skips
-// (filter not finalized). Returns the surviving row ids of the input chunk (ascending).
+// (filter not finalized). Returns the surviving row ids of the input chunk (ascending). A chunk of at
+// most RPT_SMALL_PROBE_ROWS rows whose applicable filters number 1..RPT_MAX_CHAIN runs the whole chain
+// as one launch (rpt_bf_probe_chain, one sync); otherwise filter by filter.
 class UseBF {
  public:
   UseBF(std::vector<std::shared_ptr<PTBloomFilter>> filters, std::vector<uint64_t> bound_column_indices,

@@ -4,13 +4,15 @@
 // CREATE_BF: 4 sink threads, 2048-row chunks (last one ragged), FLAT/CONSTANT/DICTIONARY vectors with
 // NULLs, sink batches staged to HBM, an under-estimated cardinality so Finalize must
 // ReinitializeAndRehash (from the HBM key segments); the parallel source re-emitting the materialized
-// chunks; then USE_BF with two filters (chain = AND), the empty-build early exit, the not-finalized
+// chunks; then USE_BF with two filters (chain = AND: one launch per chunk, and the filter-by-filter loop
+// over a chunk beyond RPT_SMALL_PROBE_ROWS), the empty-build early exit, the not-finalized
 // skip and passthrough; the build's min/max dynamic filter; a composite (two-column) key filter; a 256 MiB filter whose
 // batched insert and lookup take the bucketed strategy.
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <iterator>
 #include <cstring>
 #include <random>
 #include <thread>
@@ -407,6 +409,40 @@ int main() {
       base += ch.count;
     }
     EXPECT(use.rows_in() == np && use.rows_out() == total, "USE_BF counters");
+    // The per-chunk Execute above runs the chain as one launch (rpt_bf_probe_chain). One FLAT chunk of all
+    // np rows (> RPT_SMALL_PROBE_ROWS) takes the filter-by-filter loop instead, and a never-finalized filter
+    // inside the chain is skipped on both paths: both must give the oracle's AND.
+    {
+      auto nf = std::make_shared<rpt::PTBloomFilter>();
+      nf->Initialize(dev, 10);
+      rpt::UseBF us({f0, nf, f1}, {0, 0, 1});
+      std::vector<uint64_t> va = pack(pt.v0, 0, np), vb = pack(pt.v1, 0, np);
+      rpt::DataChunk big;
+      big.count = np;
+      big.data.resize(2);
+      big.data[0].key_type = rpt::KeyType::I64;
+      big.data[0].data = pt.c0.data();
+      big.data[0].validity = va.data();
+      big.data[1].key_type = rpt::KeyType::I32;
+      big.data[1].data = pt.c1.data();
+      big.data[1].validity = vb.data();
+      std::vector<uint32_t> a(np), b(np), exp;
+      const uint64_t n0 = rpt_oracle_probe_i64(w0.data(), lnb, pt.c0.data(), nullptr, va.data(), np, a.data());
+      const uint64_t n1 = rpt_oracle_probe_i32(w1.data(), lnb, pt.c1.data(), nullptr, vb.data(), np, b.data());
+      std::set_intersection(a.begin(), a.begin() + n0, b.begin(), b.begin() + n1, std::back_inserter(exp));
+      rpt::SelectionVector out;
+      us.Execute(ctx, big, out);
+      EXPECT(np > RPT_SMALL_PROBE_ROWS && out == exp, "USE_BF over one %zu-row chunk: %zu survivors, oracle %zu", np,
+             out.size(), exp.size());
+      size_t base2 = 0;
+      for (const auto& ch : pst.chunks) {  // the chained launch with the skipped filter in the middle
+        rpt::SelectionVector o2, o1;
+        us.Execute(ctx, ch, o2);
+        use.Execute(ctx, ch, o1);
+        EXPECT(o2 == o1, "skipped filter inside the chain changed chunk at row %zu", base2);
+        base2 += ch.count;
+      }
+    }
     // the same chain over the whole batch at once (survivors stay on the device between filters)
     {
       std::vector<const rpt::DataChunk*> ptrs;

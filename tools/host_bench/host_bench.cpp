@@ -128,6 +128,28 @@ int main() {
     printf("{\"op\": \"LookupSel\", \"threads\": %d, \"calls_per_thread\": %zu, \"us_per_call\": %.1f, \"rows_per_s\": %.4g}\n",
            T, per_thread, s / per_thread * 1e6, rows / s);
   }
+  // USE_BF's filter chain on one 2048-row vector per call: UseBF::Execute (K filters in one launch,
+  // rpt_bf_probe_chain) against K LookupSel calls one after another (one launch + sync each: the
+  // filter-by-filter loop's cost without its slicing), one operator thread
+  {
+    auto shared = std::shared_ptr<rpt::PTBloomFilter>(&bf, [](rpt::PTBloomFilter*) {});
+    for (size_t K : {1, 2, 3, 4}) {
+      rpt::UseBF ub(std::vector<std::shared_ptr<rpt::PTBloomFilter>>(K, shared), std::vector<uint64_t>(K, 0));
+      const size_t calls = 2000;
+      rpt::SelectionVector sv;
+      ub.Execute(ctx, pchunks[0], sv);  // warm-up
+      auto t0 = clk::now();
+      for (size_t c = 0; c < calls; c++) ub.Execute(ctx, pchunks[c % pchunks.size()], sv);
+      const double s_chain = std::chrono::duration<double>(clk::now() - t0).count();
+      t0 = clk::now();
+      for (size_t c = 0; c < calls; c++)
+        for (size_t k = 0; k < K; k++) bf.LookupSel(ctx, pchunks[c % pchunks.size()], sv, {0});
+      const double s_seq = std::chrono::duration<double>(clk::now() - t0).count();
+      printf("{\"op\": \"UseBF::Execute\", \"filters\": %zu, \"calls\": %zu, \"us_per_call\": %.1f, "
+             "\"us_per_call_filter_by_filter\": %.1f}\n",
+             K, calls, s_chain / calls * 1e6, s_seq / calls * 1e6);
+    }
+  }
   // a caching USE_BF: UseBF::ExecuteBatch over 16 .. 1024 chunks per call (one filter)
   {
     rpt::UseBF ub({std::shared_ptr<rpt::PTBloomFilter>(&bf, [](rpt::PTBloomFilter*) {})}, {0});
