@@ -109,7 +109,7 @@ def test_chain_of_eight_with_hash_column(rpt):
 
 
 def test_chain_segments_emptied_early(rpt):
-    """Segments whose rows all fail the first filter skip the rest; others go on (early-exit path)."""
+    """Segments whose rows all fail the first filter next to segments where most pass it."""
     n = 8192
     b0, b1 = keys_of(np.int64, 5000, 11), keys_of(np.int64, 5000, 12)
     (f0, w0), (f1, w1) = built(rpt, 14, b0), built(rpt, 14, b1)
@@ -150,3 +150,43 @@ def test_chain_argument_errors(rpt):
         rpt.probe_chain([f], [big])  # more than RPT_SMALL_PROBE_ROWS
     with pytest.raises(rpt.RptError):
         rpt.probe_chain([f, f], [p])  # one column per filter
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_chain_random(rpt, seed):
+    """Seeded sweep: 1..8 filters of random sizes (128 B..64 MiB), each over its own column with a random
+    key type (int64 / int32 / precomputed hashes), NULL rate, dictionary; random row counts and row
+    selections. The AND of the oracle's per-filter results, bit-exact."""
+    rng = np.random.default_rng(1000 + seed)
+    k = int(rng.integers(1, 9))
+    n = int(rng.choice([1, 2, 64, 513, 2048, int(rng.integers(1, 16385))]))
+    filters, cols, refs = [], [], []
+    for f in range(k):
+        log_nb = int(rng.choice([4, 10, 14, 17, 21, 23]))
+        dtype = np.int64 if rng.random() < 0.6 else np.int32
+        build = keys_of(dtype, int(rng.integers(1, 50_000)), seed * 16 + f)
+        bf, w = built(rpt, log_nb, build)
+        filters.append(bf)
+        m = int(rng.integers(1, 2 * n + 1)) if rng.random() < 0.4 else n  # dictionary size (if used)
+        vals = mostly_hits(rng, build, m, dtype, 500 + seed * 16 + f, frac=float(rng.choice([0.5, 0.9, 1.0])))
+        ksel = rng.integers(0, m, n).astype(np.uint32) if m != n else None
+        valid = gu.validity_words(rng.random(m) >= 0.1) if rng.random() < 0.4 else None
+        if rng.random() < 0.2 and dtype == np.int64:  # the column as precomputed hashes (NULLs not applied)
+            h = rpt.hash_keys(dev(vals))
+            col = {"keys": h, "key_type": rpt.RPT_KEY_HASH}
+            ref = orc.probe_keys(w, log_nb, vals, key_sel=ksel)
+        else:
+            col = {"keys": dev(vals), "validity": dev(valid) if valid is not None else None}
+            ref = orc.probe_keys(w, log_nb, vals, key_sel=ksel, validity=valid)
+        if ksel is not None:
+            col["key_sel"] = dev(ksel)
+        cols.append(col)
+        refs.append(ref)
+    exp = functools.reduce(np.intersect1d, refs).astype(np.uint32)
+    row_sel = None
+    if rng.random() < 0.3:
+        row_sel = np.sort(rng.choice(n, size=int(rng.integers(1, n + 1)), replace=False)).astype(np.uint32)
+        exp = np.intersect1d(exp, row_sel).astype(np.uint32)
+    got = rpt.probe_chain(filters, cols, row_sel=dev(row_sel) if row_sel is not None else None,
+                          n=row_sel.size if row_sel is not None else n)
+    assert np.array_equal(sel_of(got), exp)
