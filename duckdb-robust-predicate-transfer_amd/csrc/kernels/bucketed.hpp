@@ -31,7 +31,8 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t h, uint32_t bucket_mask) 
   return static_cast<uint32_t>(h >> (kLogNumMasks + 6 + kSliceLog + kBucketSliceLog)) & bucket_mask;
 }
 
-constexpr uint32_t kChunkEmpty = ~0u;
+constexpr uint32_t kChunkEmpty = ~0u;        // an extent not taken yet
+constexpr uint32_t kChunkInvalid = ~0u - 1;  // beyond the list's extent bound (never expected: flags `error`)
 constexpr uint32_t kMaxRunChunks = static_cast<uint32_t>(kL1TileRows / kChunkRows) + 1;  // chunks one run can touch
 constexpr uint32_t kL1Groups = 8;
 constexpr uint32_t kExtentChunks = 16;          // overflow extents: 64 Ki rows
@@ -49,11 +50,12 @@ struct L1Lists {
   uint32_t n_lists;     // groups * nb
 };
 
-// Chunk id of chunk c of list `list` when it is a fixed one or its extent is published (else kChunkEmpty).
+// Chunk id of chunk c of list `list` when it is a fixed one or its extent is published (else kChunkEmpty,
+// or kChunkInvalid past the list's extent bound).
 __device__ __forceinline__ uint32_t l1_chunk_id(const L1Lists& L, uint64_t list, uint32_t c) {
   if (c < L.k_fixed) return static_cast<uint32_t>(list * L.k_fixed + c);
   const uint32_t x = c - L.k_fixed, e = x / kExtentChunks;
-  if (e >= L.n_ext) return kChunkEmpty;
+  if (e >= L.n_ext) return kChunkInvalid;
   const uint32_t base = __hip_atomic_load(&L.ext_dir[list * L.n_ext + e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return base == kChunkEmpty ? kChunkEmpty : base + x % kExtentChunks;
 }
@@ -200,12 +202,14 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
       // ... then the ids of the chunks the run covers (fixed, own extents, or an extent an earlier run took)
       for (uint32_t cc = c0; cc <= c1; cc++) {
         uint32_t id, spins = 0;
-        while ((id = l1_chunk_id(L, list, cc)) == kChunkEmpty) {
-          if (++spins > kChunkSpinLimit) {
-            l1_flag_error(L);
+        for (;;) {
+          id = l1_chunk_id(L, list, cc);
+          if (id == kChunkInvalid || (id == kChunkEmpty && ++spins > kChunkSpinLimit)) {
+            l1_flag_error(L);  // copy the run into chunk 0 (in bounds); the result degrades, see B2 / B6
             id = 0;
             break;
           }
+          if (id != kChunkEmpty) break;
           __builtin_amdgcn_s_sleep(2);
         }
         s_chunk[cc - c0][own_b] = id;
@@ -246,9 +250,10 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
 // B2: per bucket (one workgroup each): its level-2 tiles are its lists' chunks in group order, 4 per tile,
 // the last tile completed with copies of the bucket's last chunk (rows past the lists' ends are never
 // read back); list_base[g][b] = the w-space row of list (g, b)'s first row; bucket_tiles[b] = the
-// bucket's first tile, bucket_tiles[nb] = the tile count (0 if the scatter flagged an error, so level 2
-// then runs on nothing and the result is visibly empty). Each list's last chunk is padded with copies of
-// its first row.
+// bucket's first tile, bucket_tiles[nb] = the tile count (0 if the scatter flagged an error: level 2 then
+// runs on nothing, and the result degrades to the conservative one, never to a false negative: a probe
+// passes every row (B6), an insert sets every filter bit (l1_error_fill_kernel)). Each list's last chunk is
+// padded with copies of its first row.
 constexpr int kListsThreads = 256;
 __global__ __launch_bounds__(kListsThreads) void bucket_lists_kernel(L1Lists L, uint32_t nb, uint32_t* __restrict__ chunk_map,
                                                                     uint64_t* __restrict__ list_base,
@@ -315,7 +320,8 @@ constexpr int kBucketUnpermuteThreads = RPT_BUCKET_UNPERMUTE_THREADS;
 __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kernel(
     const uint16_t* __restrict__ pos1, const uint64_t* __restrict__ bits2, uint64_t n, uint32_t bucket_mask,
     const uint32_t* __restrict__ counts_tm, const uint32_t* __restrict__ pre_tm, const uint64_t* __restrict__ list_base,
-    uint32_t groups, uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
+    uint32_t groups, const uint32_t* __restrict__ l1_error, uint64_t* __restrict__ out_bits,
+    uint32_t* __restrict__ seg_counts) {
   __shared__ uint32_t s_bits[kL1TileRows / 32];
   __shared__ uint32_t s_start[kMaxBuckets], s_item[kMaxBuckets + 1], s_cnt[kMaxBuckets];
   __shared__ uint64_t s_g[kMaxBuckets];
@@ -375,9 +381,12 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
     oc += c[i];
     ok_ += k[i];
   }
-  if (threadIdx.x == 0) s_item[nb] = total_items;
+  // the scatter hit a bound (never expected): level 2 did not run, every row passes (a Bloom filter may
+  // return false positives, never false negatives)
+  const bool err = __hip_atomic_load(l1_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  if (threadIdx.x == 0) s_item[nb] = err ? 0u : total_items;
   __syncthreads();
-  for (uint32_t it = threadIdx.x; it < total_items; it += kBucketUnpermuteThreads) {
+  for (uint32_t it = threadIdx.x; it < s_item[nb]; it += kBucketUnpermuteThreads) {
     uint32_t lo = 0, hi = nb;  // last bucket whose first item <= it
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
@@ -407,11 +416,23 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
     uint32_t byte = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) byte |= pass_bits2(s_bits, pv[sg][c]) << (2 * c);
+    if (err) byte = 0xFFu;
     const uint64_t row0 = seg * kSegRows + lane * 8;
     if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);
     out_bytes[seg * (kSegRows / 8) + lane] = static_cast<uint8_t>(byte);
     const uint32_t cnt = wave_sum(__popc(byte));
     if (lane == 0) seg_counts[seg] = cnt;
   }
+}
+
+// B7: after a bucketed insert whose scatter hit a bound (never expected; B1): every filter bit set, so the
+// keys it could not insert still pass every probe. Without the flag each workgroup reads one word and leaves.
+constexpr int kErrorFillThreads = 256;
+__global__ __launch_bounds__(kErrorFillThreads) void l1_error_fill_kernel(uint64_t* __restrict__ words, uint64_t n_words,
+                                                                         const uint32_t* __restrict__ l1_error) {
+  if (__hip_atomic_load(l1_error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;  // uniform
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kErrorFillThreads + threadIdx.x; i < n_words;
+       i += static_cast<uint64_t>(gridDim.x) * kErrorFillThreads)
+    words[i] = ~0ULL;
 }
 }  // namespace rpt

@@ -759,6 +759,11 @@ struct BucketLevel1 {
   uint32_t* counts_tm;  // probe only
   uint32_t* pre_tm;     // probe only
 };
+// The level-1 error flag (L1Lists::error) inside the lists block.
+uint32_t* l1_error_flag(uint32_t* lists, const L1Geom& g) { return lists + g.n_lists + g.groups; }
+#ifdef RPT_TESTING_HOOKS
+std::atomic<int> g_force_l1_error{0};  // rpt_testing_force_l1_error
+#endif
 int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool dense, uint64_t n, int L,
                       const BucketLevel1& w, int64_t* stats) {
   const L1Geom g = l1_geom(n, L);
@@ -769,9 +774,12 @@ int run_bucket_level1(hipStream_t s, int key_type, const rpt::KeyArgs& a, bool d
   if (g.n_ext)
     RPT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(w.ext_dir), static_cast<int>(rpt::kChunkEmpty),
                               n_lists * g.n_ext, s));
-  const rpt::L1Lists lists{w.lists, w.lists + n_lists, w.lists + n_lists + g.groups, w.ext_dir,
-                           static_cast<uint32_t>(g.k_fixed), static_cast<uint32_t>(g.n_ext),
-                           static_cast<uint32_t>(g.shard_ext), g.groups, static_cast<uint32_t>(n_lists)};
+  rpt::L1Lists lists{w.lists, w.lists + n_lists, l1_error_flag(w.lists, g), w.ext_dir,
+                     static_cast<uint32_t>(g.k_fixed), static_cast<uint32_t>(g.n_ext),
+                     static_cast<uint32_t>(g.shard_ext), g.groups, static_cast<uint32_t>(n_lists)};
+#ifdef RPT_TESTING_HOOKS
+  if (g_force_l1_error.load()) lists.k_fixed = lists.n_ext = 0;  // every chunk past the bound: the error path
+#endif
   RPT_DISPATCH_KD(launch_bucket_scatter_t, key_type, dense, static_cast<unsigned>(g.t1), s, a, n, g.nb - 1, lists, w.hash_lo,
                   w.hash_hi, w.pos1, w.counts_tm, w.pre_tm, stats);
   RPT_LAUNCHED("bucket_scatter_kernel");
@@ -1196,6 +1204,11 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   hipLaunchKernelGGL(rpt::slice_insert_kernel, dim3(grid_slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words, splits,
                      n_tiles, ws.recs, ws.runs, static_cast<uint32_t>(rpt::tile_cap_for(tile_slices, tm)), bucket_tiles, mode);
   prof_i.end();
+  if (buck) {  // a level-1 bound hit (never expected): every bit set instead of keys missing
+    const uint64_t n_words = 1ULL << L;
+    hipLaunchKernelGGL(rpt::l1_error_fill_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(ceil_div(n_words, rpt::kErrorFillThreads * 8ULL), 4096))),
+                       dim3(rpt::kErrorFillThreads), 0, s, bf->words, n_words, l1_error_flag(ws.lists, l1_geom(n, L)));
+  }
   const hipError_t el = hipGetLastError();
   if (store_all && el == hipSuccess) bf->clear_pending.store(false);  // the slice stores zeroed the words
   order.done(false);
@@ -1357,7 +1370,8 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
       ProfScope prof8b_("bucket_unpermute_kernel", s);
       hipLaunchKernelGGL(rpt::bucket_unpermute_kernel, dim3(static_cast<unsigned>(ceil_div(n, rpt::kL1TileRows))),
                          dim3(rpt::kBucketUnpermuteThreads), 0, s, ws.pos1, ws.bits2, n, bucket_count(L) - 1,
-                         ws.counts_tm, ws.pre_tm, ws.list_base, l1_geom(n, L).groups, ws.bits, ws.seg_counts);
+                         ws.counts_tm, ws.pre_tm, ws.list_base, l1_geom(n, L).groups, l1_error_flag(ws.lists, l1_geom(n, L)),
+                         ws.bits, ws.seg_counts);
       prof8b_.end();
       RPT_LAUNCHED("bucket_unpermute_kernel");
     }
@@ -1858,6 +1872,7 @@ int rpt_testing_set_rccl_api(const rpt_rccl_api_table* table) {
   return RPT_OK;
 }
 uint64_t rpt_testing_bucketed_insert_batch(void) { return kBucketedInsertBatch; }
+void rpt_testing_force_l1_error(int on) { g_force_l1_error.store(on != 0); }
 #endif  // RPT_TESTING_HOOKS
 
 int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out) {

@@ -49,6 +49,9 @@ int rpt_testing_set_rccl_api(const rpt_rccl_api_table* table);
 /* Test build only: the row count above which rpt_bf_insert_ws runs a bucketed insert in batches (2^31 in
  * the product, 2^20 here, so the batching runs at test sizes). */
 uint64_t rpt_testing_bucketed_insert_batch(void);
+/* Test build only: on != 0 makes every later bucketed level 1 hit its chunk bound (the never-expected
+ * error path: the probe must then pass every row and the insert set every filter bit). */
+void rpt_testing_force_l1_error(int on);
 #endif
 
 #ifdef __cplusplus

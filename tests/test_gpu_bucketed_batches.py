@@ -73,3 +73,43 @@ def test_bucketed_insert_in_batches_vs_oracle(tlib, dtype, n, nulls, dictionary)
     assert np.array_equal(bf.export_words(), w)
     assert bf.minmax() == orc.minmax(keys, validity=vw, **kw)
     bf.close()
+
+
+def test_level1_error_path_is_conservative(tlib):
+    """A level-1 chunk bound hit (never expected: the bounds cover one list holding a whole group) must not
+    turn into false negatives. Forced through the test build's hook: a bucketed probe then passes every row
+    and a bucketed insert sets every filter bit; clearing the hook restores exact results."""
+    import rpt_amd
+
+    tlib.rpt_testing_force_l1_error.argtypes = [ctypes.c_int]
+    tlib.rpt_testing_force_l1_error.restype = None
+    log_nb = 23  # 64 MiB, 2 buckets
+    rng = np.random.default_rng(5)
+    keys = rng.integers(-2**62, 2**62, size=300_000, dtype=np.int64)
+    probe = np.where(rng.random(200_003) < 0.2, keys[rng.integers(0, keys.size, 200_003)],
+                     rng.integers(-2**62, 2**62, size=200_003, dtype=np.int64))
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, keys)
+    bf = rpt_amd.BloomFilter(log_num_blocks=log_nb, lib=tlib)
+    bf.probe_strategy = 4  # BUCKETED
+    bf.insert(dev(keys), strategy=1)  # atomic: exact words
+    assert np.array_equal(bf.export_words(), w)
+    try:
+        tlib.rpt_testing_force_l1_error(1)
+        sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
+        assert np.array_equal(sel, np.arange(probe.size, dtype=np.uint32))  # every row passes
+        full = rpt_amd.BloomFilter(log_num_blocks=log_nb, lib=tlib)
+        full.insert(dev(keys), strategy=INS_BUCKETED)
+        torch.cuda.synchronize()
+        assert (full.export_words() == np.uint64(2**64 - 1)).all()  # every bit set
+        assert full.minmax() == orc.minmax(keys)
+        full.close()
+    finally:
+        tlib.rpt_testing_force_l1_error(0)
+    sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
+    again = rpt_amd.BloomFilter(log_num_blocks=log_nb, lib=tlib)
+    again.insert(dev(keys), strategy=INS_BUCKETED)
+    assert np.array_equal(again.export_words(), w)
+    again.close()
+    bf.close()
