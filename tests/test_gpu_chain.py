@@ -2,6 +2,7 @@
 the chain, each probed on its own key column (physical_use_bf.cpp:127-179 probes them one after another, each
 LookupSel over the previous survivors: the AND of the per-filter oracle results). Bit-exact."""
 import functools
+import os
 
 import numpy as np
 import pytest
@@ -152,7 +153,7 @@ def test_chain_argument_errors(rpt):
         rpt.probe_chain([f, f], [p])  # one column per filter
 
 
-@pytest.mark.parametrize("seed", range(16))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("RPT_FUZZ_SEEDS", "16"))))
 def test_chain_random(rpt, seed):
     """Seeded sweep: 1..8 filters of random sizes (128 B..64 MiB), each over its own column with a random
     key type (int64 / int32 / precomputed hashes), NULL rate, dictionary; random row counts and row
