@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <limits>
 #include <thread>
 #include <utility>
 
@@ -32,7 +33,64 @@ struct DeviceScope {
   }
 };
 
+// Bytes per key of a device column (I32 / I64) or of a host column of any KeyType.
 size_t key_size(KeyType t) { return t == KeyType::I32 ? 4 : 8; }
+size_t source_size(KeyType t) {
+  switch (t) {
+    case KeyType::I8:
+    case KeyType::U8: return 1;
+    case KeyType::I16:
+    case KeyType::U16: return 2;
+    case KeyType::I32:
+    case KeyType::U32:
+    case KeyType::F32: return 4;
+    default: return 8;
+  }
+}
+// The device key type a host column is staged as (rpt_host.hpp, KeyType).
+KeyType device_type(KeyType t) {
+  switch (t) {
+    case KeyType::I8:
+    case KeyType::I16:
+    case KeyType::U8:
+    case KeyType::U16:
+    case KeyType::I32:
+    case KeyType::F32: return KeyType::I32;
+    default: return KeyType::I64;
+  }
+}
+bool keeps_minmax(KeyType t) { return t != KeyType::U64 && t != KeyType::F32 && t != KeyType::F64; }
+
+// One host key (its source bytes) -> its device value: what DuckDB's Hash<T> hashes (rpt_host.hpp KeyType).
+uint64_t device_value(KeyType t, const uint8_t* p) {
+  switch (t) {
+    case KeyType::I8: { int8_t v; std::memcpy(&v, p, 1); return static_cast<uint32_t>(static_cast<int32_t>(v)); }
+    case KeyType::I16: { int16_t v; std::memcpy(&v, p, 2); return static_cast<uint32_t>(static_cast<int32_t>(v)); }
+    case KeyType::U8: return p[0];
+    case KeyType::U16: { uint16_t v; std::memcpy(&v, p, 2); return v; }
+    case KeyType::I32:
+    case KeyType::U32: { uint32_t v; std::memcpy(&v, p, 4); return v; }
+    case KeyType::F32: {
+      float v;
+      std::memcpy(&v, p, 4);
+      if (v == 0.0f) v = 0.0f;                                        // -0.0 -> 0.0
+      else if (v != v) v = std::numeric_limits<float>::quiet_NaN();   // every NaN -> the quiet NaN
+      uint32_t b;
+      std::memcpy(&b, &v, 4);
+      return b;
+    }
+    case KeyType::F64: {
+      double v;
+      std::memcpy(&v, p, 8);
+      if (v == 0.0) v = 0.0;
+      else if (v != v) v = std::numeric_limits<double>::quiet_NaN();
+      uint64_t b;
+      std::memcpy(&b, &v, 8);
+      return b;
+    }
+    default: { uint64_t v; std::memcpy(&v, p, 8); return v; }
+  }
+}
 
 bool valid_bit(const uint64_t* validity, uint64_t idx) {
   return validity == nullptr || ((validity[idx >> 6] >> (idx & 63)) & 1ULL);
@@ -58,12 +116,50 @@ uint64_t mask_bits(const uint64_t* validity, uint64_t r, uint32_t n) {
   return n >= 64 ? b : b & ((1ULL << n) - 1);
 }
 
-// Flatten one column of `chunk` (FLAT / CONSTANT / DICTIONARY / SEQUENCE) into `keys` (element size of the
-// column) and clear the bits of its NULL rows at row offset `row0` of `valid_words` (preset to
-// all-valid: a chunk without NULLs touches no validity word), 64 rows per step. Returns true if any
-// row was NULL.
-bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* valid_words, uint64_t row0) {
-  const size_t es = key_size(v.key_type);
+// A column whose keys must be converted on the way to the device (everything but I32 / I64) into `keys` as
+// device values, its NULL rows cleared in `valid_words` as flatten_column does.
+bool flatten_converted(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* valid_words, uint64_t row0) {
+  const size_t ss = source_size(v.key_type), ds = key_size(device_type(v.key_type));
+  const uint8_t* src = static_cast<const uint8_t*>(v.data);
+  bool any_null = false;
+  for (uint64_t r = 0; r < count; r += 64) {
+    const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));
+    uint64_t nulls = 0;
+    for (uint32_t e = 0; e < n; e++) {
+      uint64_t idx = r + e, x = 0;
+      uint8_t seq[8];
+      const uint8_t* p;
+      if (v.type == VectorType::SEQUENCE) {  // start + row * increment, wrapped to the column's width
+        x = static_cast<uint64_t>(v.seq_start) + static_cast<uint64_t>(v.seq_increment) * idx;
+        std::memcpy(seq, &x, 8);             // little-endian: the low bytes are the narrower value
+        p = seq;
+      } else {
+        if (v.type == VectorType::CONSTANT) idx = 0;
+        else if (v.type == VectorType::DICTIONARY) {
+          idx = v.sel[r + e];
+          if (idx >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
+        }
+        p = src + idx * ss;
+        nulls |= static_cast<uint64_t>(!valid_bit(v.validity, idx)) << e;
+      }
+      const uint64_t d = device_value(v.key_type, p);
+      std::memcpy(keys + (r + e) * ds, &d, ds);  // little-endian: an I32 device value is the low 4 bytes
+    }
+    any_null |= nulls != 0;
+    clear_bits(valid_words, row0 + r, nulls, n);
+  }
+  return any_null;
+}
+
+// Flatten one column of `chunk` (FLAT / CONSTANT / DICTIONARY / SEQUENCE) into `keys` and clear the bits of
+// its NULL rows at row offset `row0` of `valid_words` (preset to all-valid: a chunk without NULLs touches
+// no validity word), 64 rows per step. Returns true if any row was NULL. to_device: keys are device values
+// (key_size(device_type) bytes each: converted for the non-I32/I64 types); else the column's own values
+// (source_size bytes: the materialized copy the CREATE_BF source re-emits).
+bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* valid_words, uint64_t row0,
+                    bool to_device = true) {
+  if (to_device && device_type(v.key_type) != v.key_type) return flatten_converted(v, count, keys, valid_words, row0);
+  const size_t es = source_size(v.key_type);
   bool any_null = false;
   switch (v.type) {
     case VectorType::FLAT:
@@ -104,14 +200,7 @@ bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* va
     case VectorType::SEQUENCE: {  // start + r * increment in two's complement (wraps as DuckDB's)
       uint64_t x = static_cast<uint64_t>(v.seq_start);
       const uint64_t inc = static_cast<uint64_t>(v.seq_increment);
-      if (es == 8) {
-        for (uint64_t r = 0; r < count; r++, x += inc) std::memcpy(keys + r * 8, &x, 8);
-      } else {
-        for (uint64_t r = 0; r < count; r++, x += inc) {
-          const uint32_t y = static_cast<uint32_t>(x);
-          std::memcpy(keys + r * 4, &y, 4);
-        }
-      }
+      for (uint64_t r = 0; r < count; r++, x += inc) std::memcpy(keys + r * es, &x, es);  // little-endian
       break;
     }
   }
@@ -132,7 +221,7 @@ Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, siz
                          uint64_t total, int slot) {
   if (n_chunks == 0) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "no chunks");
   const Vector& v0 = chunks[0]->data.at(col);
-  const size_t es = key_size(v0.key_type);
+  const size_t es = key_size(device_type(v0.key_type));
   const uint64_t nwords = (total + 63) / 64;
   auto* hkeys = static_cast<uint8_t*>(ctx.host(slot, std::max<size_t>(total * es, 16)));
   auto* hvalid = static_cast<uint64_t*>(ctx.host(slot + 1, std::max<size_t>(nwords * 8, 8)));
@@ -168,7 +257,7 @@ Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, siz
     for (auto& th : pool) th.join();
     for (char c : nulls) any_null |= c != 0;
   }
-  return Flattened{v0.key_type, hkeys, hvalid, any_null};
+  return Flattened{device_type(v0.key_type), hkeys, hvalid, any_null};
 }
 
 // Copy a flattened column to device buffers (dvalid is only written when the batch had NULLs).
@@ -444,6 +533,7 @@ void PTBloomFilter::Initialize(int device, uint32_t est_num_rows) {
     bf_ = nullptr;
   }
   check(rpt_bf_create(device, est_num_rows, &bf_));
+  minmax_kept_.store(true);
 }
 
 void PTBloomFilter::Insert(DeviceContext& ctx, const DataChunk& chunk, const std::vector<uint64_t>& cols) {
@@ -454,6 +544,7 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
                                 const std::vector<uint64_t>& cols) {
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:72-74
+  if (cols.size() == 1) NoteKeyType(chunks[0]->data.at(cols[0]).key_type);  // (composite keys carry no min/max)
   if (cols.size() == 1 && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
     InsertPipelined(ctx, chunks, cols[0]);
     return;
@@ -484,7 +575,7 @@ void PTBloomFilter::InsertPipelined(DeviceContext& ctx, const std::vector<const 
     max_rows = std::max(max_rows, r.rows);
     ws_bytes = std::max(ws_bytes, rpt_bf_insert_workspace_bytes(bf_, r.rows));
   }
-  const size_t es = key_size(chunks[st[0].c_lo]->data.at(col).key_type);
+  const size_t es = key_size(device_type(chunks[st[0].c_lo]->data.at(col).key_type));
   PipelineBuffers pb(ctx, max_rows, es);
   void* ws = ws_bytes ? ctx.dev(6, ws_bytes) : nullptr;
   auto s = static_cast<hipStream_t>(ctx.stream());
@@ -611,7 +702,7 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
     max_rows = std::max(max_rows, r.rows);
     ws_bytes = std::max(ws_bytes, rpt_bf_probe_workspace_bytes(bf_, r.rows));
   }
-  const size_t es = key_size(chunks[st[0].c_lo]->data.at(col).key_type);
+  const size_t es = key_size(device_type(chunks[st[0].c_lo]->data.at(col).key_type));
   PipelineBuffers pb(ctx, max_rows, es);
   void* ws = ctx.dev(2, ws_bytes);
   auto s = static_cast<hipStream_t>(ctx.stream());
@@ -715,7 +806,11 @@ int PTBloomFilter::LogNumBlocks() const {
 bool PTBloomFilter::MinMax(int64_t& min_value, int64_t& max_value) const {
   int has = 0;
   check(rpt_bf_get_minmax(bf_, &min_value, &max_value, &has, nullptr));
-  return has != 0;
+  return has != 0 && minmax_kept_.load();
+}
+
+void PTBloomFilter::NoteKeyType(KeyType t) {
+  if (!keeps_minmax(t)) minmax_kept_.store(false);
 }
 
 std::vector<uint64_t> PTBloomFilter::ExportWords() const {
@@ -757,10 +852,11 @@ void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
   for (size_t c = 0; c < chunk.data.size(); c++) {
     const Vector& v = chunk.data[c];
     if (v.data == nullptr && v.type != VectorType::SEQUENCE) continue;  // a column this mirror does not carry
-    const size_t es = key_size(v.key_type);
+    const size_t es = source_size(v.key_type);
     std::vector<uint64_t> keys((chunk.count * es + 7) / 8 + 1, 0);
     std::vector<uint64_t> valid((chunk.count + 63) / 64 + 1, ~0ULL);  // all valid; NULL rows cleared
-    const bool any_null = flatten_column(v, chunk.count, reinterpret_cast<uint8_t*>(keys.data()), valid.data(), 0);
+    const bool any_null =
+        flatten_column(v, chunk.count, reinterpret_cast<uint8_t*>(keys.data()), valid.data(), 0, /*to_device=*/false);
     Vector f;
     f.type = VectorType::FLAT;
     f.key_type = v.key_type;
@@ -786,6 +882,7 @@ void CreateBF::Flush(LocalState& local) const {
     if (local.chunks[k].count) batch.push_back(&local.chunks[k]);
   for (size_t i = 0; i < cols_.size(); i++) {
     const DeviceKeyColumn::Segment& g = local.keys[i].Append(local.ctx, batch, cols_[i]);
+    filters_[i]->NoteKeyType(batch[0]->data.at(cols_[i]).key_type);
     filters_[i]->InsertDevice(local.ctx, g.col, g.rows);
   }
   local.pending_from = local.chunks.size();
@@ -929,7 +1026,7 @@ uint64_t UseBF::Execute(DeviceContext& ctx, const DataChunk& input, SelectionVec
     std::vector<uint32_t> composed;
     std::vector<uint64_t> seq_vals;  // SEQUENCE: the selected rows' values (as FLAT)
     if (v.type == VectorType::SEQUENCE) {
-      const size_t es = key_size(v.key_type);
+      const size_t es = source_size(v.key_type);
       seq_vals.resize((out.size() * es + 7) / 8 + 1);
       uint8_t* dst = reinterpret_cast<uint8_t*>(seq_vals.data());
       for (size_t r = 0; r < out.size(); r++) {

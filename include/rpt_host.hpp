@@ -38,7 +38,15 @@ class GpuError : public std::runtime_error {
 // DuckDB VectorType subset the hot path sees (HashColumns flattens CONSTANT, bloom_filter.cpp:19-21;
 // VectorOperations::Hash reads the others through their unified format).
 enum class VectorType { FLAT, CONSTANT, DICTIONARY, SEQUENCE };
-enum class KeyType { I32 = RPT_KEY_I32, I64 = RPT_KEY_I64 };
+// DuckDB physical key types. I32 (INTEGER, DATE) and I64 (BIGINT, TIMESTAMP) go to the device as they are.
+// The others are converted while the column is staged, to the value DuckDB's Hash<T> hashes (restated, parity
+// unpinned like the int32 rule): I8 / I16 (TINYINT, SMALLINT) sign-extended and U8 / U16 (UTINYINT,
+// USMALLINT) zero-extended to I32 (Hash<T> casts to uint32_t); U32 (UINTEGER) zero-extended to I64 (same hash,
+// and the key min/max stays exact); U64 (UBIGINT) as its bits; F32 / F64 (FLOAT, DOUBLE) as their bits after
+// DuckDB's equality transform (-0.0 -> 0.0, every NaN -> the quiet NaN), F32's zero-extended like a uint32.
+// The key min/max (MinMax) is exact for I8..U32 and not kept for U64 / F32 / F64 (their device values do not
+// order like the keys): there the shim keeps the reference's host UpdateMinMax.
+enum class KeyType { I32 = RPT_KEY_I32, I64 = RPT_KEY_I64, I8 = 16, I16, U8, U16, U32, U64, F32, F64 };
 
 // One key column of a DataChunk.
 //   FLAT:       data[row], validity indexed by row
@@ -170,8 +178,12 @@ class PTBloomFilter {
   bool NeedsResize(uint64_t actual_rows) const;
   bool IsEmpty() const;
   int LogNumBlocks() const;
-  // Min/max of the valid I32/I64 keys inserted (the min/max dynamic filter; false: none yet).
+  // Min/max of the valid keys inserted (the min/max dynamic filter), as int64 (I8..U32 values exactly);
+  // false: none yet, or a U64 / F32 / F64 column was inserted (KeyType).
   bool MinMax(int64_t& min_value, int64_t& max_value) const;
+  // A host column of this type is inserted (Insert / InsertBatch / CreateBF note it themselves; callers that
+  // stage their own device columns from such keys call it).
+  void NoteKeyType(KeyType t);
   std::vector<uint64_t> ExportWords() const;
   // Multi-GPU Combine: OR all-reduce of every rank's partial filter over an RCCL communicator
   // (ncclComm_t, one rank per GPU; collective: every rank calls it). rpt_bf_allreduce_or.
@@ -188,6 +200,7 @@ class PTBloomFilter {
   void LookupSelMapped(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                        std::vector<SelectionVector>& sels, uint64_t col, uint64_t total) const;
   rpt_bf* bf_ = nullptr;
+  std::atomic<bool> minmax_kept_{true};  // no U64 / F32 / F64 column inserted since Initialize
 };
 
 // The hot-path part of PhysicalCreateBF: parallel Sink (materialize + insert), Combine, Finalize

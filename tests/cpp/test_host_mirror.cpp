@@ -13,6 +13,8 @@
 #include <cstdlib>
 #include <algorithm>
 #include <iterator>
+#include <limits>
+#include <type_traits>
 #include <cstring>
 #include <random>
 #include <thread>
@@ -177,6 +179,226 @@ static Table make_table(size_t n, uint64_t seed, int null_every, size_t const_ru
     t.v0[i] = true;
   }
   return t;
+}
+
+
+// ---------------- key types beyond INTEGER / BIGINT (rpt_host.hpp KeyType) -------------------------
+// The conversion restated independently of the mirror: what DuckDB's Hash<T> hashes, as an I32 / I64 device
+// value (Hash<T> casts narrow integers to uint32_t; FLOAT / DOUBLE hash their bits after -0.0 -> 0.0 and
+// NaN -> the quiet NaN; parity unpinned, like the int32 rule).
+template <typename T>
+static uint64_t expect_device(T v) {
+  if constexpr (std::is_floating_point<T>::value) {
+    if (v == T(0)) v = T(0);
+    else if (v != v) v = std::numeric_limits<T>::quiet_NaN();
+    if constexpr (sizeof(T) == 4) {
+      uint32_t b;
+      std::memcpy(&b, &v, 4);
+      return b;
+    } else {
+      uint64_t b;
+      std::memcpy(&b, &v, 8);
+      return b;
+    }
+  } else if constexpr (sizeof(T) == 8) {
+    return static_cast<uint64_t>(v);
+  } else {
+    return static_cast<uint32_t>(v);  // sign-extends signed types, as static_cast<uint32_t> in Hash<T>
+  }
+}
+
+// One key type end to end: FLAT (with NULLs), DICTIONARY and CONSTANT chunks (+ SEQUENCE for integers)
+// inserted through PTBloomFilter::InsertBatch and through CreateBF; filter words and LookupSel against the
+// oracle fed the restated device values; min/max exact or absent per KeyType; the CREATE_BF source
+// re-emits the original values.
+template <typename T>
+static void typed_keys_case(int dev, rpt::KeyType kt, const std::vector<T>& vals, bool minmax_kept, const char* name) {
+  const size_t n = vals.size();
+  const bool dev64 = kt == rpt::KeyType::U32 || kt == rpt::KeyType::U64 || kt == rpt::KeyType::F64;
+  std::vector<bool> valid(n);
+  for (size_t i = 0; i < n; i++) valid[i] = i % 13 != 5;
+  // chunks: [0, 2048) FLAT, [2048, n) DICTIONARY (reversed), plus one CONSTANT and (integers) one SEQUENCE chunk
+  std::vector<uint64_t> vw0 = pack(valid, 0, 2048), vw1;
+  std::vector<T> dict(vals.begin() + 2048, vals.end());
+  std::reverse(dict.begin(), dict.end());
+  std::vector<uint32_t> dsel(n - 2048);
+  std::vector<bool> dvalid(n - 2048);
+  for (size_t i = 0; i < n - 2048; i++) {
+    dsel[i] = static_cast<uint32_t>(n - 2048 - 1 - i);
+    dvalid[n - 2048 - 1 - i] = valid[2048 + i];
+  }
+  vw1 = pack(dvalid, 0, n - 2048);
+  const T cval = vals[7];
+  const uint64_t cvalid = 1;
+  std::vector<rpt::DataChunk> chunks(3);
+  chunks[0].count = 2048;
+  chunks[0].data.resize(1);
+  chunks[0].data[0].key_type = kt;
+  chunks[0].data[0].data = vals.data();
+  chunks[0].data[0].validity = vw0.data();
+  chunks[1].count = n - 2048;
+  chunks[1].data.resize(1);
+  chunks[1].data[0].key_type = kt;
+  chunks[1].data[0].type = rpt::VectorType::DICTIONARY;
+  chunks[1].data[0].data = dict.data();
+  chunks[1].data[0].sel = dsel.data();
+  chunks[1].data[0].dict_size = dict.size();
+  chunks[1].data[0].validity = vw1.data();
+  chunks[2].count = 100;
+  chunks[2].data.resize(1);
+  chunks[2].data[0].key_type = kt;
+  chunks[2].data[0].type = rpt::VectorType::CONSTANT;
+  chunks[2].data[0].data = &cval;
+  chunks[2].data[0].validity = &cvalid;
+  const bool integer = !std::is_floating_point<T>::value;
+  if (integer) {  // a SEQUENCE chunk whose values wrap at the column's width
+    rpt::DataChunk q;
+    q.count = 300;
+    q.data.resize(1);
+    q.data[0].key_type = kt;
+    q.data[0].type = rpt::VectorType::SEQUENCE;
+    q.data[0].seq_start = -150;
+    q.data[0].seq_increment = 97;
+    chunks.push_back(q);
+  }
+  // the same rows flattened by hand: device values + validity
+  std::vector<uint64_t> dv;
+  std::vector<bool> ok;
+  std::vector<T> orig;
+  for (size_t i = 0; i < 2048; i++) { dv.push_back(expect_device(vals[i])); ok.push_back(valid[i]); orig.push_back(vals[i]); }
+  for (size_t i = 0; i < n - 2048; i++) {
+    dv.push_back(expect_device(dict[dsel[i]]));
+    ok.push_back(dvalid[dsel[i]]);
+    orig.push_back(dict[dsel[i]]);
+  }
+  for (size_t i = 0; i < 100; i++) { dv.push_back(expect_device(cval)); ok.push_back(true); orig.push_back(cval); }
+  if (integer)
+    for (size_t i = 0; i < 300; i++) {
+      const T x = static_cast<T>(static_cast<uint64_t>(-150) + 97ULL * i);
+      dv.push_back(expect_device(x));
+      ok.push_back(true);
+      orig.push_back(x);
+    }
+  const size_t total = dv.size();
+  const std::vector<uint64_t> vwall = pack(ok, 0, total);
+  rpt::PTBloomFilter f;
+  f.Initialize(dev, static_cast<uint32_t>(total));
+  const int lnb = f.LogNumBlocks();
+  std::vector<uint64_t> w(1ULL << lnb, 0);
+  std::vector<int64_t> d64(total);
+  std::vector<int32_t> d32(total);
+  for (size_t i = 0; i < total; i++) {
+    d64[i] = static_cast<int64_t>(dv[i]);
+    d32[i] = static_cast<int32_t>(static_cast<uint32_t>(dv[i]));
+  }
+  if (dev64) rpt_oracle_insert_i64(w.data(), lnb, d64.data(), nullptr, vwall.data(), total);
+  else rpt_oracle_insert_i32(w.data(), lnb, d32.data(), nullptr, vwall.data(), total);
+  rpt::DeviceContext ctx(dev);
+  std::vector<const rpt::DataChunk*> ptrs;
+  for (const auto& c : chunks) ptrs.push_back(&c);
+  f.InsertBatch(ctx, ptrs, {0});
+  EXPECT(f.ExportWords() == w, "%s: filter words differ from the oracle", name);
+  // LookupSel of every chunk == the oracle's probe of the device values
+  size_t base = 0;
+  std::vector<uint32_t> exp(total);
+  for (const auto& c : chunks) {
+    rpt::SelectionVector sel;
+    f.LookupSel(ctx, c, sel, {0});
+    const std::vector<uint64_t> vwc = pack(ok, base, c.count);
+    const uint64_t ne = dev64 ? rpt_oracle_probe_i64(w.data(), lnb, d64.data() + base, nullptr, vwc.data(), c.count, exp.data())
+                              : rpt_oracle_probe_i32(w.data(), lnb, d32.data() + base, nullptr, vwc.data(), c.count, exp.data());
+    EXPECT(sel == std::vector<uint32_t>(exp.begin(), exp.begin() + ne), "%s: LookupSel chunk at row %zu", name, base);
+    base += c.count;
+  }
+  // min/max: exact for the integer types up to 32 bits, absent for U64 / F32 / F64
+  int64_t mn = 0, mx = 0;
+  const bool has = f.MinMax(mn, mx);
+  if (minmax_kept) {
+    int64_t emn = INT64_MAX, emx = INT64_MIN;
+    for (size_t i = 0; i < total; i++)
+      if (ok[i]) {
+        emn = std::min<int64_t>(emn, static_cast<int64_t>(orig[i]));
+        emx = std::max<int64_t>(emx, static_cast<int64_t>(orig[i]));
+      }
+    EXPECT(has && mn == emn && mx == emx, "%s: min/max %lld %lld, expected %lld %lld", name, (long long)mn, (long long)mx,
+           (long long)emn, (long long)emx);
+  } else {
+    EXPECT(!has, "%s: min/max must not be reported", name);
+  }
+  // CREATE_BF over the same chunks: the same filter words; the source re-emits the original values
+  rpt::CreateBF cb(dev, total, {0});
+  auto l = cb.MakeLocalState();
+  for (const auto& c : chunks) cb.Sink(*l, c);
+  cb.Combine(*l);
+  cb.Finalize();
+  EXPECT(cb.GetBloomFilter(0)->ExportWords() == w, "%s: CREATE_BF filter words differ", name);
+  EXPECT(cb.MinMax(0, mn, mx) == minmax_kept, "%s: CREATE_BF min/max presence", name);
+  auto gs = cb.GetGlobalSourceState(1);
+  rpt::CreateBF::LocalSourceState ls;
+  rpt::DataChunk out;
+  size_t r = 0;
+  bool same = true;
+  while (cb.GetData(*gs, ls, out)) {
+    const T* p = static_cast<const T*>(out.data[0].data);
+    for (size_t i = 0; i < out.count; i++, r++)
+      if (ok[r] && std::memcmp(&p[i], &orig[r], sizeof(T)) != 0) same = false;
+  }
+  EXPECT(same && r == total, "%s: CREATE_BF source re-emits the original values", name);
+}
+
+static void typed_keys(int dev) {
+  std::mt19937_64 rng(77);
+  const size_t n = 5000;
+  auto gen = [&](auto zero) {
+    using T = decltype(zero);
+    std::vector<T> v(n);
+    for (auto& x : v) x = static_cast<T>(rng());
+    return v;
+  };
+  typed_keys_case(dev, rpt::KeyType::I8, gen(int8_t{}), true, "TINYINT");
+  typed_keys_case(dev, rpt::KeyType::I16, gen(int16_t{}), true, "SMALLINT");
+  typed_keys_case(dev, rpt::KeyType::U8, gen(uint8_t{}), true, "UTINYINT");
+  typed_keys_case(dev, rpt::KeyType::U16, gen(uint16_t{}), true, "USMALLINT");
+  typed_keys_case(dev, rpt::KeyType::U32, gen(uint32_t{}), true, "UINTEGER");  // values >= 2^31 included
+  typed_keys_case(dev, rpt::KeyType::U64, gen(uint64_t{}), false, "UBIGINT");
+  std::vector<float> fv(n);
+  std::vector<double> dv(n);
+  for (size_t i = 0; i < n; i++) {
+    fv[i] = static_cast<float>(static_cast<int64_t>(rng() % 2000001) - 1000000) / 7.0f;
+    dv[i] = static_cast<double>(static_cast<int64_t>(rng() % 2000001) - 1000000) / 7.0;
+  }
+  uint32_t fnan = 0x7FC01234u;  // a NaN with a payload, and its sign-flipped twin
+  uint64_t dnan = 0xFFF0000000000042ULL;
+  std::memcpy(&fv[10], &fnan, 4);
+  fnan ^= 0x80000000u;
+  std::memcpy(&fv[11], &fnan, 4);
+  std::memcpy(&dv[10], &dnan, 8);
+  fv[12] = -0.0f;
+  dv[12] = -0.0;
+  fv[13] = std::numeric_limits<float>::infinity();
+  dv[13] = -std::numeric_limits<double>::infinity();
+  typed_keys_case(dev, rpt::KeyType::F32, fv, false, "FLOAT");
+  typed_keys_case(dev, rpt::KeyType::F64, dv, false, "DOUBLE");
+  // the equality transform: -0.0 finds 0.0, a NaN finds any other NaN
+  rpt::PTBloomFilter f;
+  f.Initialize(dev, 100);
+  rpt::DeviceContext ctx(dev);
+  const double ins[2] = {-0.0, std::numeric_limits<double>::quiet_NaN()};
+  uint64_t other_nan = 0x7FF0000000000001ULL;  // signalling, another payload
+  double probe[3] = {0.0, 0.0, 1.5};
+  std::memcpy(&probe[1], &other_nan, 8);
+  rpt::DataChunk a, b;
+  a.count = 2;
+  a.data.resize(1);
+  a.data[0].key_type = rpt::KeyType::F64;
+  a.data[0].data = ins;
+  b = a;
+  b.count = 3;
+  b.data[0].data = probe;
+  f.Insert(ctx, a, {0});
+  rpt::SelectionVector sel;
+  f.LookupSel(ctx, b, sel, {0});
+  EXPECT(sel.size() >= 2 && sel[0] == 0 && sel[1] == 1, "DOUBLE: -0.0 / NaN equality transform");
 }
 
 int main() {
@@ -596,6 +818,7 @@ int main() {
         EXPECT(sels[k] == std::vector<uint32_t>(exp.begin(), exp.begin() + ne), "bucketed probe chunk %zu", k);
       }
     }
+    typed_keys(dev);
   } catch (const std::exception& e) {
     fprintf(stderr, "exception: %s\n", e.what());
     return 2;
