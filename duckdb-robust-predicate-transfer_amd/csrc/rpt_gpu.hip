@@ -556,19 +556,17 @@ size_t insert_workspace_layout(uint64_t n, int log_num_blocks, int strategy, voi
   return total;
 }
 
-constexpr uint64_t kPartitionedInsertMinRows = 1ULL << 20;
-
-// AUTO insert, from the measured crossovers (profiles/r01/strategy_crossover.jsonl): memory-side
-// atomics cost ~37 ps/key at any filter size; the partitioned insert ~4-9 ps/key plus ~40 us (it
-// overtakes from ~1 Mi rows; ~4 Mi for single-slice filters, whose partition pass funnels every row
-// into one LDS counter); the bucketed insert ~9 ps/key plus a pass over the whole filter (~2 ms per
-// 8 GiB), so from ~blocks/16 rows.
+// AUTO insert, from the measured crossovers (profiles/r03/strategy_crossover_insert.jsonl): memory-side
+// atomics cost ~40 ps/key at any filter size; the partitioned insert ~4-9 ps/key plus ~40-80 us, so it
+// overtakes between 1 and 2 Mi rows (2-4 Mi above 128 slices, where it partitions 32 Ki-row tiles: at 2 Mi
+// rows into 128 MiB, 0.103 vs 0.088 ms atomic); the bucketed insert ~9 ps/key plus a pass over the whole
+// filter (~2 ms per 8 GiB), so from ~blocks/16 rows.
+uint64_t partitioned_insert_min_rows(int L) { return L > rpt::kSliceLog + 7 ? (1ULL << 22) : (1ULL << 21); }
 int resolve_insert_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_INSERT_AUTO) return requested;
   const int L = log_num_blocks;
   if (strategy_supported(RPT_PROBE_PARTITIONED, L))
-    return n >= (L <= rpt::kSliceLog + 1 ? (1ULL << 22) : kPartitionedInsertMinRows) ? RPT_INSERT_PARTITIONED
-                                                                                     : RPT_INSERT_ATOMIC;
+    return n >= partitioned_insert_min_rows(L) ? RPT_INSERT_PARTITIONED : RPT_INSERT_ATOMIC;
   if (strategy_supported(RPT_PROBE_BUCKETED, L) && n >= std::max<uint64_t>((1ULL << L) >> 4, 1ULL << 23))
     return RPT_INSERT_BUCKETED;
   return RPT_INSERT_ATOMIC;

@@ -119,6 +119,12 @@ def test_auto_routes_large_filters(rpt):
     assert mid19.probe_strategy_for(1 << 22) == PARTITIONED and mid19.probe_strategy_for(1 << 21) == GATHER
     mid = rpt.BloomFilter(log_num_blocks=21)  # 16 MiB (C2): routed from 4 Mi rows
     assert mid.probe_strategy_for(1 << 22) == PARTITIONED and mid.probe_strategy_for(1 << 21) == GATHER
+    # partitioned inserts from 2 Mi rows, 4 Mi above 128 slices (profiles/r03/strategy_crossover_insert.jsonl)
+    assert mid.insert_strategy_for(1 << 21) == INS_PARTITIONED and mid.insert_strategy_for(1 << 20) == INS_ATOMIC
+    assert tiny.insert_strategy_for(1 << 21) == INS_PARTITIONED and tiny.insert_strategy_for((1 << 21) - 1) == INS_ATOMIC
+    big = rpt.BloomFilter(log_num_blocks=24)  # 128 MiB, 1024 slices
+    assert big.insert_strategy_for(1 << 22) == INS_PARTITIONED and big.insert_strategy_for(1 << 21) == INS_ATOMIC
+    big.close()
     n_build = 5_000_000
     build = keys_of(np.int64, n_build, 11)
     bf.insert(dev(build))  # AUTO: atomic at this batch size

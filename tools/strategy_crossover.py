@@ -46,8 +46,9 @@ def insert_sweep():
     keys = rpt_amd.synth_build_keys(1 << 27)
     for L in (12, 14, 16, 18, 21, 24, 27):
         bf = rpt_amd.BloomFilter(log_num_blocks=L)
-        for lg in (16, 20, 22, 24, 26):
+        for lg in (16, 20, 21, 22, 24, 26):
             n = 1 << lg
+            lib.rpt_bf_set_insert_strategy(bf._h, 0)  # time_insert pins a strategy: AUTO's choice first
             row = {"op": "insert", "log_blocks": L, "n": n, "auto": bf.insert_strategy_for(n)}
             for name, st in (("atomic", 1), ("partitioned", 2), ("bucketed", 3)):
                 if (st == 2 and not lib.rpt_probe_strategy_supported(3, L)) or (st == 3 and not lib.rpt_probe_strategy_supported(4, L)):
@@ -88,7 +89,7 @@ def main():
         return mid_sweep()
     lib = rpt_amd.load()
     n_max = 1 << 28
-    for build in (10**5, 10**7, 10**8, 10**9):
+    for build in (10**5, 10**7, 3 * 10**7, 10**8, 10**9):
         bf = rpt_amd.BloomFilter(build)
         bf.insert(rpt_amd.synth_build_keys(min(build, 10**8)))
         L = bf.log_num_blocks
