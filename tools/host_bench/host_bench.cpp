@@ -11,10 +11,21 @@
 #include <thread>
 #include <vector>
 
+#include <cstdlib>
+#include <cstring>
+
+#include <hip/hip_runtime_api.h>
+
 #include "rpt_host.hpp"
 
-int main() {
+int main(int argc, char** argv) {
   const int dev = 0;
+  // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
+  // synchronize waits for the device (per-vector call latency experiment)
+  if (argc > 1 && std::strcmp(argv[1], "--spin") == 0) {
+    if (hipSetDevice(dev) != hipSuccess || hipSetDeviceFlags(hipDeviceScheduleSpin) != hipSuccess) return 3;
+    printf("{\"op\": \"config\", \"device_flags\": \"hipDeviceScheduleSpin\"}\n");
+  }
   const size_t n_build = 10000000, n_probe = 1ULL << 25;  // 33.5M probe rows = 16384 chunks
   std::mt19937_64 rng(42);
   std::vector<int64_t> build(n_build), probe(n_probe);
