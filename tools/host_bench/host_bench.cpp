@@ -78,7 +78,7 @@ int main(int argc, char** argv) {
     uint64_t pipeline_rows;  // ~0: one staged copy per call (no pipeline)
     unsigned threads = 8;    // flatten threads
   };
-  std::vector<Case> cases = {{1, ~0ULL}, {16, ~0ULL}, {128, ~0ULL}, {1024, ~0ULL}, {8192, ~0ULL}, {16384, ~0ULL}};
+  std::vector<Case> cases = {{1, ~0ULL}, {8, ~0ULL}, {16, ~0ULL}, {128, ~0ULL}, {1024, ~0ULL}, {8192, ~0ULL}, {16384, ~0ULL}};
   for (size_t per_call : {8192, 16384})
     for (uint64_t pr : {uint64_t(1) << 20, uint64_t(1) << 21, uint64_t(1) << 22}) cases.push_back({per_call, pr});
   for (unsigned th : {4u, 12u, 16u}) cases.push_back({16384, uint64_t(1) << 22, th});
