@@ -183,15 +183,26 @@ __global__ __launch_bounds__(kSmallThreads) void probe_small_kernel(const uint64
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t n_segs = static_cast<uint32_t>((n + kSegRows - 1) / kSegRows);
-  for (uint32_t seg = wave; seg < n_segs; seg += kWaves) {
-    uint64_t h[8];
-    bool ok[8], pass[8];
-    load_hashes<K, DENSE>(a, static_cast<uint64_t>(seg) * kSegRows, n, lane, h, ok);
+  // a wave's segments (<= kSegs / kWaves) are all loaded before any is probed: the keys usually sit in
+  // device-mapped host memory, one PCIe round trip per dependent load
+  constexpr uint32_t kPerWave = kSegs / kWaves;
+  uint64_t h[kPerWave][8];
+  bool ok[kPerWave][8];
+#pragma unroll
+  for (uint32_t i = 0; i < kPerWave; i++) {
+    const uint32_t seg = wave + i * kWaves;
+    if (seg < n_segs) load_hashes<K, DENSE>(a, static_cast<uint64_t>(seg) * kSegRows, n, lane, h[i], ok[i]);
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < kPerWave; i++) {
+    const uint32_t seg = wave + i * kWaves;
+    if (seg >= n_segs) break;
+    bool pass[8];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
-      const uint64_t m = mask_of(s_masks, h[j]);
-      const uint64_t w = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
-      pass[j] = ok[j] && (w & m) == m;
+      const uint64_t m = mask_of(s_masks, h[i][j]);
+      const uint64_t w = ok[i][j] ? words[block_of(h[i][j], block_mask)] : 0ULL;
+      pass[j] = ok[i][j] && (w & m) == m;
     }
     store_segment_bits<K, DENSE>(pass, lane, seg, s_words, s_cnt);
   }
