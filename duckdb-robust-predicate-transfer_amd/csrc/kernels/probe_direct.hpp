@@ -145,11 +145,10 @@ constexpr int kSmallThreads = 1024;
 constexpr uint64_t kSmallRows = RPT_SMALL_PROBE_ROWS;
 // The small kernels' tail: segment counts (<= 32) -> the ascending selection vector. Every wave scans the
 // counts itself (lane i holds segment i's) and expands its own segments' row-ordered result words.
-template <int THREADS = kSmallThreads>
 __device__ __forceinline__ void small_sel_tail(const uint64_t* s_words, const uint32_t* s_cnt, uint32_t n_segs,
                                                const uint32_t* __restrict__ row_sel, uint32_t* __restrict__ out_sel,
                                                uint64_t* __restrict__ out_count) {
-  constexpr uint32_t kWaves = THREADS / 64;
+  constexpr uint32_t kWaves = kSmallThreads / 64;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t c = lane < n_segs ? s_cnt[lane] : 0u;
   const uint32_t incl = wave_inclusive_sum(c);
@@ -209,54 +208,6 @@ __global__ __launch_bounds__(kSmallThreads) void probe_small_kernel(const uint64
   }
   __syncthreads();
   small_sel_tail(s_words, s_cnt, n_segs, row_sel, out_sel, out_count);
-}
-
-// The same small probe spread over several workgroups (one 512-row segment per wave, so up to 8 CUs for
-// 8 vectors): a lone workgroup's key loads from device-mapped host memory queue behind one CU's
-// outstanding-miss limit (8 vectors 50 us vs 19-21 us for one). Each wave stores its segment's pass words
-// and count into the caller's workspace; the last workgroup to arrive (a ticket the host zeroes before
-// the launch) expands them into the ascending sel. Device-scope fences order the words across the
-// XCDs' L2s (release before the ticket, acquire after it). n <= kSmallRows.
-constexpr int kSmallMwThreads = 256;
-constexpr uint32_t kSmallMwSegsPerGroup = kSmallMwThreads / 64;
-struct SmallMwScratch {
-  uint64_t words[kSmallRows / kSegRows * kWordsPerSeg];
-  uint32_t cnt[kSmallRows / kSegRows];
-  uint32_t ticket;
-};
-template <int K, bool DENSE>
-__global__ __launch_bounds__(kSmallMwThreads) void probe_small_mw_kernel(const uint64_t* __restrict__ words,
-                                                                         uint64_t block_mask, KeyArgs a, uint64_t n,
-                                                                         const uint32_t* __restrict__ row_sel,
-                                                                         uint32_t* __restrict__ out_sel,
-                                                                         uint64_t* __restrict__ out_count,
-                                                                         SmallMwScratch* __restrict__ ws) {
-  __shared__ uint64_t s_masks[kNumMasks];
-  __shared__ uint32_t s_last;
-  fill_mask_table(s_masks);
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t n_segs = static_cast<uint32_t>((n + kSegRows - 1) / kSegRows);
-  const uint32_t seg = blockIdx.x * kSmallMwSegsPerGroup + wave;
-  if (seg < n_segs) {
-    uint64_t h[8];
-    bool ok[8], pass[8];
-    load_hashes<K, DENSE>(a, static_cast<uint64_t>(seg) * kSegRows, n, lane, h, ok);
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-      const uint64_t m = mask_of(s_masks, h[j]);
-      const uint64_t w = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
-      pass[j] = ok[j] && (w & m) == m;
-    }
-    store_segment_bits<K, DENSE>(pass, lane, seg, ws->words, ws->cnt);
-  }
-  __threadfence();  // release this workgroup's words and counts at device scope
-  __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&ws->ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
-  __syncthreads();
-  if (s_last == 0) return;
-  __threadfence();  // acquire the other workgroups' words
-  small_sel_tail<kSmallMwThreads>(ws->words, ws->cnt, n_segs, row_sel, out_sel, out_count);
 }
 
 // ---- USE_BF's filter chain in one launch -----------------------------------------------------------

@@ -55,10 +55,6 @@
 #define RPT_L1_FIXED_PCT 0
 #endif
 
-#ifndef RPT_SMALL_MW_MIN_ROWS
-#define RPT_SMALL_MW_MIN_ROWS 2049  // fused small probes of this many rows and more spread over several workgroups
-#endif
-
 // The product build runs the tuning macros at the defaults the GPU suite tests. Other values exist for
 // A/B timing only (tools/build_variants.sh builds them under other names, without RPT_PRODUCT_BUILD);
 // several were never run through the parity suite (tuning macros).
@@ -66,7 +62,7 @@
 static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG == 8 && RPT_L1_TILE_ROWS == 16384 &&
                   RPT_L1_FIXED_PCT == 0 && RPT_BUCKET_UNPERMUTE_THREADS == 256 && RPT_SLICE_UNROLL == 4 &&
                   RPT_PARTITION_MIN_WAVES == 8 && RPT_PROBE_PREFETCH == 2 && RPT_SEL_BALLOT_MIN == 192 &&
-                  RPT_COMPACT_BALLOT_MIN == 384 && RPT_SMALL_MW_MIN_ROWS == 2049,
+                  RPT_COMPACT_BALLOT_MIN == 384,
               "product build: tuning macros must keep their tested defaults (use tools/build_variants.sh)");
 static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
                   RPT_NT_REC_LOADS == 0 && RPT_NT_SLICE_LOADS == 1 && RPT_PARK_LANE_MAJOR == 1 && RPT_SLICE_XCD_MAP == 1 &&
@@ -611,17 +607,6 @@ void launch_probe_small_t(hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a
                      (1ULL << bf->log_num_blocks) - 1, a, n, row_sel, out_sel, out_count);
   prof.end();
 }
-template <int K, bool D>
-void launch_probe_small_mw_t(hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
-                             const uint32_t* row_sel, uint32_t* out_sel, uint64_t* out_count,
-                             rpt::SmallMwScratch* ws) {
-  const uint32_t n_segs = static_cast<uint32_t>((n + rpt::kSegRows - 1) / rpt::kSegRows);
-  const uint32_t groups = (n_segs + rpt::kSmallMwSegsPerGroup - 1) / rpt::kSmallMwSegsPerGroup;
-  ProfScope prof(inst_name<K, D>("probe_small_mw_kernel"), s);
-  hipLaunchKernelGGL((rpt::probe_small_mw_kernel<K, D>), dim3(groups), dim3(rpt::kSmallMwThreads), 0, s, bf->words,
-                     (1ULL << bf->log_num_blocks) - 1, a, n, row_sel, out_sel, out_count, ws);
-  prof.end();
-}
 
 // Whole filter in LDS (dynamic LDS = filter bytes), 1024-thread workgroups (16 waves): as many per CU as
 // LDS allows. Measured against 256-thread workgroups: 16 KiB 1.79 -> 1.67 ms, 64 KiB 2.07 -> 1.73 ms per
@@ -921,15 +906,11 @@ int rpt_bf_needs_resize_alloc(const rpt_bf* bf, uint64_t actual_rows) {
   return actual_rows > (64ULL << bf->log_num_blocks) / 8 ? 1 : 0;
 }
 
-constexpr size_t kSmallMwScratchBytes = (sizeof(rpt::SmallMwScratch) + 255) & ~size_t{255};
-
 size_t rpt_probe_workspace_bytes(uint64_t n_rows, int log_num_blocks) {
   // enough for any strategy the filter may run
   size_t m = 0;
   for (int st : {RPT_PROBE_GATHER, RPT_PROBE_LDS, RPT_PROBE_PARTITIONED, RPT_PROBE_BUCKETED})
     if (strategy_supported(st, log_num_blocks)) m = std::max(m, workspace_layout(n_rows, log_num_blocks, st, nullptr, nullptr));
-  // the fused small probe's scratch (kept for every n, so the size never shrinks as n grows)
-  if (n_rows > 0) m = std::max(m, kSmallMwScratchBytes);
   return m;
 }
 
@@ -941,8 +922,7 @@ int rpt_bf_probe_strategy_for(const rpt_bf* bf, uint64_t n_rows) {
 size_t rpt_bf_probe_workspace_bytes(const rpt_bf* bf, uint64_t n_rows) {
   if (!bf) return 0;
   const int st = resolve_strategy(bf->probe_strategy.load(), bf->log_num_blocks, n_rows);
-  const size_t m = workspace_layout(n_rows, bf->log_num_blocks, st, nullptr, nullptr);
-  return n_rows > 0 ? std::max(m, kSmallMwScratchBytes) : m;
+  return workspace_layout(n_rows, bf->log_num_blocks, st, nullptr, nullptr);
 }
 
 int rpt_probe_strategy_supported(int strategy, int log_num_blocks) {
@@ -1452,22 +1432,13 @@ int rpt_bf_probe(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* ro
   if (!bf || !out_count_dev) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
   RPT_ON_DEVICE(bf->device);
   if (rpt_bf_probe_is_fused(bf, n) == 1) {
-    // small batch: one fused launch (several workgroups when the caller workspace holds their scratch)
+    // small batch: one fused launch, no workspace
     int st = check_col(col);
     if (st != RPT_OK) return st;
     if (!out_sel) return fail(RPT_ERR_INVALID_ARGUMENT, "null out_sel");
     hipStream_t s = as_stream(stream);
     RPT_SETTLE(bf, s);
     const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, row_sel};
-    if (n >= RPT_SMALL_MW_MIN_ROWS && workspace && workspace_bytes >= sizeof(rpt::SmallMwScratch) &&
-        reinterpret_cast<uintptr_t>(workspace) % alignof(rpt::SmallMwScratch) == 0) {
-      auto* ws = static_cast<rpt::SmallMwScratch*>(workspace);
-      RPT_HIP(hipMemsetAsync(&ws->ticket, 0, sizeof ws->ticket, s));
-      RPT_DISPATCH_KD(launch_probe_small_mw_t, col->key_type, dense_ok(col, row_sel), s, bf, a, n, row_sel, out_sel,
-                      out_count_dev, ws);
-      RPT_LAUNCHED("probe_small_mw_kernel");
-      return RPT_OK;
-    }
     RPT_DISPATCH_KD(launch_probe_small_t, col->key_type, dense_ok(col, row_sel), s, bf, a, n, row_sel, out_sel,
                     out_count_dev);
     RPT_LAUNCHED("probe_small_kernel");

@@ -1,5 +1,8 @@
 """Fused small-probe latency: one workgroup vs several (probe_small_kernel vs probe_small_mw_kernel).
 
+The several-workgroup kernel was measured in commit 8980ddc and rejected (DESIGN §5 rejected list);
+at later commits both modes run the one-workgroup kernel.
+
 Keys in device memory and in pinned host memory (device-mapped, what the DuckDB host mirror passes).
 Per n: the synchronized per-call latency (probe + count read back, what a USE_BF vector waits for)
 for AUTO with the filter's workspace (several workgroups from RPT_SMALL_MW_MIN_ROWS rows) and with an
@@ -54,9 +57,20 @@ def main():
                 assert c == ref
                 out[mode] = round(dt, 1)
                 out[mode + "_count"] = c
+            # the same calls queued back to back (no host round trip between them): kernel durations
+            # under the tracer without the GPU idling between calls
+            for mode, ws in (("multi", big), ("one", tiny)):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(calls):
+                    probe(bf, keys, n, sel, cnt, ws)
+                torch.cuda.synchronize()
+                out[mode + "_queued"] = round((time.perf_counter() - t0) / calls * 1e6, 1)
             assert out["multi_count"] == out["one_count"]
             print(json.dumps({"op": "small_probe", "n": n, "keys": where, "us_per_call_multi": out["multi"],
-                              "us_per_call_one": out["one"], "survivors": out["one_count"]}), flush=True)
+                              "us_per_call_one": out["one"],
+                              "us_per_call_queued_multi": out["multi_queued"], "us_per_call_queued_one": out["one_queued"],
+                              "survivors": out["one_count"]}), flush=True)
 
 
 if __name__ == "__main__":
