@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "rpt_bloom_device.hpp"
@@ -76,16 +77,19 @@ __global__ __launch_bounds__(rpt::kSmallThreads) void phases_kernel(const uint64
   if (dep == 0x12345 && dep2 == 7) sink[threadIdx.x] = dep;  // keeps the dependences live
 }
 
-int main() {
+int main(int argc, char** argv) {
   const int log_nb = 17;  // 1 MiB filter, the size a 1 Mi-key build gets
   const uint64_t n_words = 1ULL << log_nb;
   std::vector<uint64_t> hw(n_words);
   uint64_t x = 88172645463325252ULL;
   for (auto& w : hw) {
     x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-    w = x & (x >> 3);  // ~25 % bits set
+    w = x & (x >> 3);  // ~25 % bits set: almost no row passes
   }
-  const uint64_t n = 512;
+  const double pass_frac = argc > 2 ? atof(argv[2]) : 0.0;  // > 0: that fraction of blocks all ones
+  if (pass_frac > 0)
+    for (uint64_t i = 0; i < n_words; i++) if ((i * 2654435761ULL % 1000) < pass_frac * 1000) hw[i] = ~0ULL;
+  const uint64_t n = argc > 1 ? std::min<uint64_t>(std::max(atoll(argv[1]), 1LL), 512) : 512;  // one segment
   std::vector<int64_t> keys(n);
   for (auto& k : keys) { x ^= x << 13; x ^= x >> 7; x ^= x << 17; k = static_cast<int64_t>(x >> 20); }
   uint64_t *d_words, *d_count, *d_stamps, *d_sink;
@@ -127,8 +131,10 @@ int main() {
     }
     auto med = [](std::vector<double> v) { std::sort(v.begin(), v.end()); return v[v.size() / 2]; };
     std::vector<double> ev(ev_us.begin(), ev_us.end());
-    printf("%s launches (n = %llu rows, median us): event-timed %.2f, in-kernel total %.2f\n", mode ? "queued" : "synchronized",
-           (unsigned long long)n, med(ev), med(d[0]));
+    uint64_t cnt = 0;
+    CHECK(hipMemcpy(&cnt, d_count, 8, hipMemcpyDeviceToHost));
+    printf("%s launches (n = %llu rows, %llu pass, median us): event-timed %.2f, in-kernel total %.2f\n",
+           mode ? "queued" : "synchronized", (unsigned long long)n, (unsigned long long)cnt, med(ev), med(d[0]));
     for (int p = 1; p < kPhases; p++) printf("  %-26s %.2f\n", names[p - 1], med(d[p]));
   }
   return 0;
