@@ -23,6 +23,11 @@ collective in the probe). A communicator that cannot be built ends the run with 
 every rank. RPT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (the merge then runs the
 torch.distributed composition over host memory, reported as torch_merge_ms).
 
+At N > 1 (and with --c5-merge at N = 1) the line also carries `c5_merge`: the north_star's C5 pipeline at
+this node's N, after the headline is timed: every rank inserts its 1e9-row shard into an 8 GiB filter sized
+for 8e9 rows, rpt_bf_allreduce_or_ws OR-merges the partials over RCCL (xGMI), the merged filter is checked
+bit-identical to a single build of all N * 1e9 rows, and every rank probes its 1e9-row slice against it.
+
 Prints ONE JSON line on rank 0. `roofline` prices the dominant kernel from HIP events the library
 records on the launch stream (rpt_profiling_*) and its PMC traffic from profiles/pmc/<config>.json
 (the exact template instantiation, or null); `cpu_baseline` times the C++ restatement (oracle/) on
@@ -45,6 +50,9 @@ sys.path.insert(0, os.path.join(REPO, "duckdb-robust-predicate-transfer_amd"))
 HBM_PEAK_BPS = 8.0e12  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 KEY_BYTES = 8           # int64 key read per probed row (algorithmic)
 SEL_BYTES = 4           # uint32 sel entry written per survivor (algorithmic)
+
+C5_FILTER_ROWS = 8 * 10**9  # BASELINE config 4: the filter of 8e9 rows (2^30 blocks = 8 GiB)
+C5_ROWS_PER_RANK = 10**9
 
 CONFIGS = {  # name -> (global build rows at N GPUs, filter sized for, description)
     "C2": (lambda n: 10**7, lambda n: 10**7),
@@ -94,6 +102,15 @@ def parse():
                     help="key column type (i32: the synthetic keys truncated to int32, as JOB's INTEGER keys)")
     ap.add_argument("--strategy", default="auto", choices=["auto", "gather", "lds", "partitioned", "bucketed"],
                     help="probe strategy (auto picks by filter and batch size)")
+    ap.add_argument("--c5-merge", action="store_true",
+                    help="run the C5 build + RCCL merge + probe section at N = 1 too (a one-rank communicator; "
+                         "at N > 1 it runs by default)")
+    ap.add_argument("--no-c5-merge", action="store_true", help="N > 1: skip the C5 build + merge + probe section")
+    ap.add_argument("--c5-rows-per-rank", type=float, default=C5_ROWS_PER_RANK,
+                    help="C5 section: build and probe rows per rank (the filter stays sized for 8e9 rows)")
+    ap.add_argument("--c5-merge-reps", type=int, default=3, help="C5 section: timed merges (after one warm-up)")
+    ap.add_argument("--collective-timeout-ms", type=int, default=None,
+                    help="bound of every OR all-reduce's waits (rpt_collective_set_timeout_ms; default the library's)")
     return ap.parse_args()
 
 
@@ -114,6 +131,105 @@ def algorithmic_bytes(kernel: str, n: int, survivors: int, key_bytes: int = KEY_
     if kernel.startswith("partition_kernel<") and kernel[len("partition_kernel<"):].split(",")[0] in ("0", "1", "2"):
         return key_bytes * n
     return 0
+
+
+def c5_merge_record(world: int, filter_bytes: int, rows_per_rank: int, insert_ms: float, merge_ms: list,
+                    probe_ms: float, survivors: int, merge_check: str, timeout_ms: int) -> dict:
+    """The `c5_merge` object of the bench line (times are the max over ranks). The merge moves 2 (W-1)/W of
+    the filter per GPU, 2 S / W over each of its W-1 point-to-point xGMI links."""
+    t = statistics.median(merge_ms) if merge_ms else None
+    return {
+        "what": ("BASELINE config 4 (C5) at this node's N: every rank inserts its shard of the N x rows_per_rank "
+                 "build column into a filter sized for 8e9 rows, rpt_bf_allreduce_or_ws OR-merges the partials "
+                 "over RCCL, every rank probes its rows_per_rank-row slice against the merged filter"),
+        "n_gpus": world,
+        "filter_bytes": filter_bytes,
+        "rows_per_rank": rows_per_rank,
+        "build_rows": world * rows_per_rank,
+        "insert_ms": insert_ms,
+        "or_merge_ms": t * 1e3 if t else None,
+        "or_merge_ms_reps": [m * 1e3 for m in merge_ms],
+        "or_merge_GBps_per_gpu": 2 * (world - 1) / world * filter_bytes / t / 1e9 if t and world > 1 else None,
+        "or_merge_GBps_per_link": 2 / world * filter_bytes / t / 1e9 if t and world > 1 else None,
+        "probe_ms": probe_ms,
+        "probe_keys_per_s_node": world * rows_per_rank / (probe_ms * 1e-3) if probe_ms else None,
+        "survivors_rank0": survivors,
+        "merge_check": merge_check,
+        "collective_timeout_ms": timeout_ms,
+    }
+
+
+def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max, all_ok) -> dict:
+    """C5 build + product merge + probe (see the module docstring). Collective: every rank runs it."""
+    import torch
+
+    import rpt_amd
+    from rpt_amd.distributed import allreduce_or_native, allreduce_workspace
+
+    rows = int(args.c5_rows_per_rank)
+    bf = rpt_amd.BloomFilter(C5_FILTER_ROWS, device=device)
+    keys = rpt_amd.synth_build_keys(rows, start=rank * rows, device=device)
+    bf.insert(keys)  # warm-up (workspace, code objects)
+    torch.cuda.synchronize()
+    bf.clear()
+    barrier()
+    t0 = time.perf_counter()
+    bf.insert(keys)
+    torch.cuda.synchronize()
+    insert_s = time.perf_counter() - t0
+    ws = allreduce_workspace(bf, comm)
+    allreduce_or_native(bf, comm, workspace=ws)  # warm-up merge: OR is idempotent, the words do not change
+    merge_s = []
+    for _ in range(args.c5_merge_reps):
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        allreduce_or_native(bf, comm, workspace=ws)
+        torch.cuda.synchronize()
+        merge_s.append(time.perf_counter() - t0)
+    del ws
+    # untimed: the merged filter against a single build of all world * rows rows (inserted piece by piece)
+    ref = rpt_amd.BloomFilter(C5_FILTER_ROWS, device=device)
+    for r in range(world):
+        rpt_amd.synth_build_keys(rows, start=r * rows, device=device, out=keys)
+        ref.insert(keys)
+    del keys
+    a = torch.empty(bf.num_blocks, dtype=torch.int64, device=device)
+    b = torch.empty_like(a)
+    bf.copy_words_to(a)
+    ref.copy_words_to(b)
+    same = bool(torch.equal(a, b)) and bf.minmax() == ref.minmax() and not bf.is_empty()
+    del a, b, ref
+    torch.cuda.empty_cache()
+    ok = all_ok(same)
+    check = ("bit-identical (words + key min/max) to a single-GPU build of all rows on every rank" if ok
+             else "MISMATCH")
+    # the node-wide probe: every rank its slice of the global probe column against the merged filter
+    n_probe = rows
+    pkeys = rpt_amd.synth_probe_keys(n_probe, world * rows, int(round(args.p * 1000)), start=rank * n_probe,
+                                     device=device)
+    out_sel = torch.empty(n_probe, dtype=torch.int32, device=device)
+    out_count = torch.zeros(1, dtype=torch.int64, device=device)
+    pws = torch.empty(bf.workspace_bytes(n_probe), dtype=torch.uint8, device=device)
+    bf.probe_async(pkeys, n=n_probe, out_sel=out_sel, out_count=out_count, workspace=pws)  # warm-up
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        bf.probe_async(pkeys, n=n_probe, out_sel=out_sel, out_count=out_count, workspace=pws)
+    torch.cuda.synchronize()
+    probe_s = (time.perf_counter() - t0) / reps
+    survivors = int(out_count.item())
+    nbytes = bf.num_blocks * 8
+    del pkeys, out_sel, pws, bf
+    torch.cuda.empty_cache()
+    insert_s, probe_s, *merge_s = reduce_max([insert_s, probe_s] + merge_s)
+    rec = c5_merge_record(world, nbytes, rows, insert_s * 1e3, merge_s, probe_s * 1e3, survivors, check,
+                          args.collective_timeout_ms or rpt_amd.load().rpt_collective_timeout_ms())
+    if not ok:
+        raise SystemExit("C5: OR-merged filter differs from the single-GPU build")
+    return rec
 
 
 def pmc_traffic(kernel: str, tag: str):
@@ -224,6 +340,9 @@ def main():
     from rpt_amd import _lib as rpt_lib
     from rpt_amd._lib import RptError
     from rpt_amd.distributed import RcclComm, allreduce_or_filter, allreduce_or_native, allreduce_workspace, shard_range
+
+    if args.collective_timeout_ms:
+        rpt_lib.check(rpt_amd.load().rpt_collective_set_timeout_ms(args.collective_timeout_ms))
 
     cfg = args.config or ("C2" if args.build_rows is None and args.filter_rows is None else None)
     n_probe = int(args.probe_rows)
@@ -362,6 +481,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, insert_s, merge_s = t.tolist()
 
+    # ---- C5 build + product merge + probe (after the headline; N > 1 by default, --c5-merge at N = 1) ----
+    c5 = None
+    if (world > 1 and comm is not None and not args.no_c5_merge) or (world == 1 and args.c5_merge):
+        del keys, out_sel, ws
+        torch.cuda.empty_cache()
+        c5_comm = comm if comm is not None else RcclComm.single(device)
+
+        def reduce_max(vals):
+            v = torch.tensor(vals, dtype=torch.float64, device=device)
+            if world > 1:
+                dist.all_reduce(v, op=dist.ReduceOp.MAX)
+            return v.tolist()
+
+        def all_ok(flag):
+            v = torch.tensor([1 if flag else 0], dtype=torch.int64, device=device)
+            if world > 1:
+                dist.all_reduce(v, op=dist.ReduceOp.MIN)
+            return bool(v.item())
+
+        c5 = run_c5_merge(args, rank, world, device, c5_comm, barrier, reduce_max, all_ok)
+        if c5_comm is not comm:
+            c5_comm.close()
+
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = world * n_probe * args.steps / elapsed
@@ -452,6 +594,8 @@ def main():
                 "merge_path": merge_path,
             },
         }
+        if c5 is not None:
+            line["c5_merge"] = c5
         if not args.no_cpu_baseline and world == 1:
             sample = int(args.cpu_sample) if args.cpu_sample else n_probe
             threads = args.cpu_threads or cpu_share()

@@ -143,6 +143,10 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
 // ascending selection vector. n <= kSmallRows.
 constexpr int kSmallThreads = 1024;
 constexpr uint64_t kSmallRows = RPT_SMALL_PROBE_ROWS;
+// Every 512-row segment is some wave's (probe_small_kernel's kPerWave = segments / waves must not round
+// down: a dropped segment would drop its rows) and small_sel_tail's one-wave scan covers every segment count.
+static_assert(kSmallRows % (kSegRows * (kSmallThreads / 64)) == 0 && kSmallRows / kSegRows <= 64,
+              "RPT_SMALL_PROBE_ROWS must be a multiple of 8192 rows, at most 32768");
 // The small kernels' tail: segment counts (<= 32) -> the ascending selection vector. Every wave scans the
 // counts itself (lane i holds segment i's) and expands its own segments' row-ordered result words.
 __device__ __forceinline__ void small_sel_tail(const uint64_t* s_words, const uint32_t* s_cnt, uint32_t n_segs,

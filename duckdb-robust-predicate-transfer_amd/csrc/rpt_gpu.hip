@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -28,6 +29,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -107,6 +109,7 @@ struct rpt_bf {
 namespace {
 
 thread_local std::string t_last_error;
+thread_local bool t_merge_stuck = false;  // the last merge on this thread aborted without draining its streams
 
 int fail(int status, const char* fmt, ...) {
   char buf[512];
@@ -252,23 +255,38 @@ hipError_t zero_pending_locked(rpt_bf* bf, hipStream_t s) {
 
 // ... and by a reader: zero the words as an ordered write on the reader's stream and record zero_ev after
 // the memset, so a reader on another stream that finds the clear already settled waits for that event
-// instead of overtaking the zeroing (no host synchronization: legal under stream capture). Reading a
-// cleared filter before any insert is rare: the fast path is two atomic loads.
+// instead of overtaking the zeroing. Reading a cleared filter before any insert is rare: the fast path is
+// two atomic loads.
+// Not inside stream capture: a captured memset would run at every replay of the graph (wiping
+// bits inserted between replays), while the flags would drop once, at capture time; and querying or waiting
+// on an event recorded outside the capture is illegal there. A capture that reads a filter with a clear
+// still pending is refused; rpt_bf_settle() before the capture settles it.
 int settle_for_read(const rpt_bf* cbf, hipStream_t s) {
   rpt_bf* bf = const_cast<rpt_bf*>(cbf);
   if (!bf->clear_pending.load() && !bf->zero_unsynced.load()) return RPT_OK;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone)
+    return fail(RPT_ERR_INVALID_ARGUMENT,
+                "read of a cleared filter inside stream capture: call rpt_bf_settle() before capturing");
   std::lock_guard<std::mutex> lk(bf->order_mu);
   if (bf->clear_pending.load()) {
-    if (bf->order_pending) RPT_HIP(hipStreamWaitEvent(s, bf->order_ev, 0));
-    RPT_HIP(hipMemsetAsync(bf->words, 0, (1ULL << bf->log_num_blocks) * 8, s));
+    // both events exist before anything is enqueued, so no early return leaves the memset unordered
     if (!bf->zero_ev) RPT_HIP(hipEventCreateWithFlags(&bf->zero_ev, hipEventDisableTiming));
     if (!bf->order_ev) RPT_HIP(hipEventCreateWithFlags(&bf->order_ev, hipEventDisableTiming));
-    RPT_HIP(hipEventRecord(bf->zero_ev, s));
-    RPT_HIP(hipEventRecord(bf->order_ev, s));  // later writes are ordered after the zeroing too
-    bf->order_pending = true;
+    if (bf->order_pending) RPT_HIP(hipStreamWaitEvent(s, bf->order_ev, 0));
+    RPT_HIP(hipMemsetAsync(bf->words, 0, (1ULL << bf->log_num_blocks) * 8, s));
     bf->pristine = true;
     bf->zero_unsynced.store(true);  // before the flag drops: a reader seeing neither may skip both
     bf->clear_pending.store(false);
+    if (hipEventRecord(bf->zero_ev, s) != hipSuccess || hipEventRecord(bf->order_ev, s) != hipSuccess) {
+      // the memset is enqueued but cannot be ordered by events: order it by waiting for it here
+      const hipError_t e = hipStreamSynchronize(s);
+      bf->order_pending = false;
+      bf->zero_unsynced.store(false);
+      if (e != hipSuccess) return fail(RPT_ERR_HIP, "settling a cleared filter: %s", hipGetErrorString(e));
+      return RPT_OK;
+    }
+    bf->order_pending = true;  // later writes are ordered after the zeroing too
     return RPT_OK;
   }
   if (bf->zero_unsynced.load()) {
@@ -393,8 +411,12 @@ struct L1Geom {
 };
 L1Geom l1_geom(uint64_t n, int log_num_blocks) {
   static const uint64_t min_rows = [] {
-    const char* e = std::getenv("RPT_L1_GROUPS_MIN_ROWS");  // tuning runs only
+#if defined(RPT_PRODUCT_BUILD)
+    return kL1GroupsMinRows;  // the product runs the geometry the GPU suite tests
+#else
+    const char* e = std::getenv("RPT_L1_GROUPS_MIN_ROWS");  // tuning variants only (tools/build_variants.sh)
     return e ? static_cast<uint64_t>(std::strtoull(e, nullptr, 10)) : kL1GroupsMinRows;
+#endif
   }();
   L1Geom g;
   g.t1 = ceil_div(n, rpt::kL1TileRows);
@@ -413,12 +435,16 @@ L1Geom l1_geom(uint64_t n, int log_num_blocks) {
 }
 uint64_t level2_tiles_max(uint64_t n, int log_num_blocks) { return l1_geom(n, log_num_blocks).t2max; }
 
-// rpt::tile_mult, with its slice threshold overridable for tuning runs (RPT_TILE_MULT_SLICES: tiles
+// rpt::tile_mult, with its slice threshold overridable in tuning variants (RPT_TILE_MULT_SLICES: tiles
 // double above that many slices).
 uint32_t tile_mult_of(uint32_t n_slices) {
   static const uint32_t above = [] {
-    const char* e = std::getenv("RPT_TILE_MULT_SLICES");
+#if defined(RPT_PRODUCT_BUILD)
+    return 0u;  // the product keeps rpt::tile_mult
+#else
+    const char* e = std::getenv("RPT_TILE_MULT_SLICES");  // tuning variants only
     return e ? static_cast<uint32_t>(std::strtoul(e, nullptr, 10)) : 0u;
+#endif
   }();
   return above ? (n_slices > above ? 2u : 1u) : rpt::tile_mult(n_slices);
 }
@@ -1036,6 +1062,20 @@ int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream) {
   return RPT_OK;
 }
 
+int rpt_bf_settle(rpt_bf* bf, rpt_stream_t stream) {
+  if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
+  RPT_ON_DEVICE(bf->device);
+  RPT_SETTLE(bf, as_stream(stream));
+  if (bf->zero_unsynced.load()) {
+    std::lock_guard<std::mutex> lk(bf->order_mu);
+    if (bf->zero_unsynced.load()) {
+      RPT_HIP(hipEventSynchronize(bf->zero_ev));
+      bf->zero_unsynced.store(false);
+    }
+  }
+  return RPT_OK;
+}
+
 int rpt_bf_get_minmax(const rpt_bf* bf, int64_t* out_min, int64_t* out_max, int* out_has_value, rpt_stream_t stream) {
   if (!bf || !out_min || !out_max || !out_has_value) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
   RPT_ON_DEVICE(bf->device);
@@ -1577,6 +1617,8 @@ std::shared_ptr<const RcclApi> load_librccl() {
   sym(a->fn.comm_count, "ncclCommCount");
   sym(a->fn.comm_user_rank, "ncclCommUserRank");
   sym(a->fn.error_string, "ncclGetErrorString");
+  sym(a->fn.comm_abort, "ncclCommAbort");
+  sym(a->fn.get_async_error, "ncclCommGetAsyncError");
   return a;
 }
 
@@ -1665,6 +1707,92 @@ void give_helper(MergeHelper* h) {
   std::lock_guard<std::mutex> lk(g_helper_mu);
   g_helper_free.push_back(h);
 }
+
+// ---- bounded waits (rpt_collective_set_timeout_ms) ----
+// A peer that dies mid-merge never posts its side of a grouped send/recv: RCCL's kernels on this rank's
+// stream then wait for it forever, and ncclGroupEnd has already returned success. So the merge never blocks
+// on the stream blindly: it polls the stream and ncclCommGetAsyncError until the deadline, and on an error or
+// timeout aborts the communicator (ncclCommAbort: RCCL's kernels leave), then drains the streams, bounded too.
+constexpr int kNcclInProgress = 7;  // rccl.h ncclInProgress (a non-blocking communicator's pending call)
+std::atomic<uint64_t> g_coll_timeout_ms{RPT_COLLECTIVE_TIMEOUT_MS_DEFAULT};
+// Communicators this library aborted: ncclCommAbort frees them, so rpt_rccl_comm_destroy must not.
+std::mutex g_aborted_mu;
+std::vector<void*> g_aborted;
+
+using Clock = std::chrono::steady_clock;
+Clock::time_point coll_deadline() { return Clock::now() + std::chrono::milliseconds(g_coll_timeout_ms.load()); }
+
+// Sleep between polls: 10 us doubling to 200 us (an 8 GiB merge takes ~0.1 s, a 16 MiB one ~1 ms).
+struct Backoff {
+  unsigned us = 10;
+  void pause() {
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+    us = std::min(us * 2, 200u);
+  }
+};
+
+// RPT_OK once every stream in `ss` has completed; otherwise a status and the reason in *why. With a
+// communicator, its asynchronous error is polled too (an error other than ncclInProgress ends the wait).
+int poll_streams(const rpt_rccl_api_table* api, void* comm, std::initializer_list<hipStream_t> ss,
+                 Clock::time_point deadline, std::string* why) {
+  Backoff b;
+  for (;;) {
+    bool all = true;
+    for (hipStream_t x : ss) {
+      const hipError_t q = hipStreamQuery(x);
+      if (q == hipErrorNotReady) {
+        all = false;
+      } else if (q != hipSuccess) {
+        *why = std::string("stream error: ") + hipGetErrorString(q);
+        return RPT_ERR_HIP;
+      }
+    }
+    if (all) return RPT_OK;
+    if (api && comm) {
+      int ae = 0;
+      const int rc = api->get_async_error(comm, &ae);
+      if (rc != 0 || (ae != 0 && ae != kNcclInProgress)) {
+        *why = std::string("RCCL asynchronous error: ") + api->error_string(rc != 0 ? rc : ae);
+        return RPT_ERR_COLLECTIVE;
+      }
+    }
+    if (Clock::now() >= deadline) {
+      *why = "no progress within " + std::to_string(g_coll_timeout_ms.load()) + " ms (a peer that never posted its side?)";
+      return RPT_ERR_COLLECTIVE;
+    }
+    b.pause();
+  }
+}
+
+// A call that returned ncclInProgress (non-blocking communicator): poll ncclCommGetAsyncError until it
+// settles or the deadline passes. Other results pass through.
+int settle_nccl(const rpt_rccl_api_table& api, void* comm, int rc, Clock::time_point deadline) {
+  Backoff b;
+  while (rc == kNcclInProgress) {
+    if (Clock::now() >= deadline) return kNcclInProgress;
+    b.pause();
+    int ae = 0;
+    const int q = api.get_async_error(comm, &ae);
+    rc = q != 0 ? q : ae;
+  }
+  return rc;
+}
+
+void abort_comm(const rpt_rccl_api_table& api, void* comm) {
+  {
+    std::lock_guard<std::mutex> lk(g_aborted_mu);
+    g_aborted.push_back(comm);
+  }
+  (void)api.comm_abort(comm);
+}
+
+bool take_aborted(void* comm) {
+  std::lock_guard<std::mutex> lk(g_aborted_mu);
+  auto it = std::find(g_aborted.begin(), g_aborted.end(), comm);
+  if (it == g_aborted.end()) return false;
+  g_aborted.erase(it);
+  return true;
+}
 }  // namespace
 extern "C" {
 
@@ -1673,7 +1801,8 @@ extern "C" {
     const int rc_ = (call);                                                                    \
     if (rc_ != 0) return fail(RPT_ERR_COLLECTIVE, "%s: %s", #call, api.error_string(rc_));      \
   } while (0)
-// inside ncclGroupStart/End: close the group before returning, so the caller's RCCL state stays usable
+// inside ncclGroupStart/End: close the group before returning (rpt_bf_allreduce_or_ws then aborts the
+// communicator: peers may already depend on this rank's earlier groups)
 #define RPT_NCCL_IN_GROUP(call)                                                                 \
   do {                                                                                         \
     const int rc_ = (call);                                                                    \
@@ -1681,6 +1810,12 @@ extern "C" {
       (void)api.group_end();                                                                   \
       return fail(RPT_ERR_COLLECTIVE, "%s: %s", #call, api.error_string(rc_));                 \
     }                                                                                          \
+  } while (0)
+// a merge call: a non-blocking communicator's ncclInProgress is polled to completion by the deadline
+#define RPT_NCCL_MERGE(call)                                                                    \
+  do {                                                                                         \
+    const int rc_ = settle_nccl(api, nccl_comm, (call), deadline);                             \
+    if (rc_ != 0) return fail(RPT_ERR_COLLECTIVE, "%s: %s", #call, api.error_string(rc_));      \
   } while (0)
 
 size_t rpt_allreduce_workspace_bytes(int world, int log_num_blocks) {
@@ -1690,6 +1825,7 @@ size_t rpt_allreduce_workspace_bytes(int world, int log_num_blocks) {
 
 int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t workspace_bytes,
                            rpt_stream_t stream) {
+  t_merge_stuck = false;
   if (!bf || !nccl_comm) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
   const std::shared_ptr<const RcclApi> api_p = rccl_api();
   const rpt_rccl_api_table& api = api_p->fn;
@@ -1710,6 +1846,9 @@ int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t 
     order.done(false);
     return fail(RPT_ERR_HIP, "hipMemsetAsync failed");
   }
+  // every RCCL call below, and the wait for the stream, ends by this deadline (rpt_collective_set_timeout_ms)
+  const Clock::time_point deadline = coll_deadline();
+  bool posted = false;          // a collective call was issued: peers may now depend on this rank
   bool helper_pending = false;  // OR kernels enqueued on the helper stream and not yet joined into s
   auto join_helper = [&]() -> hipError_t {
     if (!helper_pending) return hipSuccess;
@@ -1732,7 +1871,8 @@ int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t 
         uint64_t* buf = stage + static_cast<uint64_t>(b) * (world - 1) * R;
         const uint64_t cnt = g.piece(me, r), stride = (cnt + 1) & ~1ULL;
         if (ored[b]) RPT_HIP(hipStreamWaitEvent(s, h->ored[b], 0));  // round r - 2's OR has read buf
-        RPT_NCCL(api.group_start());
+        posted = true;
+        RPT_NCCL_MERGE(api.group_start());
         for (int p = 0, k = 0; p < world; p++) {
           if (p == me) continue;
           const uint64_t out = g.piece(p, r);
@@ -1740,7 +1880,7 @@ int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t 
           if (cnt) RPT_NCCL_IN_GROUP(api.recv(buf + static_cast<uint64_t>(k) * stride, cnt, kNcclUint64, p, nccl_comm, s));
           k++;
         }
-        RPT_NCCL(api.group_end());
+        RPT_NCCL_MERGE(api.group_end());
         if (cnt) {
           RPT_HIP(hipEventRecord(h->rx[b], s));
           RPT_HIP(hipStreamWaitEvent(h->s, h->rx[b], 0));
@@ -1757,35 +1897,62 @@ int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t 
       }
       // all-gather: every rank's merged words to every peer, once its OR kernels are done
       RPT_HIP(join_helper());
-      RPT_NCCL(api.group_start());
+      RPT_NCCL_MERGE(api.group_start());
       for (int p = 0; p < world; p++) {
         if (p == me) continue;
         if (g.len(me)) RPT_NCCL_IN_GROUP(api.send(bf->words + g.lo(me), g.len(me), kNcclUint64, p, nccl_comm, s));
         if (g.len(p)) RPT_NCCL_IN_GROUP(api.recv(bf->words + g.lo(p), g.len(p), kNcclUint64, p, nccl_comm, s));
       }
-      RPT_NCCL(api.group_end());
+      RPT_NCCL_MERGE(api.group_end());
     }
     hipLaunchKernelGGL(minmax_pack_kernel, dim3(1), dim3(1), 0, s, bf->stats, bf->has_data.load(), v);
     RPT_LAUNCHED("minmax_pack_kernel");
-    RPT_NCCL(api.all_reduce(v, v, 3, kNcclInt64, kNcclMin, nccl_comm, s));
+    posted = true;
+    RPT_NCCL_MERGE(api.all_reduce(v, v, 3, kNcclInt64, kNcclMin, nccl_comm, s));
     hipLaunchKernelGGL(minmax_unpack_kernel, dim3(1), dim3(1), 0, s, v, bf->stats, reinterpret_cast<int*>(v + 3));
     RPT_LAUNCHED("minmax_unpack_kernel");
+    // bounded wait for everything enqueued above (never a blind hipStreamSynchronize: see poll_streams)
+    std::string why;
+    const int ws = poll_streams(&api, nccl_comm, {s}, deadline, &why);
+    if (ws != RPT_OK) return fail(ws, "OR all-reduce (rank %d of %d): %s", me, world, why.c_str());
     int has = 0;
-    RPT_HIP(hipMemcpyAsync(&has, v + 3, sizeof(int), hipMemcpyDeviceToHost, s));
+    RPT_HIP(hipMemcpyAsync(&has, v + 3, sizeof(int), hipMemcpyDeviceToHost, s));  // s is idle: returns at once
     RPT_HIP(hipStreamSynchronize(s));
     bf->has_data.store(has ? 1 : 0);
     return RPT_OK;
   };
-  const int st = run();
-  // on an error path the helper may still hold OR kernels: the caller's stream waits for them, so the
-  // workspace is free once `stream` is
-  if (h) {
+  int st = run();
+  const std::string err = t_last_error;
+  bool drained = true;
+  if (st != RPT_OK && posted) {
+    // peers may be blocked on this rank, or this rank on a dead peer: the communicator cannot be reused.
+    // Abort it (RCCL's kernels on s leave), then drain s and the helper stream, bounded again, so the
+    // workspace is free on return.
+    abort_comm(api, nccl_comm);
+    (void)join_helper();
+    std::string why;
+    drained = poll_streams(nullptr, nullptr, {s}, coll_deadline(), &why) == RPT_OK &&
+              (!h || poll_streams(nullptr, nullptr, {h->s}, coll_deadline(), &why) == RPT_OK);
+    t_merge_stuck = !drained;
+    t_last_error = err + "; communicator aborted" +
+                   (drained ? "" : "; streams did not drain (" + why + "): the workspace is still in use");
+  } else if (h) {
+    // on an error before any collective call the helper may still hold OR kernels: the caller's stream
+    // waits for them, so the workspace is free once `stream` is
     if (join_helper() != hipSuccess) (void)hipStreamSynchronize(h->s);
-    give_helper(h);
   }
+  if (h && drained) give_helper(h);  // a helper stream that did not drain is leaked, never reused
   order.done(false);
   return st;
 }
+
+int rpt_collective_set_timeout_ms(uint64_t ms) {
+  if (ms == 0) return fail(RPT_ERR_INVALID_ARGUMENT, "collective timeout of 0 ms");
+  g_coll_timeout_ms.store(ms);
+  return RPT_OK;
+}
+
+uint64_t rpt_collective_timeout_ms(void) { return g_coll_timeout_ms.load(); }
 
 int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
   if (!bf || !nccl_comm) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
@@ -1804,6 +1971,7 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
     return fail(RPT_ERR_OUT_OF_MEMORY, "all-reduce workspace of %zu bytes", bytes);
   }
   const int st = rpt_bf_allreduce_or_ws(bf, nccl_comm, ws, bytes, stream);
+  if (t_merge_stuck) return st;  // aborted and still not drained: the workspace is leaked, never freed in use
   (void)hipStreamSynchronize(as_stream(stream));  // nothing may still use the workspace
   (void)hipFree(ws);
   return st;
@@ -1838,12 +2006,14 @@ int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, 
   std::memcpy(uid.internal, id, RPT_RCCL_UNIQUE_ID_BYTES);
   void* comm = nullptr;
   RPT_NCCL(api.comm_init_rank(&comm, world, uid, rank));
+  (void)take_aborted(comm);  // a new communicator at an aborted one's address is live
   *out_comm = comm;
   return RPT_OK;
 }
 
 int rpt_rccl_comm_destroy(void* comm) {
   if (!comm) return RPT_OK;
+  if (take_aborted(comm)) return RPT_OK;  // a failed merge aborted it: ncclCommAbort already freed it
   const std::shared_ptr<const RcclApi> api_p = rccl_api();
   const rpt_rccl_api_table& api = api_p->fn;
   if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
@@ -1851,6 +2021,7 @@ int rpt_rccl_comm_destroy(void* comm) {
   return RPT_OK;
 }
 #undef RPT_NCCL_IN_GROUP
+#undef RPT_NCCL_MERGE
 #undef RPT_NCCL
 
 #ifdef RPT_TESTING_HOOKS

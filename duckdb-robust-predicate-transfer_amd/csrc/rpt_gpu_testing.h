@@ -40,6 +40,8 @@ typedef struct rpt_rccl_api_table {
   int (*comm_count)(void* comm, int* count);                                       /* ncclCommCount */
   int (*comm_user_rank)(void* comm, int* rank);                                    /* ncclCommUserRank */
   const char* (*error_string)(int result);                                         /* ncclGetErrorString */
+  int (*comm_abort)(void* comm);                                                   /* ncclCommAbort */
+  int (*get_async_error)(void* comm, int* async_error);                            /* ncclCommGetAsyncError */
 } rpt_rccl_api_table;
 
 #ifdef RPT_TESTING_HOOKS

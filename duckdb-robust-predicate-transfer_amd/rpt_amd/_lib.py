@@ -97,6 +97,7 @@ SIGNATURES = {
     "rpt_bf_reinitialize": (c_int, [c_void_p, c_uint64]),
     "rpt_bf_set_finalized": (c_int, [c_void_p, c_int]),
     "rpt_bf_clear": (c_int, [c_void_p, c_void_p]),
+    "rpt_bf_settle": (c_int, [c_void_p, c_void_p]),
     "rpt_bf_insert": (c_int, [c_void_p, POINTER(KeyColumn), c_uint64, c_void_p]),
     "rpt_insert_workspace_bytes": (c_size_t, [c_uint64, c_int]),
     "rpt_bf_insert_workspace_bytes": (c_size_t, [c_void_p, c_uint64]),
@@ -124,6 +125,8 @@ SIGNATURES = {
     "rpt_bf_allreduce_or": (c_int, [c_void_p, c_void_p, c_void_p]),
     "rpt_bf_allreduce_or_ws": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "rpt_allreduce_workspace_bytes": (c_size_t, [c_int, c_int]),
+    "rpt_collective_set_timeout_ms": (c_int, [c_uint64]),
+    "rpt_collective_timeout_ms": (c_uint64, []),
     "rpt_rccl_available": (c_int, [c_int]),
     "rpt_rccl_get_unique_id": (c_int, [c_void_p]),
     "rpt_rccl_comm_init_rank": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),

@@ -259,6 +259,10 @@ class BloomFilter:
     def clear(self, stream=None) -> None:
         check(self._lib.rpt_bf_clear(self._h, _stream(self.device, stream)))
 
+    def settle(self, stream=None) -> None:
+        """Settle a deferred clear now (rpt_bf_settle; before a stream capture reads the filter)."""
+        check(self._lib.rpt_bf_settle(self._h, _stream(self.device, stream)))
+
     def minmax(self, stream=None) -> Optional[tuple[int, int]]:
         """(min, max) of the valid I32/I64 keys inserted so far, or None (the CREATE_BF min/max
         dynamic filter, physical_create_bf.cpp:82-176, computed inside the insert kernels)."""

@@ -117,6 +117,28 @@ class RcclComm:
             raise RptError(st, self._lib.rpt_last_error().decode(errors="replace"))
         self.handle = h
 
+    @classmethod
+    def single(cls, device: torch.device) -> "RcclComm":
+        """A one-rank communicator without a torch.distributed group (bench.py --c5-merge at N = 1: the
+        merge's min/max all-reduce and bounded wait run through real RCCL; no peer words move)."""
+        from ._lib import RptError, load
+
+        self = cls.__new__(cls)
+        self._lib = load()
+        self.handle = None
+        self.device = torch.device(device)
+        self.world, self.rank = 1, 0
+        dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        uid = (ctypes.c_uint8 * cls.ID_BYTES)()
+        h = ctypes.c_void_p()
+        for call in (lambda: self._lib.rpt_rccl_available(dev), lambda: self._lib.rpt_rccl_get_unique_id(uid),
+                     lambda: self._lib.rpt_rccl_comm_init_rank(dev, 1, uid, 0, ctypes.byref(h))):
+            st = call()
+            if st != 0:
+                raise RptError(st, self._lib.rpt_last_error().decode(errors="replace"))
+        self.handle = h
+        return self
+
     def close(self) -> None:
         if self.handle is not None and self.handle.value:
             self._lib.rpt_rccl_comm_destroy(self.handle)

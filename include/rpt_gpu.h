@@ -154,6 +154,11 @@ size_t rpt_bf_probe_workspace_bytes(const rpt_bf* bf, uint64_t n_rows);
  * probe, copy or export zeroes the words first, ordered like any other write. Only a direct read through
  * rpt_bf_info::words can see the words before that. */
 int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
+/* Settle a deferred clear now: zero the words on `stream` and wait until that zeroing has completed (a
+ * no-op if no clear is pending). Needed before a stream capture (graph) reads a cleared filter: a read
+ * inside a capture that would have to settle the clear is refused with RPT_ERR_INVALID_ARGUMENT (the
+ * zeroing would be replayed with the graph). Synchronous. */
+int rpt_bf_settle(rpt_bf* bf, rpt_stream_t stream);
 
 /* ---- build ------------------------------------------------------------------------------- */
 /* PTBloomFilter::Insert (bloom_filter.cpp:70-78): hash each of n rows of `col` and OR its mask into
@@ -255,12 +260,27 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream);
  * round r + 1 transfers on `stream`. rpt_bf_allreduce_or_ws takes that staging from the caller
  * (rpt_allreduce_workspace_bytes(world, log_num_blocks) bytes of device memory, exclusively owned until
  * the call returns; <= 2 (W-1) * 32 MiB + 256 B whatever the filter size); rpt_bf_allreduce_or allocates
- * and frees it itself. */
+ * and frees it itself.
+ * Failure (the cross-GPU analogue of a Combine that cannot finish, physical_create_bf.cpp:244-275): the
+ * call never blocks on the stream blindly. It polls the stream and ncclCommGetAsyncError until every
+ * transfer completed or the collective timeout (rpt_collective_set_timeout_ms) passed; a non-blocking
+ * communicator's ncclInProgress results are polled against the same deadline. A peer that dies mid-merge
+ * never posts its side, so its peers' streams would wait forever: on a timeout, an asynchronous RCCL error
+ * or any error after the first collective call, the call ABORTS the communicator (ncclCommAbort, which
+ * frees it: do not use it again; rpt_rccl_comm_destroy accepts it and does nothing), drains the streams
+ * (bounded again) and returns RPT_ERR_COLLECTIVE. The filter then holds its own partial plus possibly some
+ * peers' bits (never fewer bits than before the call): rebuild it, or merge again on a new communicator. */
 #define RPT_ALLREDUCE_ROUND_WORDS (4ULL << 20)
 size_t rpt_allreduce_workspace_bytes(int world, int log_num_blocks);
 int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t workspace_bytes,
                            rpt_stream_t stream);
 int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream);
+/* Bound of one OR all-reduce's waits (process-wide; default RPT_COLLECTIVE_TIMEOUT_MS_DEFAULT). An 8 GiB
+ * filter merges in well under a second over xGMI; the bound only has to outlast RCCL's first connection
+ * setup between the ranks. 0 is rejected. */
+#define RPT_COLLECTIVE_TIMEOUT_MS_DEFAULT 120000ULL
+int rpt_collective_set_timeout_ms(uint64_t ms);
+uint64_t rpt_collective_timeout_ms(void);
 /* RCCL communicator for callers that bring none (bench.py, tests; a DuckDB shim that owns an
  * ncclComm_t passes it to rpt_bf_allreduce_or directly). Rank 0 calls rpt_rccl_get_unique_id, the
  * caller broadcasts the RPT_RCCL_UNIQUE_ID_BYTES bytes out of band (torch.distributed, MPI, a file),

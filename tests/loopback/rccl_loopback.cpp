@@ -15,10 +15,21 @@
 //       sender's stream waits on the done events of its sends (the buffer may be reused after).
 //       No host synchronization: every dependency is a stream-event wait.
 //   ncclAllReduce   int64/uint64 MIN / MAX / SUM, staged through the host (3 words in the product)
-//   failure injection: rpt_loopback_fail_op(rank, k) makes the k-th send/recv call of that rank fail;
-//       the failing rank's GroupEnd then aborts the world and every rank's pending GroupEnd fails.
+//   ncclCommAbort / ncclCommGetAsyncError   rank-local, as in RCCL: an abort frees that rank's communicator and
+//       releases only that rank's blocked streams (below); the asynchronous error is the world's (0 unless a
+//       silent peer was set to report)
+//   failure injection:
+//     rpt_loopback_fail_op(rank, k)   the k-th send/recv call of that rank fails; the failing rank's GroupEnd
+//       aborts the world and every rank's pending GroupEnd fails (an error RCCL propagated);
+//     rpt_loopback_silent_peer(rank, k, report)   the k-th send/recv call of that rank fails and its group
+//       closes WITHOUT telling the world: as a peer that died mid-merge. The other ranks' GroupEnd (and
+//       AllReduce) calls then return success, as RCCL's do, and block their streams instead (a host function
+//       on the stream that waits until that rank aborts its communicator; 60 s safety bound), so only a
+//       bounded wait in the caller ends them. report != 0: ncclCommGetAsyncError reports ncclRemoteError
+//       once the peer is gone.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -26,15 +37,18 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <vector>
 
 namespace {
 
-constexpr int kSuccess = 0, kUnhandledCudaError = 1, kInternalError = 3, kInvalidArgument = 4, kInvalidUsage = 5;
+constexpr int kSuccess = 0, kUnhandledCudaError = 1, kInternalError = 3, kInvalidArgument = 4, kInvalidUsage = 5,
+              kRemoteError = 6;
 constexpr int kInt64 = 4, kUint64 = 5;                 // ncclDataType_t
 constexpr int kSum = 0, kMax = 2, kMin = 3;            // ncclRedOp_t
 constexpr auto kBarrierTimeout = std::chrono::seconds(120);
+constexpr auto kBlockedStreamBound = std::chrono::seconds(60);  // safety bound of a silent-peer stream block
 
 struct UniqueId {
   char internal[128];
@@ -58,7 +72,10 @@ struct World {
   std::condition_variable cv;
   int arrived = 0;
   uint64_t gen = 0;
-  bool aborted = false;
+  bool aborted = false;           // an error propagated to every rank (rpt_loopback_fail_op)
+  bool dead = false;              // a silent peer is gone (rpt_loopback_silent_peer): groups never match
+  int async_err = kSuccess;       // what ncclCommGetAsyncError reports
+  std::vector<bool> rank_aborted;  // ncclCommAbort per rank: releases that rank's blocked streams
   std::map<std::pair<int, int>, std::deque<SendRec*>> chan;  // (src, dst) -> posted sends
   std::vector<hipEvent_t> retired;                           // destroyed when the world ends
   std::vector<std::vector<int64_t>> ar;                      // all-reduce contributions
@@ -66,7 +83,7 @@ struct World {
 };
 
 struct Comm {
-  World* w;
+  std::shared_ptr<World> w;
   int rank, device;
   std::atomic<int> ops{0};
 };
@@ -82,17 +99,19 @@ struct Op {
 };
 
 std::mutex g_mu;
-std::map<uint64_t, World*> g_worlds;
+std::map<uint64_t, std::shared_ptr<World>> g_worlds;
 std::atomic<uint64_t> g_next_id{1};
 std::atomic<int> g_fail_rank{-1}, g_fail_op{-1};
+std::atomic<int> g_silent{0}, g_silent_report{0};  // the armed failure is a silent peer (and reports it)
 
 thread_local int t_depth = 0;
 thread_local bool t_err = false;
 thread_local std::vector<Op> t_ops;
+thread_local Comm* t_err_comm = nullptr;  // the communicator of the group's failed call
 
-// All ranks of w meet; false on abort or timeout (the world is then aborted).
+// All ranks of w meet; false on abort, timeout (the world is then aborted) or a dead peer (w->dead).
 bool barrier(World* w, std::unique_lock<std::mutex>& lk) {
-  if (w->aborted) return false;
+  if (w->aborted || w->dead) return false;
   const uint64_t g = w->gen;
   if (++w->arrived == w->size) {
     w->arrived = 0;
@@ -100,11 +119,31 @@ bool barrier(World* w, std::unique_lock<std::mutex>& lk) {
     w->cv.notify_all();
     return true;
   }
-  if (!w->cv.wait_for(lk, kBarrierTimeout, [&] { return w->gen != g || w->aborted; })) {
+  if (!w->cv.wait_for(lk, kBarrierTimeout, [&] { return w->gen != g || w->aborted || w->dead; })) {
     w->aborted = true;
     w->cv.notify_all();
   }
   return w->gen != g;
+}
+
+// A silent peer's group never completes: block `stream` (as RCCL's kernels would) until rank `rank` aborts
+// its communicator, or the safety bound passes.
+struct BlockArg {
+  std::shared_ptr<World> w;
+  int rank;
+};
+void block_host_fn(void* p) {
+  std::unique_ptr<BlockArg> a(static_cast<BlockArg*>(p));
+  std::unique_lock<std::mutex> lk(a->w->mu);
+  a->w->cv.wait_for(lk, kBlockedStreamBound, [&] { return a->w->rank_aborted[a->rank]; });
+}
+int block_stream(const std::shared_ptr<World>& w, int rank, hipStream_t stream) {
+  auto* a = new BlockArg{w, rank};
+  if (hipLaunchHostFunc(stream, block_host_fn, a) != hipSuccess) {
+    delete a;
+    return kUnhandledCudaError;
+  }
+  return kSuccess;
 }
 
 void abort_world(World* w) {
@@ -124,24 +163,51 @@ int enqueue(bool send, const void* buf, size_t count, int dt, int peer, void* co
     return kInvalidArgument;
   }
   if (fail_injected(c)) {
-    if (t_depth > 0) t_err = true;
+    if (t_depth > 0) {
+      t_err = true;
+      t_err_comm = c;
+    }
     return kInternalError;
   }
   t_ops.push_back(Op{send, c, const_cast<void*>(buf), count * dtype_bytes(dt), peer, stream});
   return kSuccess;
 }
 
-int run_group(std::vector<Op>& ops, bool err) {
-  if (ops.empty()) return err ? kInternalError : kSuccess;
-  World* w = ops[0].c->w;
-  const int me = ops[0].c->rank;
+// A group of a world whose silent peer is gone: "succeeds" on the host, every stream of it blocks.
+int dead_group(const std::shared_ptr<World>& w, int me, std::vector<Op>& ops) {
+  int rc = kSuccess;
+  std::vector<hipStream_t> seen;
+  for (Op& o : ops) {
+    if (std::find(seen.begin(), seen.end(), o.stream) != seen.end()) continue;
+    seen.push_back(o.stream);
+    if (block_stream(w, me, o.stream) != kSuccess) rc = kUnhandledCudaError;
+  }
+  return rc;
+}
+
+int run_group(std::vector<Op>& ops, bool err, Comm* err_comm) {
+  Comm* c0 = !ops.empty() ? ops[0].c : err_comm;
+  if (!c0) return err ? kInternalError : kSuccess;
+  std::shared_ptr<World> wp = c0->w;
+  World* w = wp.get();
+  const int me = c0->rank;
   for (const Op& o : ops)
-    if (o.c->w != w) return kInvalidUsage;  // one communicator per group in this loopback
-  if (hipSetDevice(ops[0].c->device) != hipSuccess) return kUnhandledCudaError;
+    if (o.c->w != wp) return kInvalidUsage;  // one communicator per group in this loopback
+  if (hipSetDevice(c0->device) != hipSuccess) return kUnhandledCudaError;
   std::unique_lock<std::mutex> lk(w->mu);
-  if (err) {
-    abort_world(w);
+  if (err) {  // the failing rank's group closes
+    if (g_silent.load()) {  // the peer "dies": nobody is told
+      w->dead = true;
+      if (g_silent_report.load()) w->async_err = kRemoteError;
+      w->cv.notify_all();
+    } else {
+      abort_world(w);
+    }
     return kInternalError;
+  }
+  if (w->dead) {
+    lk.unlock();
+    return dead_group(wp, me, ops);
   }
   // (1) post the sends
   for (Op& o : ops) {
@@ -154,7 +220,11 @@ int run_group(std::vector<Op>& ops, bool err) {
     }
     w->chan[{me, o.peer}].push_back(o.rec);
   }
-  if (!barrier(w, lk)) return kInternalError;
+  if (!barrier(w, lk)) {
+    if (!w->dead || w->aborted) return kInternalError;
+    lk.unlock();
+    return dead_group(wp, me, ops);
+  }
   // (2) match the receives in issue order per peer
   int rc = kSuccess;
   for (Op& o : ops) {
@@ -221,14 +291,15 @@ int ncclCommInitRank(void** comm, int nranks, UniqueId id, int rank) {
     return kInvalidArgument;
   uint64_t key = 0;
   std::memcpy(&key, id.internal + 8, sizeof key);
-  World* w = nullptr;
+  std::shared_ptr<World> w;
   {
     std::lock_guard<std::mutex> g(g_mu);
-    World*& slot = g_worlds[key];
+    std::shared_ptr<World>& slot = g_worlds[key];
     if (!slot) {
-      slot = new World();
+      slot = std::make_shared<World>();
       slot->size = nranks;
       slot->ar.resize(nranks);
+      slot->rank_aborted.assign(nranks, false);
     }
     w = slot;
   }
@@ -239,7 +310,7 @@ int ncclCommInitRank(void** comm, int nranks, UniqueId id, int rank) {
   std::unique_lock<std::mutex> lk(w->mu);
   w->joined++;
   w->live++;
-  if (!barrier(w, lk)) {  // collective: every rank joins before any returns
+  if (!barrier(w.get(), lk)) {  // collective: every rank joins before any returns
     w->live--;
     delete c;
     return kInternalError;
@@ -248,33 +319,59 @@ int ncclCommInitRank(void** comm, int nranks, UniqueId id, int rank) {
   return kSuccess;
 }
 
-int ncclCommDestroy(void* comm) {
-  Comm* c = static_cast<Comm*>(comm);
-  if (!c) return kInvalidArgument;
-  World* w = c->w;
+// Frees the communicator; the last one of its world releases the world's events (the World itself lives
+// on while a blocked stream's host function still holds it).
+int release_comm(Comm* c, bool abort) {
+  std::shared_ptr<World> w = c->w;
   bool last = false;
   {
     std::lock_guard<std::mutex> lk(w->mu);
+    if (abort) {
+      w->rank_aborted[c->rank] = true;  // this rank's blocked streams resume
+      w->cv.notify_all();
+    }
     last = --w->live == 0;
   }
   if (last) {
     (void)hipSetDevice(c->device);
-    (void)hipDeviceSynchronize();  // every retired event has completed
+    (void)hipDeviceSynchronize();  // every retired event has completed (every rank has aborted or destroyed)
     for (hipEvent_t e : w->retired) (void)hipEventDestroy(e);
+    w->retired.clear();
     for (auto& kv : w->chan)
       for (SendRec* r : kv.second) {
         if (r->ready) (void)hipEventDestroy(r->ready);
         delete r;
       }
+    w->chan.clear();
     std::lock_guard<std::mutex> g(g_mu);
     for (auto it = g_worlds.begin(); it != g_worlds.end(); ++it)
       if (it->second == w) {
         g_worlds.erase(it);
         break;
       }
-    delete w;
   }
   delete c;
+  return kSuccess;
+}
+
+int ncclCommDestroy(void* comm) {
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c) return kInvalidArgument;
+  return release_comm(c, false);
+}
+
+// Rank-local, as RCCL's: frees this rank's communicator and releases this rank's blocked streams only.
+int ncclCommAbort(void* comm) {
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c) return kInvalidArgument;
+  return release_comm(c, true);
+}
+
+int ncclCommGetAsyncError(void* comm, int* async_error) {
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c || !async_error) return kInvalidArgument;
+  std::lock_guard<std::mutex> lk(c->w->mu);
+  *async_error = c->w->async_err;
   return kSuccess;
 }
 
@@ -294,6 +391,7 @@ int ncclGroupStart() {
   if (t_depth++ == 0) {
     t_ops.clear();
     t_err = false;
+    t_err_comm = nullptr;
   }
   return kSuccess;
 }
@@ -304,8 +402,10 @@ int ncclGroupEnd() {
   std::vector<Op> ops;
   ops.swap(t_ops);
   const bool err = t_err;
+  Comm* err_comm = t_err_comm;
   t_err = false;
-  return run_group(ops, err);
+  t_err_comm = nullptr;
+  return run_group(ops, err, err_comm);
 }
 
 int ncclSend(const void* buf, size_t count, int dt, int peer, void* comm, hipStream_t stream) {
@@ -328,8 +428,12 @@ int ncclAllReduce(const void* sendbuf, void* recvbuf, size_t count, int dt, int 
   Comm* c = static_cast<Comm*>(comm);
   if (!c || (dt != kInt64 && dt != kUint64) || (op != kMin && op != kMax && op != kSum) || t_depth > 0)
     return kInvalidArgument;
-  World* w = c->w;
+  World* w = c->w.get();
   if (hipSetDevice(c->device) != hipSuccess) return kUnhandledCudaError;
+  {
+    std::lock_guard<std::mutex> lk(w->mu);
+    if (w->dead) return block_stream(c->w, c->rank, stream);  // never completes, as RCCL's would not
+  }
   std::vector<int64_t> mine(count);
   if (hipStreamSynchronize(stream) != hipSuccess ||
       (count && hipMemcpy(mine.data(), sendbuf, count * 8, hipMemcpyDeviceToHost) != hipSuccess))
@@ -340,6 +444,10 @@ int ncclAllReduce(const void* sendbuf, void* recvbuf, size_t count, int dt, int 
     w->ar[c->rank] = mine;
     if (!barrier(w, lk)) {
       delete out;
+      if (w->dead && !w->aborted) {
+        lk.unlock();
+        return block_stream(c->w, c->rank, stream);
+      }
       return kInternalError;
     }
     for (size_t i = 0; i < count; i++) {
@@ -368,6 +476,16 @@ int ncclAllReduce(const void* sendbuf, void* recvbuf, size_t count, int dt, int 
 // ---- test controls ----------------------------------------------------------------------------------
 // The k-th send/recv call (0-based, counted per communicator) of rank `rank` fails; (-1, -1) disarms.
 void rpt_loopback_fail_op(int rank, int k) {
+  g_silent.store(0);
+  g_silent_report.store(0);
+  g_fail_op.store(k);
+  g_fail_rank.store(rank);
+}
+// The k-th send/recv call of rank `rank` fails and that rank goes silent (a peer dying mid-merge: see the
+// header); report != 0 makes ncclCommGetAsyncError return ncclRemoteError afterwards. (-1, -1, 0) disarms.
+void rpt_loopback_silent_peer(int rank, int k, int report) {
+  g_silent.store(rank >= 0 ? 1 : 0);
+  g_silent_report.store(report != 0 ? 1 : 0);
   g_fail_op.store(k);
   g_fail_rank.store(rank);
 }

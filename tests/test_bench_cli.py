@@ -67,3 +67,32 @@ def test_configs():
     assert bench.CONFIGS["C2"][0](1) == 10**7 and bench.CONFIGS["C3"][1](8) == 10**8
     assert bench.CONFIGS["C5"][0](8) == 8 * 10**9 and bench.CONFIGS["C5"][1](1) == 8 * 10**9
     assert bench.config_tag("C2", "i32") == "C2-i32"
+
+
+def test_c5_merge_record_schema():
+    """The `c5_merge` object bench.py adds at N > 1: merge time as the median of the
+    timed reps, GB/s per GPU = 2 (W-1)/W S / t and per link = 2 S / W / t, the node-wide probe rate."""
+    S = 8 << 30
+    rec = bench.c5_merge_record(8, S, 10**9, 7.5, [0.30, 0.20, 0.25], 8.6, 12345, "bit-identical", 120000)
+    for k in ("what", "n_gpus", "filter_bytes", "rows_per_rank", "build_rows", "insert_ms", "or_merge_ms",
+              "or_merge_ms_reps", "or_merge_GBps_per_gpu", "or_merge_GBps_per_link", "probe_ms",
+              "probe_keys_per_s_node", "survivors_rank0", "merge_check", "collective_timeout_ms"):
+        assert k in rec, k
+    assert rec["build_rows"] == 8 * 10**9 and rec["or_merge_ms"] == pytest.approx(250.0)
+    assert rec["or_merge_GBps_per_gpu"] == pytest.approx(2 * 7 / 8 * S / 0.25 / 1e9)
+    assert rec["or_merge_GBps_per_link"] == pytest.approx(2 / 8 * S / 0.25 / 1e9)
+    assert rec["probe_keys_per_s_node"] == pytest.approx(8e9 / 8.6e-3)
+    json.dumps(rec)
+    one = bench.c5_merge_record(1, S, 10**7, 1.0, [0.001], 2.0, 1, "bit-identical", 1000)
+    assert one["or_merge_GBps_per_gpu"] is None and one["or_merge_GBps_per_link"] is None  # no peer traffic
+
+
+def test_c5_merge_flags(monkeypatch):
+    assert bench.C5_FILTER_ROWS == 8 * 10**9 and bench.C5_ROWS_PER_RANK == 10**9
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    a = bench.parse()
+    assert not a.c5_merge and not a.no_c5_merge and a.c5_rows_per_rank == 1e9 and a.c5_merge_reps == 3
+    assert a.collective_timeout_ms is None
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--c5-merge", "--c5-rows-per-rank", "1e7", "--collective-timeout-ms", "5000"])
+    a = bench.parse()
+    assert a.c5_merge and a.c5_rows_per_rank == 1e7 and a.collective_timeout_ms == 5000

@@ -47,3 +47,27 @@ def test_product_build_pins_tuning_macros(macro):
     r = syntax_check("RPT_PRODUCT_BUILD=1", macro)
     assert r.returncode != 0 and "must keep their tested defaults" in r.stderr
     assert syntax_check(macro).returncode == 0
+
+
+def test_small_probe_rows_cover_every_segment():
+    """RPT_SMALL_PROBE_ROWS (include/rpt_gpu.h) that is not a multiple of 16 waves x 512 rows
+    would leave segments unprobed (their rows silently dropped); more than 64 segments overflow the one-wave
+    sel-tail scan. The kernels static_assert both; the header's value obeys them."""
+    import re
+
+    hdr = open(os.path.join(REPO, "include", "rpt_gpu.h")).read()
+    rows = int(re.search(r"#define RPT_SMALL_PROBE_ROWS (\d+)", hdr).group(1))
+    assert rows % (512 * 16) == 0 and rows // 512 <= 64
+    src = open(os.path.join(PKG, "csrc", "kernels", "probe_direct.hpp")).read()
+    assert "static_assert(kSmallRows % (kSegRows * (kSmallThreads / 64)) == 0 && kSmallRows / kSegRows <= 64" in src
+
+
+def test_product_library_reads_no_tuning_environment():
+    """the product library's level-1 geometry and partition tile size ignore the tuning
+    environment variables (only the variant builds of tools/build_variants.sh read them)."""
+    lib = os.path.join(PKG, "build", "librpt_gpu.so")
+    if not os.path.exists(lib):
+        pytest.skip("product library not built")
+    blob = open(lib, "rb").read()
+    for var in (b"RPT_L1_GROUPS_MIN_ROWS", b"RPT_TILE_MULT_SLICES"):
+        assert var not in blob, var

@@ -200,3 +200,65 @@ def test_clear_settled_by_a_reader_orders_other_streams(rpt):
     torch.cuda.synchronize()
     assert int(cnt.item()) == 0
     assert not out.any()
+
+
+@pytest.mark.parametrize("log_nb,n", [(14, 200_000), (21, 5_000_000)])  # LDS probe; partitioned probe
+def test_graph_capture_of_a_cleared_filter(rpt, log_nb, n):
+    """a probe captured into a HIP graph must not carry the deferred clear's zeroing (each replay
+    would wipe the bits inserted since). A capture that would have to settle the clear is refused
+    (RPT_ERR_INVALID_ARGUMENT, the capture itself stays valid); after rpt_bf_settle the probe captures, and
+    replays after later inserts see those inserts (the oracle's sel each time)."""
+    import ctypes
+
+    from rpt_amd._lib import RptError
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    for fn in ("hipStreamBeginCapture", "hipStreamEndCapture", "hipGraphInstantiate", "hipGraphLaunch",
+               "hipGraphExecDestroy", "hipGraphDestroy"):
+        getattr(hip, fn).restype = ctypes.c_int
+    bf = filled(rpt, log_nb)
+    bf.clear()
+    p = keys(n, 7)
+    b, c = keys(300_000, 8), keys(300_000, 9)
+    m = min(n // 10, b.size)
+    p[:m] = b[:m]  # some probe rows are B's keys, more are C's after the second insert
+    p[m: 2 * m] = c[:m]
+    kp = dev(p)
+    out_sel = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    out_count = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    ws = torch.empty(bf.workspace_bytes(n), dtype=torch.uint8, device="cuda:0")
+    s = torch.cuda.Stream(device="cuda:0")
+    sh = ctypes.c_void_p(s.cuda_stream)
+    graph, exe = ctypes.c_void_p(), ctypes.c_void_p()
+
+    def capture():
+        assert hip.hipStreamBeginCapture(sh, 2) == 0  # hipStreamCaptureModeRelaxed
+        err = None
+        try:
+            bf.probe_async(kp, n=n, out_sel=out_sel, out_count=out_count, workspace=ws, stream=s)
+        except RptError as e:
+            err = e
+        assert hip.hipStreamEndCapture(sh, ctypes.byref(graph)) == 0  # still a valid capture
+        return err
+
+    err = capture()
+    assert err is not None and err.status == 1 and "rpt_bf_settle" in str(err)
+    assert hip.hipGraphDestroy(graph) == 0
+    bf.settle()
+    bf.insert(dev(b))
+    assert capture() is None
+    assert hip.hipGraphInstantiate(ctypes.byref(exe), graph, None, None, ctypes.c_size_t(0)) == 0
+    ref = orc.new_words(log_nb)
+    orc.insert_keys(ref, log_nb, b)
+    for extra in (None, c):
+        if extra is not None:  # an insert between replays: the replay must see it, and nothing wiped
+            bf.insert(dev(extra))
+            orc.insert_keys(ref, log_nb, extra)
+        torch.cuda.synchronize()
+        assert hip.hipGraphLaunch(exe, sh) == 0
+        s.synchronize()
+        cnt = int(out_count.item())
+        want = orc.probe_keys(ref, log_nb, p)
+        assert np.array_equal(out_sel[:cnt].cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(bf.export_words(), ref)
+    assert hip.hipGraphExecDestroy(exe) == 0 and hip.hipGraphDestroy(graph) == 0

@@ -15,11 +15,16 @@ key min/max and has_data must be reduced:
   one 32-word slice granule;
 * C5's geometry: the 8 GiB / 2^30-block filter sized for 8e9 rows, W = 4;
 * an error injected inside a group: every rank fails with RPT_ERR_COLLECTIVE, every group is closed,
-  and the filters stay usable.
+  and the filters stay usable;
+* a silent peer (a rank that dies mid-merge without posting its side): the surviving ranks' grouped calls
+  "succeed" and their streams block, as with RCCL, so only the merge's bounded wait ends them: every
+  surviving rank aborts its communicator and returns RPT_ERR_COLLECTIVE within the collective timeout (at
+  once when RCCL reports the peer's death asynchronously), and no thread hangs.
 """
 import ctypes
 import os
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -32,9 +37,10 @@ pytestmark = pytest.mark.gpu
 
 LOOP_DIR = os.path.join(REPO, "tests", "loopback", "build")
 API_FIELDS = ["get_unique_id", "comm_init_rank", "comm_destroy", "group_start", "group_end", "send", "recv",
-              "all_reduce", "comm_count", "comm_user_rank", "error_string"]
+              "all_reduce", "comm_count", "comm_user_rank", "error_string", "comm_abort", "get_async_error"]
 LOOP_SYMBOLS = ["ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclGroupStart", "ncclGroupEnd",
-                "ncclSend", "ncclRecv", "ncclAllReduce", "ncclCommCount", "ncclCommUserRank", "ncclGetErrorString"]
+                "ncclSend", "ncclRecv", "ncclAllReduce", "ncclCommCount", "ncclCommUserRank", "ncclGetErrorString",
+                "ncclCommAbort", "ncclCommGetAsyncError"]
 ROUND_WORDS = 4 << 20  # RPT_ALLREDUCE_ROUND_WORDS
 RPT_ERR_COLLECTIVE = 6
 
@@ -56,6 +62,7 @@ def env():
     tlib.rpt_testing_set_rccl_api.argtypes = [ctypes.c_void_p]
     loop = ctypes.CDLL(os.path.join(LOOP_DIR, "librccl_loopback.so"))
     loop.rpt_loopback_fail_op.argtypes = [ctypes.c_int, ctypes.c_int]
+    loop.rpt_loopback_silent_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
     loop.rpt_loopback_group_depth.restype = ctypes.c_int
     loop.rpt_loopback_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     table = ApiTable(*[ctypes.cast(getattr(loop, s), ctypes.c_void_p) for s in LOOP_SYMBOLS])
@@ -64,7 +71,7 @@ def env():
     assert tlib.rpt_testing_set_rccl_api(None) == 0
 
 
-def in_threads(world, fn):
+def in_threads(world, fn, join_timeout=600):
     """Run fn(rank) on `world` threads (ctypes releases the GIL inside the library calls)."""
     errs = []
 
@@ -77,8 +84,9 @@ def in_threads(world, fn):
     ts = [threading.Thread(target=wrap, args=(r,)) for r in range(world)]
     for t in ts:
         t.start()
+    deadline = time.monotonic() + join_timeout
     for t in ts:
-        t.join(timeout=600)
+        t.join(timeout=max(0.0, deadline - time.monotonic()))
     assert not any(t.is_alive() for t in ts), "a rank thread hung"
     assert not errs, errs
 
@@ -270,3 +278,57 @@ def test_loopback_workspace_is_checked(env):
     in_threads(2, run)
     assert st == [4, 4]  # RPT_ERR_WORKSPACE, before any collective call
     destroy_comms(tlib, comms)
+
+
+@pytest.mark.parametrize("silent_rank,silent_op,report", [(1, 1, 0), (0, 0, 1), (2, 9, 0), (1, 4, 1)])
+def test_loopback_silent_peer_is_bounded(env, silent_rank, silent_op, report):
+    """A rank fails inside a group and goes silent (rpt_loopback_silent_peer): it never posts the rest of
+    its sends and tells nobody. The surviving ranks' ncclGroupEnd / ncclAllReduce return success and their
+    streams block, as RCCL's kernels would wait for the dead peer. rpt_bf_allreduce_or_ws must not wait
+    blindly: every rank returns RPT_ERR_COLLECTIVE, the survivors within the collective timeout (promptly
+    when ncclCommGetAsyncError reports the death), each communicator aborted (rpt_rccl_comm_destroy then
+    does nothing), no thread left hanging, and the filters usable afterwards."""
+    tlib, loop = env
+    world, log_nb, bound_ms = 3, 25, 3000  # 3 reduce-scatter rounds: op 9 lands in round 2
+    prev = tlib.rpt_collective_timeout_ms()
+    assert tlib.rpt_collective_set_timeout_ms(0) == 1  # RPT_ERR_INVALID_ARGUMENT
+    assert tlib.rpt_collective_set_timeout_ms(bound_ms) == 0
+    comms = make_comms(tlib, world)
+    bfs, _keys = build_partials(tlib, world, log_nb, 300_000, set())
+    need = tlib.rpt_allreduce_workspace_bytes(world, log_nb)
+    wss = [torch.empty(need, dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    streams = [torch.cuda.Stream(device="cuda:0") for _ in range(world)]
+    st, took, err, depth = [None] * world, [None] * world, [None] * world, [None] * world
+
+    def run(r):
+        t0 = time.monotonic()
+        st[r] = tlib.rpt_bf_allreduce_or_ws(bfs[r].handle, comms[r], wss[r].data_ptr(), need, streams[r].cuda_stream)
+        took[r] = time.monotonic() - t0
+        err[r] = tlib.rpt_last_error().decode(errors="replace")
+        depth[r] = loop.rpt_loopback_group_depth()
+
+    loop.rpt_loopback_silent_peer(silent_rank, silent_op, report)
+    try:
+        in_threads(world, run, join_timeout=bound_ms / 1000 * 4 + 30)
+    finally:
+        loop.rpt_loopback_silent_peer(-1, -1, 0)
+        assert tlib.rpt_collective_set_timeout_ms(prev) == 0
+    torch.cuda.synchronize()  # every stream drained: the aborts released the blocked ones
+    assert st == [RPT_ERR_COLLECTIVE] * world, err
+    assert depth == [0] * world
+    for r in range(world):
+        assert "communicator aborted" in err[r], err[r]
+        assert "did not drain" not in err[r], err[r]
+        if r == silent_rank:
+            continue
+        assert took[r] < bound_ms / 1000 + 10, (r, took[r])
+        if report:
+            assert "asynchronous error" in err[r] and took[r] < bound_ms / 1000, (r, took[r], err[r])
+        else:
+            assert "no progress within" in err[r] and took[r] >= bound_ms / 1000 * 0.9, (r, took[r], err[r])
+    for bf in bfs:  # still usable: its write order was released
+        bf.insert(torch.arange(1000, dtype=torch.int64, device="cuda:0"))
+        assert bf.export_words().any()
+    destroy_comms(tlib, comms)  # aborted communicators: accepted, nothing called
+    for bf in bfs:
+        bf.close()

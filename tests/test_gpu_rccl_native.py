@@ -6,9 +6,14 @@ callers) over a communicator from rpt_rccl_comm_init_rank.
 * two ranks, one GPU each (skipped on a one-GPU box: RCCL refuses two ranks on one device): every
   rank inserts its row-range shard, the merged filter equals the oracle's filter of all rows, and the
   key min/max / has_data are reduced (an empty rank included). The torch.distributed composition used
-  for gloo rehearsals is covered at world sizes 2-4 in tests/test_distributed_gloo.py."""
+  for gloo rehearsals is covered at world sizes 2-4 in tests/test_distributed_gloo.py;
+* bench.py's C5 section (the `c5_merge` object of an N > 1 run) end to end at N = 1 through a one-rank
+  communicator (`--c5-merge`, fewer rows per rank; the filter stays the 8 GiB one sized for 8e9 rows)."""
 import ctypes
+import json
 import os
+import subprocess
+import sys
 import tempfile
 
 import numpy as np
@@ -123,3 +128,17 @@ def test_two_rank_allreduce_matches_single_build(n_build, empty_rank):
         for p in procs:
             p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
+
+
+def test_bench_c5_merge_section_one_rank():
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--steps", "2", "--warmup", "1", "--probe-rows", "1e7",
+           "--no-cpu-baseline", "--c5-merge", "--c5-rows-per-rank", "2e7", "--collective-timeout-ms", "60000"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    c5 = line["c5_merge"]
+    assert c5["merge_check"].startswith("bit-identical"), c5
+    assert c5["filter_bytes"] == 8 << 30 and c5["rows_per_rank"] == 2 * 10**7 and c5["n_gpus"] == 1
+    assert len(c5["or_merge_ms_reps"]) == 3 and c5["or_merge_ms"] > 0 and c5["collective_timeout_ms"] == 60000
+    assert 0.09 < c5["survivors_rank0"] / c5["rows_per_rank"] < 0.2  # p = 0.1 plus the filter's false positives
