@@ -17,6 +17,7 @@
 //   merge   : OR of partial filters / peer slices;  fold;  popcount (misc.hpp).
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // ncclConfig_t / NCCL_CONFIG_INITIALIZER only: librccl itself is dlopened, never linked
 
 #include <algorithm>
 #include <atomic>
@@ -1619,6 +1620,7 @@ std::shared_ptr<const RcclApi> load_librccl() {
   sym(a->fn.error_string, "ncclGetErrorString");
   sym(a->fn.comm_abort, "ncclCommAbort");
   sym(a->fn.get_async_error, "ncclCommGetAsyncError");
+  sym(a->fn.comm_init_rank_config, "ncclCommInitRankConfig");
   return a;
 }
 
@@ -2011,13 +2013,39 @@ int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, 
   return RPT_OK;
 }
 
+int rpt_rccl_comm_init_rank_nonblocking(int device, int world, const uint8_t* id, int rank, void** out_comm) {
+  if (!id || !out_comm || world < 1 || rank < 0 || rank >= world)
+    return fail(RPT_ERR_INVALID_ARGUMENT, "bad communicator arguments (world %d, rank %d)", world, rank);
+  const std::shared_ptr<const RcclApi> api_p = rccl_api();
+  const rpt_rccl_api_table& api = api_p->fn;
+  if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
+  RPT_ON_DEVICE(device);
+  rpt_rccl_unique_id uid{};
+  std::memcpy(uid.internal, id, RPT_RCCL_UNIQUE_ID_BYTES);
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;  // every call may return ncclInProgress; the merge polls it against its deadline
+  void* comm = nullptr;
+  int rc = api.comm_init_rank_config(&comm, world, uid, rank, &cfg);
+  if (rc == kNcclInProgress && comm) rc = settle_nccl(api, comm, rc, coll_deadline());
+  if (rc != 0) {
+    if (comm) (void)api.comm_abort(comm);  // never handed out: nothing to record
+    return fail(RPT_ERR_COLLECTIVE, "ncclCommInitRankConfig (non-blocking): %s",
+                rc == kNcclInProgress ? "no completion within the collective timeout" : api.error_string(rc));
+  }
+  (void)take_aborted(comm);
+  *out_comm = comm;
+  return RPT_OK;
+}
+
 int rpt_rccl_comm_destroy(void* comm) {
   if (!comm) return RPT_OK;
   if (take_aborted(comm)) return RPT_OK;  // a failed merge aborted it: ncclCommAbort already freed it
   const std::shared_ptr<const RcclApi> api_p = rccl_api();
   const rpt_rccl_api_table& api = api_p->fn;
   if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
-  RPT_NCCL(api.comm_destroy(comm));
+  const int rc = api.comm_destroy(comm);
+  if (rc != 0 && rc != kNcclInProgress)  // a non-blocking communicator finishes tearing down on its own
+    return fail(RPT_ERR_COLLECTIVE, "ncclCommDestroy: %s", api.error_string(rc));
   return RPT_OK;
 }
 #undef RPT_NCCL_IN_GROUP

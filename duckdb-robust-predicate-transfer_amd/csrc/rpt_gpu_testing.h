@@ -42,6 +42,8 @@ typedef struct rpt_rccl_api_table {
   const char* (*error_string)(int result);                                         /* ncclGetErrorString */
   int (*comm_abort)(void* comm);                                                   /* ncclCommAbort */
   int (*get_async_error)(void* comm, int* async_error);                            /* ncclCommGetAsyncError */
+  int (*comm_init_rank_config)(void** comm, int nranks, rpt_rccl_unique_id id, int rank,
+                               void* config);                                      /* ncclCommInitRankConfig */
 } rpt_rccl_api_table;
 
 #ifdef RPT_TESTING_HOOKS

@@ -130,6 +130,7 @@ SIGNATURES = {
     "rpt_rccl_available": (c_int, [c_int]),
     "rpt_rccl_get_unique_id": (c_int, [c_void_p]),
     "rpt_rccl_comm_init_rank": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),
+    "rpt_rccl_comm_init_rank_nonblocking": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),
     "rpt_rccl_comm_destroy": (c_int, [c_void_p]),
     "rpt_words_or": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_words_or_slices": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p]),

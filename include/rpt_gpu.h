@@ -293,6 +293,11 @@ uint64_t rpt_collective_timeout_ms(void);
 int rpt_rccl_available(int device);
 int rpt_rccl_get_unique_id(uint8_t* out_id);
 int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, void** out_comm);
+/* The same as a NON-BLOCKING communicator (ncclCommInitRankConfig, blocking = 0): every RCCL call on it returns
+ * at once (ncclInProgress) and rpt_bf_allreduce_or[_ws] polls ncclCommGetAsyncError against the collective
+ * timeout, so even RCCL's host-side connection setup with a peer that died cannot block the caller past the
+ * bound (a blocking communicator's ncclGroupEnd can). Init itself completes within the timeout or fails. */
+int rpt_rccl_comm_init_rank_nonblocking(int device, int world, const uint8_t* id, int rank, void** out_comm);
 int rpt_rccl_comm_destroy(void* comm);
 /* dst[i] |= src[i] for n_words words (device pointers): the local step of the multi-GPU
  * OR all-reduce (reduce-scatter slices). */

@@ -15,6 +15,9 @@
 //       sender's stream waits on the done events of its sends (the buffer may be reused after).
 //       No host synchronization: every dependency is a stream-event wait.
 //   ncclAllReduce   int64/uint64 MIN / MAX / SUM, staged through the host (3 words in the product)
+//   ncclCommInitRankConfig   config->blocking == 0 makes a NON-BLOCKING communicator: init, ncclGroupEnd and
+//       ncclAllReduce do their work as above but return ncclInProgress, and ncclCommGetAsyncError reports
+//       ncclInProgress for two more polls before the call's result (so a caller's polling path runs)
 //   ncclCommAbort / ncclCommGetAsyncError   rank-local, as in RCCL: an abort frees that rank's communicator and
 //       releases only that rank's blocked streams (below); the asynchronous error is the world's (0 unless a
 //       silent peer was set to report)
@@ -44,7 +47,8 @@
 namespace {
 
 constexpr int kSuccess = 0, kUnhandledCudaError = 1, kInternalError = 3, kInvalidArgument = 4, kInvalidUsage = 5,
-              kRemoteError = 6;
+              kRemoteError = 6, kInProgress = 7;
+constexpr int kNonblockingPolls = 2;  // ncclCommGetAsyncError answers ncclInProgress this many times first
 constexpr int kInt64 = 4, kUint64 = 5;                 // ncclDataType_t
 constexpr int kSum = 0, kMax = 2, kMin = 3;            // ncclRedOp_t
 constexpr auto kBarrierTimeout = std::chrono::seconds(120);
@@ -86,7 +90,19 @@ struct Comm {
   std::shared_ptr<World> w;
   int rank, device;
   std::atomic<int> ops{0};
+  bool nonblocking = false;
+  std::atomic<int> polls{0};           // non-blocking: ncclInProgress answers left for the pending call
+  std::atomic<int> result{kSuccess};   // non-blocking: the pending call's result
 };
+
+// A non-blocking communicator's call has done its work: report ncclInProgress now and `rc` after the polls.
+std::atomic<int> g_stuck{0};  // rpt_loopback_stuck: non-blocking calls never leave ncclInProgress
+int complete(Comm* c, int rc) {
+  if (!c || !c->nonblocking) return rc;
+  c->result.store(rc);
+  c->polls.store(g_stuck.load() ? (1 << 30) : kNonblockingPolls);
+  return kInProgress;
+}
 
 struct Op {
   bool send;
@@ -273,6 +289,8 @@ const char* ncclGetErrorString(int r) {
     case kInternalError: return "internal error (loopback: injected failure or aborted world)";
     case kInvalidArgument: return "invalid argument (loopback)";
     case kInvalidUsage: return "invalid usage (loopback: unmatched or mismatched send/recv)";
+    case kRemoteError: return "remote error (loopback: a silent peer is gone)";
+    case kInProgress: return "in progress (loopback: non-blocking communicator)";
     default: return "unknown (loopback)";
   }
 }
@@ -286,7 +304,7 @@ int ncclGetUniqueId(UniqueId* id) {
   return kSuccess;
 }
 
-int ncclCommInitRank(void** comm, int nranks, UniqueId id, int rank) {
+static int init_rank(void** comm, int nranks, UniqueId id, int rank, bool nonblocking) {
   if (!comm || nranks < 1 || rank < 0 || rank >= nranks || std::memcmp(id.internal, "rptloop", 7) != 0)
     return kInvalidArgument;
   uint64_t key = 0;
@@ -307,6 +325,7 @@ int ncclCommInitRank(void** comm, int nranks, UniqueId id, int rank) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return kUnhandledCudaError;
   auto* c = new Comm{w, rank, dev};
+  c->nonblocking = nonblocking;
   std::unique_lock<std::mutex> lk(w->mu);
   w->joined++;
   w->live++;
@@ -316,12 +335,25 @@ int ncclCommInitRank(void** comm, int nranks, UniqueId id, int rank) {
     return kInternalError;
   }
   *comm = c;
-  return kSuccess;
+  return complete(c, kSuccess);
+}
+
+// rccl.h ncclConfig_t, as far as read here
+struct ConfigHead {
+  size_t size;
+  unsigned int magic, version;
+  int blocking;
+};
+
+int ncclCommInitRank(void** comm, int nranks, UniqueId id, int rank) { return init_rank(comm, nranks, id, rank, false); }
+
+int ncclCommInitRankConfig(void** comm, int nranks, UniqueId id, int rank, const ConfigHead* config) {
+  return init_rank(comm, nranks, id, rank, config != nullptr && config->blocking == 0);
 }
 
 // Frees the communicator; the last one of its world releases the world's events (the World itself lives
 // on while a blocked stream's host function still holds it).
-int release_comm(Comm* c, bool abort) {
+static int release_comm(Comm* c, bool abort) {
   std::shared_ptr<World> w = c->w;
   bool last = false;
   {
@@ -370,8 +402,13 @@ int ncclCommAbort(void* comm) {
 int ncclCommGetAsyncError(void* comm, int* async_error) {
   Comm* c = static_cast<Comm*>(comm);
   if (!c || !async_error) return kInvalidArgument;
+  if (c->nonblocking && c->polls.load() > 0) {
+    c->polls.fetch_sub(1);
+    *async_error = kInProgress;
+    return kSuccess;
+  }
   std::lock_guard<std::mutex> lk(c->w->mu);
-  *async_error = c->w->async_err;
+  *async_error = c->w->async_err != kSuccess ? c->w->async_err : (c->nonblocking ? c->result.load() : kSuccess);
   return kSuccess;
 }
 
@@ -405,7 +442,8 @@ int ncclGroupEnd() {
   Comm* err_comm = t_err_comm;
   t_err = false;
   t_err_comm = nullptr;
-  return run_group(ops, err, err_comm);
+  Comm* c0 = !ops.empty() ? ops[0].c : err_comm;
+  return complete(c0, run_group(ops, err, err_comm));
 }
 
 int ncclSend(const void* buf, size_t count, int dt, int peer, void* comm, hipStream_t stream) {
@@ -424,7 +462,7 @@ int ncclRecv(void* buf, size_t count, int dt, int peer, void* comm, hipStream_t 
   return rc != kSuccess ? rc : rc2;
 }
 
-int ncclAllReduce(const void* sendbuf, void* recvbuf, size_t count, int dt, int op, void* comm, hipStream_t stream) {
+static int all_reduce_impl(const void* sendbuf, void* recvbuf, size_t count, int dt, int op, void* comm, hipStream_t stream) {
   Comm* c = static_cast<Comm*>(comm);
   if (!c || (dt != kInt64 && dt != kUint64) || (op != kMin && op != kMax && op != kSum) || t_depth > 0)
     return kInvalidArgument;
@@ -473,6 +511,11 @@ int ncclAllReduce(const void* sendbuf, void* recvbuf, size_t count, int dt, int 
   return rc;
 }
 
+int ncclAllReduce(const void* sendbuf, void* recvbuf, size_t count, int dt, int op, void* comm, hipStream_t stream) {
+  const int rc = all_reduce_impl(sendbuf, recvbuf, count, dt, op, comm, stream);
+  return rc == kInvalidArgument ? rc : complete(static_cast<Comm*>(comm), rc);
+}
+
 // ---- test controls ----------------------------------------------------------------------------------
 // The k-th send/recv call (0-based, counted per communicator) of rank `rank` fails; (-1, -1) disarms.
 void rpt_loopback_fail_op(int rank, int k) {
@@ -489,6 +532,8 @@ void rpt_loopback_silent_peer(int rank, int k, int report) {
   g_fail_op.store(k);
   g_fail_rank.store(rank);
 }
+// on != 0: every later call on a non-blocking communicator stays ncclInProgress (a call that never completes).
+void rpt_loopback_stuck(int on) { g_stuck.store(on != 0); }
 // Group nesting depth of the calling thread (0 once every group is closed).
 int rpt_loopback_group_depth() { return t_depth; }
 // Grouped exchanges completed and bytes copied by the world of `comm`.

@@ -16,6 +16,8 @@ key min/max and has_data must be reduced:
 * C5's geometry: the 8 GiB / 2^30-block filter sized for 8e9 rows, W = 4;
 * an error injected inside a group: every rank fails with RPT_ERR_COLLECTIVE, every group is closed,
   and the filters stay usable;
+* non-blocking communicators (rpt_rccl_comm_init_rank_nonblocking): every grouped call and the all-reduce
+  return ncclInProgress and the merge polls them to completion; results as with blocking ones;
 * a silent peer (a rank that dies mid-merge without posting its side): the surviving ranks' grouped calls
   "succeed" and their streams block, as with RCCL, so only the merge's bounded wait ends them: every
   surviving rank aborts its communicator and returns RPT_ERR_COLLECTIVE within the collective timeout (at
@@ -37,10 +39,11 @@ pytestmark = pytest.mark.gpu
 
 LOOP_DIR = os.path.join(REPO, "tests", "loopback", "build")
 API_FIELDS = ["get_unique_id", "comm_init_rank", "comm_destroy", "group_start", "group_end", "send", "recv",
-              "all_reduce", "comm_count", "comm_user_rank", "error_string", "comm_abort", "get_async_error"]
+              "all_reduce", "comm_count", "comm_user_rank", "error_string", "comm_abort", "get_async_error",
+              "comm_init_rank_config"]
 LOOP_SYMBOLS = ["ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclGroupStart", "ncclGroupEnd",
                 "ncclSend", "ncclRecv", "ncclAllReduce", "ncclCommCount", "ncclCommUserRank", "ncclGetErrorString",
-                "ncclCommAbort", "ncclCommGetAsyncError"]
+                "ncclCommAbort", "ncclCommGetAsyncError", "ncclCommInitRankConfig"]
 ROUND_WORDS = 4 << 20  # RPT_ALLREDUCE_ROUND_WORDS
 RPT_ERR_COLLECTIVE = 6
 
@@ -63,6 +66,7 @@ def env():
     loop = ctypes.CDLL(os.path.join(LOOP_DIR, "librccl_loopback.so"))
     loop.rpt_loopback_fail_op.argtypes = [ctypes.c_int, ctypes.c_int]
     loop.rpt_loopback_silent_peer.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    loop.rpt_loopback_stuck.argtypes = [ctypes.c_int]
     loop.rpt_loopback_group_depth.restype = ctypes.c_int
     loop.rpt_loopback_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
     table = ApiTable(*[ctypes.cast(getattr(loop, s), ctypes.c_void_p) for s in LOOP_SYMBOLS])
@@ -91,14 +95,15 @@ def in_threads(world, fn, join_timeout=600):
     assert not errs, errs
 
 
-def make_comms(tlib, world):
+def make_comms(tlib, world, nonblocking=False):
     uid = (ctypes.c_uint8 * 128)()
     assert tlib.rpt_rccl_get_unique_id(uid) == 0, tlib.rpt_last_error()
     comms = [ctypes.c_void_p() for _ in range(world)]
     st = [None] * world
+    init_fn = tlib.rpt_rccl_comm_init_rank_nonblocking if nonblocking else tlib.rpt_rccl_comm_init_rank
 
     def init(r):
-        st[r] = tlib.rpt_rccl_comm_init_rank(0, world, uid, r, ctypes.byref(comms[r]))
+        st[r] = init_fn(0, world, uid, r, ctypes.byref(comms[r]))
 
     in_threads(world, init)
     assert st == [0] * world
@@ -332,3 +337,53 @@ def test_loopback_silent_peer_is_bounded(env, silent_rank, silent_op, report):
     destroy_comms(tlib, comms)  # aborted communicators: accepted, nothing called
     for bf in bfs:
         bf.close()
+
+
+@pytest.mark.parametrize("world,log_nb,n_build", [(3, 25, 3_000_000), (2, 14, 20_000)])
+def test_loopback_nonblocking_comms(env, world, log_nb, n_build):
+    """Non-blocking communicators: init, every ncclGroupEnd and the all-reduce return ncclInProgress and
+    report it twice more through ncclCommGetAsyncError (the loopback's emulation), so the merge's polling of
+    in-progress calls runs for every group; the merged filters equal the oracle's as with blocking ones."""
+    tlib, _loop = env
+    comms = make_comms(tlib, world, nonblocking=True)
+    bfs, keys = build_partials(tlib, world, log_nb, n_build, set())
+    st, _need = allreduce_all(tlib, bfs, comms)
+    assert st == [0] * world, tlib.rpt_last_error()
+    ref = orc.new_words(log_nb)
+    orc.insert_keys(ref, log_nb, keys)
+    for r, bf in enumerate(bfs):
+        assert np.array_equal(bf.export_words(), ref), f"rank {r} words"
+        assert bf.minmax() == orc.minmax(keys)
+    destroy_comms(tlib, comms)
+    for bf in bfs:
+        bf.close()
+
+
+def test_loopback_inprogress_forever_is_bounded(env):
+    """A non-blocking communicator whose grouped call never leaves ncclInProgress (one rank, so nothing else
+    waits): the merge polls it until the collective timeout, aborts the communicator and returns
+    RPT_ERR_COLLECTIVE; the filter stays usable and rpt_rccl_comm_destroy accepts the aborted handle."""
+    tlib, loop = env
+    bound_ms = 1500
+    prev = tlib.rpt_collective_timeout_ms()
+    comms = make_comms(tlib, 1, nonblocking=True)
+    bfs, _keys = build_partials(tlib, 1, 20, 100_000, set())
+    need = tlib.rpt_allreduce_workspace_bytes(1, 20)
+    ws = torch.empty(need, dtype=torch.uint8, device="cuda:0")
+    assert tlib.rpt_collective_set_timeout_ms(bound_ms) == 0
+    loop.rpt_loopback_stuck(1)
+    try:
+        t0 = time.monotonic()
+        st = tlib.rpt_bf_allreduce_or_ws(bfs[0].handle, comms[0], ws.data_ptr(), need, None)
+        took = time.monotonic() - t0
+        err = tlib.rpt_last_error().decode(errors="replace")
+    finally:
+        loop.rpt_loopback_stuck(0)
+        assert tlib.rpt_collective_set_timeout_ms(prev) == 0
+    assert st == RPT_ERR_COLLECTIVE and "communicator aborted" in err, err
+    assert bound_ms / 1000 * 0.9 <= took < bound_ms / 1000 + 10, took
+    torch.cuda.synchronize()
+    bfs[0].insert(torch.arange(1000, dtype=torch.int64, device="cuda:0"))
+    assert bfs[0].export_words().any()
+    destroy_comms(tlib, comms)
+    bfs[0].close()

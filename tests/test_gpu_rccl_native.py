@@ -2,7 +2,8 @@
 callers) over a communicator from rpt_rccl_comm_init_rank.
 
 * one rank: librccl loads, the collective runs, and the filter words, key min/max and has_data come
-  back unchanged (also with a communicator the caller created itself through librccl);
+  back unchanged (with a blocking and a non-blocking communicator the library made, and with one the caller
+  created itself through librccl);
 * two ranks, one GPU each (skipped on a one-GPU box: RCCL refuses two ranks on one device): every
   rank inserts its row-range shard, the merged filter equals the oracle's filter of all rows, and the
   key min/max / has_data are reduced (an empty rank included). The torch.distributed composition used
@@ -29,7 +30,7 @@ class _UniqueId(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]  # rccl.h NCCL_UNIQUE_ID_BYTES
 
 
-@pytest.fixture(scope="module", params=["library", "caller"])
+@pytest.fixture(scope="module", params=["library", "library-nonblocking", "caller"])
 def comm(request):
     if not torch.cuda.is_available():
         pytest.fail("gpu test run without a visible GPU")
@@ -38,10 +39,11 @@ def comm(request):
 
     lib = _lib.load()
     c = ctypes.c_void_p()
-    if request.param == "library":  # rpt_rccl_get_unique_id + rpt_rccl_comm_init_rank
+    if request.param.startswith("library"):  # rpt_rccl_get_unique_id + rpt_rccl_comm_init_rank[_nonblocking]
         uid = (ctypes.c_uint8 * 128)()
         assert lib.rpt_rccl_get_unique_id(uid) == 0, lib.rpt_last_error()
-        assert lib.rpt_rccl_comm_init_rank(0, 1, uid, 0, ctypes.byref(c)) == 0, lib.rpt_last_error()
+        init = lib.rpt_rccl_comm_init_rank_nonblocking if request.param.endswith("nonblocking") else lib.rpt_rccl_comm_init_rank
+        assert init(0, 1, uid, 0, ctypes.byref(c)) == 0, lib.rpt_last_error()
         yield c
         assert lib.rpt_rccl_comm_destroy(c) == 0
     else:  # a communicator the caller made itself (a DuckDB shim that owns one)

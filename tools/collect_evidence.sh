@@ -11,4 +11,4 @@ for c in "$@"; do
   grep '^{' "gpurun_out/bench_$c.json" > "profiles/$R/bench_$c.json"
   cp "gpurun_out/benchtrace_$c/bench_kernel_stats.csv" "profiles/$R/bench_${c}_kernel_stats.csv"
 done
-cp gpurun_out/gpu_tests.log "profiles/$R/gpu_tests.txt"
+if [ -f gpurun_out/gpu_tests.log ]; then cp gpurun_out/gpu_tests.log "profiles/$R/gpu_tests.txt"; fi
