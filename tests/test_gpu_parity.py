@@ -326,10 +326,16 @@ def _window_check(bf, w, lnb, probe_dev, sel, lo, hi):
     assert np.array_equal(sel[a:b], exp)
 
 
+def _i32_as_oracle(k):
+    """int32 keys as the oracle hashes them: zero-extended through uint32 (DuckDB's Hash<int32_t>)."""
+    return k.astype(np.int32).view(np.uint32).astype(np.int64)
+
+
 def _full_check(w, lnb, probe_dev, sel, piece=10**8):
     """Every row of the probe against the oracle: the column is copied back in `piece`-row slices and
     each slice's expected survivors (oracle LookupSel + slice offset) must equal the sel entries that
-    fall inside it. Slices are probed on host threads (ctypes releases the GIL)."""
+    fall inside it. Slices are probed on host threads (ctypes releases the GIL). int32 columns are
+    zero-extended for the oracle."""
     from concurrent.futures import ThreadPoolExecutor
 
     n = probe_dev.numel()
@@ -339,7 +345,8 @@ def _full_check(w, lnb, probe_dev, sel, piece=10**8):
         lo, keys = lo_keys
         return lo, orc.probe_keys(w, lnb, keys).astype(np.int64) + lo
 
-    jobs = ((lo, probe_dev[lo:min(lo + piece, n)].cpu().numpy()) for lo in range(0, n, piece))
+    conv = _i32_as_oracle if probe_dev.dtype == torch.int32 else (lambda k: k)
+    jobs = ((lo, conv(probe_dev[lo:min(lo + piece, n)].cpu().numpy())) for lo in range(0, n, piece))
     checked = 0
     with ThreadPoolExecutor(threads) as ex:
         for lo, exp in ex.map(one, jobs):
@@ -383,28 +390,38 @@ def test_full_size_probe_properties(rpt, n_probe, n_build, p, strategy):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("config,n_build,n_filter", [("C3", 10**8, 10**8), ("C5 share", 10**9, 8 * 10**9)])
+@pytest.mark.parametrize("config,n_build,n_filter", [("C3", 10**8, 10**8), ("C5 share", 10**9, 8 * 10**9),
+                                                     ("C2-i32", 10**7, 10**7)])
 def test_full_size_configs_every_row(rpt, config, n_build, n_filter):
-    """BASELINE C3 (1e8-key build, 128 MiB filter: partitioned, 32 Ki-row tiles) and one rank's share of
-    C5 (1e9 keys into the 8 GiB filter sized for 8e9: bucketed insert and probe) at full size, as
-    bench.py runs them (AUTO strategies): the filter word for word and every one of the 1e9 probe rows
-    against the oracle (built with host threads from the same synthetic streams)."""
+    """BASELINE C3 (1e8-key build, 128 MiB filter: partitioned, 32 Ki-row tiles), one rank's share of
+    C5 (1e9 keys into the 8 GiB filter sized for 8e9: bucketed insert and probe) and C2 with int32 keys
+    (JOB's INTEGER join keys: the synthetic streams truncated to int32, as bench.py --key-type i32) at
+    full size, as bench.py runs them (AUTO strategies): the filter word for word and every one of the 1e9
+    probe rows against the oracle (built with host threads from the same synthetic streams)."""
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     n_probe = 10**9
+    i32 = config.endswith("-i32")
     build = rpt.synth_build_keys(n_build)
+    if i32:
+        build = build.to(torch.int32)
     bf = rpt.BloomFilter(n_filter)
     bf.insert(build)
     del build
     lnb = bf.log_num_blocks
-    assert bf.probe_strategy_for(n_probe) == (3 if config == "C3" else 4)
+    assert bf.probe_strategy_for(n_probe) == (4 if config.startswith("C5") else 3)
     ow = orc.new_words(lnb)
-    orc.build_mt(ow, lnb, orc.synth_build_keys(n_build), threads)
+    okeys = orc.synth_build_keys(n_build)
+    orc.build_mt(ow, lnb, _i32_as_oracle(okeys) if i32 else okeys, threads)
+    del okeys
     got = torch.empty(bf.num_blocks, dtype=torch.int64, device="cuda:0")
     bf.copy_words_to(got)
     assert torch.equal(got, torch.from_numpy(ow.view(np.int64)).to("cuda:0")), "filter words differ from the oracle"
     del got
     torch.cuda.empty_cache()
     probe = rpt.synth_probe_keys(n_probe, n_build, 100)
+    if i32:
+        probe = probe.to(torch.int32)
+        torch.cuda.empty_cache()
     sel_t, cnt = bf.probe_async(probe)
     count = int(cnt.item())
     sel = sel_t[:count].cpu().numpy().astype(np.int64)
