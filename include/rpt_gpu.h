@@ -269,7 +269,10 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream);
  * or any error after the first collective call, the call ABORTS the communicator (ncclCommAbort, which
  * frees it: do not use it again; rpt_rccl_comm_destroy accepts it and does nothing), drains the streams
  * (bounded again) and returns RPT_ERR_COLLECTIVE. The filter then holds its own partial plus possibly some
- * peers' bits (never fewer bits than before the call): rebuild it, or merge again on a new communicator. */
+ * peers' bits (never fewer bits than before the call): rebuild it, or merge again on a new communicator.
+ * If even the aborted streams do not drain by the second deadline, the message says "streams did not
+ * drain": the workspace, `stream` and the filter stay in use by work that may never finish (later work
+ * ordered after them may never run; rpt_bf_allreduce_or then leaks its workspace rather than free it). */
 #define RPT_ALLREDUCE_ROUND_WORDS (4ULL << 20)
 size_t rpt_allreduce_workspace_bytes(int world, int log_num_blocks);
 int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t workspace_bytes,
