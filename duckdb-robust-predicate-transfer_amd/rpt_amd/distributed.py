@@ -79,7 +79,7 @@ class RcclComm:
     ID_BYTES = 128  # RPT_RCCL_UNIQUE_ID_BYTES
 
     def __init__(self, device: torch.device, group=None):
-        from ._lib import RptError, load
+        from ._lib import RPT_ERR_COLLECTIVE, RptError, load
 
         self._lib = load()
         self.handle = None
@@ -96,7 +96,8 @@ class RcclComm:
         ok = torch.tensor([1 if st == 0 else 0], dtype=torch.int64, device=self.device if on_device else "cpu")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
         if not int(ok.item()):
-            raise RptError(7, f"RCCL unavailable on {'this rank: ' + err if st != 0 else 'another rank'}")
+            where = "this rank: " + err if st != 0 else "another rank"
+            raise RptError(RPT_ERR_COLLECTIVE, f"RCCL unavailable on {where}")
         # 2. rank 0 draws the id; a status byte rides along, so a failure there reaches every rank
         uid = torch.zeros(self.ID_BYTES + 1, dtype=torch.uint8)
         err = ""
@@ -109,7 +110,7 @@ class RcclComm:
         dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         uid = t.cpu().contiguous()
         if int(uid[self.ID_BYTES]) != 0:
-            raise RptError(7, f"rpt_rccl_get_unique_id failed on rank 0{': ' + err if err else ''}")
+            raise RptError(RPT_ERR_COLLECTIVE, f"rpt_rccl_get_unique_id failed on rank 0{': ' + err if err else ''}")
         # 3. the collective init
         h = ctypes.c_void_p()
         st = self._lib.rpt_rccl_comm_init_rank(dev, self.world, uid.data_ptr(), self.rank, ctypes.byref(h))
