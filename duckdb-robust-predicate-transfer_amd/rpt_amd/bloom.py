@@ -292,6 +292,8 @@ class BloomFilter:
         if out_count is None:
             out_count = self._count
         ws = workspace if workspace is not None else self._ws.get_bytes(self.workspace_bytes(n))
+        if workspace is None and isinstance(stream, torch.cuda.Stream):
+            ws.record_stream(stream)  # the filter's workspace may be regrown (freed) while this probe runs
         check(self._lib.rpt_bf_probe(self._h, ctypes.byref(col), _ptr(row_sel), n, out_sel.data_ptr(),
                                      out_count.data_ptr(), ws.data_ptr(), ws.numel() * ws.element_size(),
                                      _stream(self.device, stream)))

@@ -268,6 +268,35 @@ def test_concurrent_inserts_on_two_streams(rpt):
     assert np.array_equal(bf.export_words(), w)
 
 
+def test_side_stream_probes_regrow_the_filter_workspace(rpt):
+    """probe_async on a side stream with the filter's own workspace, growing it between probes (the
+    smaller buffer is freed while the earlier probe may still run: the binding records the side stream on
+    it), while the current stream allocates; every result equals the oracle's."""
+    keys = orc.synth_build_keys(300000)
+    bf = rpt.BloomFilter(keys.size)
+    bf.insert(dev(keys))
+    lnb = orc.log_num_blocks(keys.size)
+    w = orc.new_words(lnb)
+    orc.insert_keys(w, lnb, keys)
+    s = torch.cuda.Stream()
+    sizes = (5000, 60000, 700000, 2100000)
+    probes = [orc.synth_probe_keys(n, keys.size, 300, start=7 * n) for n in sizes]
+    torch.cuda.synchronize()
+    outs = []
+    for p in probes:
+        t = dev(p)
+        s.wait_stream(torch.cuda.current_stream())
+        sel = torch.empty(p.size, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        bf.probe_async(t, out_sel=sel, out_count=cnt, stream=s)
+        for _ in range(4):  # churn the current stream's allocator while the probe runs
+            torch.empty(p.size * 3, dtype=torch.int64, device="cuda").fill_(-1)
+        outs.append((t, sel, cnt))
+    torch.cuda.synchronize()
+    for p, (_, sel, cnt) in zip(probes, outs):
+        assert np.array_equal(sel[: int(cnt.item())].cpu().numpy().view(np.uint32), orc.probe_keys(w, lnb, p))
+
+
 def test_empty_filter_and_empty_input(rpt):
     bf = rpt.BloomFilter(1000)
     assert bf.is_empty()
