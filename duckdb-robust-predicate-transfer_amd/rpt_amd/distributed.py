@@ -74,11 +74,14 @@ def or_allreduce_words(full: torch.Tensor, group=None, or_slices: Optional[OrSli
 class RcclComm:
     """An RCCL communicator created by librpt_gpu.so for the ranks of a torch.distributed group (one GPU
     per rank): rank 0 draws the unique id (rpt_rccl_get_unique_id), the group broadcasts it, every rank
-    joins with rpt_rccl_comm_init_rank. Pass `.handle` to rpt_bf_allreduce_or (allreduce_or_native)."""
+    joins with rpt_rccl_comm_init_rank. Pass `.handle` to rpt_bf_allreduce_or (allreduce_or_native).
+    nonblocking=True joins with rpt_rccl_comm_init_rank_nonblocking instead: every RCCL call on the
+    communicator returns at once and the merge polls it against the collective timeout, so even RCCL's
+    host-side connection setup with a dead peer cannot block a rank past that bound."""
 
     ID_BYTES = 128  # RPT_RCCL_UNIQUE_ID_BYTES
 
-    def __init__(self, device: torch.device, group=None):
+    def __init__(self, device: torch.device, group=None, *, nonblocking: bool = False):
         from ._lib import RPT_ERR_COLLECTIVE, RptError, load
 
         self._lib = load()
@@ -113,13 +116,14 @@ class RcclComm:
             raise RptError(RPT_ERR_COLLECTIVE, f"rpt_rccl_get_unique_id failed on rank 0{': ' + err if err else ''}")
         # 3. the collective init
         h = ctypes.c_void_p()
-        st = self._lib.rpt_rccl_comm_init_rank(dev, self.world, uid.data_ptr(), self.rank, ctypes.byref(h))
+        init = self._lib.rpt_rccl_comm_init_rank_nonblocking if nonblocking else self._lib.rpt_rccl_comm_init_rank
+        st = init(dev, self.world, uid.data_ptr(), self.rank, ctypes.byref(h))
         if st != 0:
             raise RptError(st, self._lib.rpt_last_error().decode(errors="replace"))
         self.handle = h
 
     @classmethod
-    def single(cls, device: torch.device) -> "RcclComm":
+    def single(cls, device: torch.device, *, nonblocking: bool = False) -> "RcclComm":
         """A one-rank communicator without a torch.distributed group (bench.py --c5-merge at N = 1: the
         merge's min/max all-reduce and bounded wait run through real RCCL; no peer words move)."""
         from ._lib import RptError, load
@@ -132,8 +136,9 @@ class RcclComm:
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
         uid = (ctypes.c_uint8 * cls.ID_BYTES)()
         h = ctypes.c_void_p()
+        init = self._lib.rpt_rccl_comm_init_rank_nonblocking if nonblocking else self._lib.rpt_rccl_comm_init_rank
         for call in (lambda: self._lib.rpt_rccl_available(dev), lambda: self._lib.rpt_rccl_get_unique_id(uid),
-                     lambda: self._lib.rpt_rccl_comm_init_rank(dev, 1, uid, 0, ctypes.byref(h))):
+                     lambda: init(dev, 1, uid, 0, ctypes.byref(h))):
             st = call()
             if st != 0:
                 raise RptError(st, self._lib.rpt_last_error().decode(errors="replace"))

@@ -3,7 +3,8 @@ callers) over a communicator from rpt_rccl_comm_init_rank.
 
 * one rank: librccl loads, the collective runs, and the filter words, key min/max and has_data come
   back unchanged (with a blocking and a non-blocking communicator the library made, and with one the caller
-  created itself through librccl);
+  created itself through librccl), and through the Python binding's RcclComm.single (blocking and
+  non-blocking) with a caller-allocated merge workspace;
 * two ranks, one GPU each (skipped on a one-GPU box: RCCL refuses two ranks on one device): every
   rank inserts its row-range shard, the merged filter equals the oracle's filter of all rows, and the
   key min/max / has_data are reduced (an empty rank included). The torch.distributed composition used
@@ -81,6 +82,29 @@ def test_single_rank_allreduce_is_identity(rpt, comm, n_keys):
     assert (not bf.is_empty()) == before_has
     if n_keys:
         assert before_mm == (int(keys.view(np.int64).min()), int(keys.view(np.int64).max()))
+
+
+@pytest.mark.parametrize("nonblocking", [False, True])
+def test_rccl_comm_single_through_python(rpt, nonblocking):
+    """rpt_amd.distributed.RcclComm.single (bench.py --c5-merge at N = 1), blocking and non-blocking, with
+    allreduce_or_native and a caller-allocated workspace: the merged filter is the rank's own."""
+    from rpt_amd.distributed import RcclComm, allreduce_or_native, allreduce_workspace
+
+    comm = RcclComm.single(torch.device("cuda", 0), nonblocking=nonblocking)
+    try:
+        keys = orc.synth_build_keys(250000)
+        bf = rpt.BloomFilter(keys.size)
+        bf.insert(torch.from_numpy(keys.view(np.int64)).to("cuda:0"))
+        ws = allreduce_workspace(bf, comm)
+        for _ in range(2):  # OR is idempotent: a second merge changes nothing
+            allreduce_or_native(bf, comm, workspace=ws)
+        lnb = bf.log_num_blocks
+        ref = orc.new_words(lnb)
+        orc.insert_keys(ref, lnb, keys)
+        assert np.array_equal(bf.export_words(), ref)
+        assert bf.minmax() == orc.minmax(keys) and not bf.is_empty()
+    finally:
+        comm.close()
 
 
 def _two_rank_worker(rank, world, store_path, n_build, empty_rank, q):
