@@ -109,6 +109,13 @@ __host__ __device__ constexpr uint64_t partition_lds_bytes(uint32_t n_slices, ui
 // atomics serialize (P = 2: 4.3 ms per 1e9 rows, P = 4: 2.9 ms, P >= 8: 2.3-2.5 ms). Each lane then counts
 // its rows per slice in registers, a wave adds its totals with one atomic per slice, and rows take
 // positions from per-lane cursors (wave base + DPP prefix over lanes).
+// NOPARK (int32 keys, dense, TM = 1, SP = 0): the records stay in registers between the passes instead of
+// being parked in LDS (16 VGPRs: the int32 kernel fits them within the 64 of two workgroups per CU, 63 used;
+// the int64 kernel does not). The int32 partition is bound by its LDS ops, not by HBM: 1.84 ->
+// 1.79 ms per 1e9 rows (profiles/r04/ab_part_nopark.txt).
+#ifndef RPT_PART_NOPARK
+#define RPT_PART_NOPARK 1
+#endif
 template <int K, bool DENSE, bool MM, int TM, int SP = 0>
 __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4) void partition_kernel(
     KeyArgs a, uint64_t n, uint32_t slice_mask, uint64_t n_tiles, uint32_t* __restrict__ recs,
@@ -122,6 +129,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
   constexpr bool PAD = TM == 1;
   constexpr uint64_t kTR = kTileRows * TM;               // rows of this tile
   constexpr int kRPT = static_cast<int>(kTR / kTileThreads), kSPW = kRPT / 8;
+  constexpr bool NOPARK = RPT_PART_NOPARK && K == 1 && TM == 1 && SP == 0 && DENSE;  // records stay in registers
   extern __shared__ uint32_t s_dyn[];
   const uint32_t n_slices = slice_mask + 1;
   const uint64_t tile_cap = tile_cap_for(n_slices, TM);
@@ -137,10 +145,11 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
     for (uint32_t i = threadIdx.x; i < n_slices; i += kTileThreads) s_cnt[i] = 0;
     __syncthreads();
     const uint64_t tile_base = tile * kTR;
-    // pass 1: hash, stage the record at its row position in LDS, count rows per slice; only the 16-bit
-    // slice ids stay in registers (2 per word).
+    // pass 1: hash, stage the record in LDS (NOPARK: in rec[]), count rows per slice; the 16-bit slice ids
+    // stay in registers (2 per word).
     static_assert(kMaxSliceCount <= 65536, "slice ids are packed as 16 bits");
     uint32_t sl2[kRPT / 2] = {};
+    uint32_t rec[kRPT];  // pass 2's records (NOPARK: already pass 1's)
     [[maybe_unused]] uint32_t lc[SP > 0 ? SP : 1] = {};  // SP: this lane's rows per slice
     int64_t wmn = kMinInit, wmx = kMaxInit;  // wave-uniform: the key min/max stays out of VGPRs
 #pragma unroll
@@ -164,7 +173,8 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const uint32_t sl = static_cast<uint32_t>(hh[j] >> (kLogNumMasks + 6 + kSliceLog)) & slice_mask;
-        s_rec[seg_local + park_slot<K, DENSE>(j, lane)] = slice_record(hh[j]);
+        if constexpr (NOPARK) rec[sg * 8 + j] = slice_record(hh[j]);
+        else s_rec[seg_local + park_slot<K, DENSE>(j, lane)] = slice_record(hh[j]);
         sl2[(sg * 8 + j) >> 1] |= sl << (16 * (j & 1));
         if constexpr (SP > 0) {
 #pragma unroll
@@ -221,10 +231,9 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
 #define RPT_EXP_PART_STOP 0  // measurement only: 1 = stop after pass 1 + the scans, 2 = after the scatter
 #endif
     if (RPT_EXP_PART_STOP == 1) return;
-    // pass 2: pull this thread's records back out of the row-ordered staging ...
-    uint32_t rec[kRPT];
+    // pass 2: pull this thread's records back out of the row-ordered staging (NOPARK: nothing to pull) ...
 #pragma unroll
-    for (int sg = 0; sg < kSPW; sg++) {
+    for (int sg = 0; sg < (NOPARK ? 0 : kSPW); sg++) {
       const uint32_t seg_local = wave * (kSPW * kSegRows) + sg * kSegRows;
 #pragma unroll
       for (int j = 0; j < 8; j++) rec[sg * 8 + j] = s_rec[seg_local + park_slot<K, DENSE>(j, lane)];
