@@ -109,10 +109,12 @@ __host__ __device__ constexpr uint64_t partition_lds_bytes(uint32_t n_slices, ui
 // atomics serialize (P = 2: 4.3 ms per 1e9 rows, P = 4: 2.9 ms, P >= 8: 2.3-2.5 ms). Each lane then counts
 // its rows per slice in registers, a wave adds its totals with one atomic per slice, and rows take
 // positions from per-lane cursors (wave base + DPP prefix over lanes).
-// NOPARK (int32 keys, dense, TM = 1, SP = 0): the records stay in registers between the passes instead of
-// being parked in LDS (16 VGPRs: the int32 kernel fits them within the 64 of two workgroups per CU, 63 used;
-// the int64 kernel does not). The int32 partition is bound by its LDS ops, not by HBM: 1.84 ->
-// 1.79 ms per 1e9 rows (profiles/r04/ab_part_nopark.txt).
+// NOPARK (dense keys, SP = 0; TM = 1 only for int32 keys): the records stay in registers between the passes
+// instead of being parked in LDS. TM = 1: 16 VGPRs, which the int32 kernel fits within the 64 of two
+// workgroups per CU (63 used; the int64 kernel does not); its partition is bound by its LDS ops, not by HBM
+// (DESIGN §5): 1.84 -> 1.79 ms per 1e9 rows (profiles/r04/ab_part_nopark.txt). TM = 2 (one workgroup per CU,
+// 128 VGPRs): 32 VGPRs, 115 used: C3 int32 partition 2.37 -> 2.26-2.28 ms, int64 2.64 -> 2.60-2.64, builds
+// -5 % (profiles/r04/ab_part_nopark_tm2.txt).
 #ifndef RPT_PART_NOPARK
 #define RPT_PART_NOPARK 1
 #endif
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
   constexpr bool PAD = TM == 1;
   constexpr uint64_t kTR = kTileRows * TM;               // rows of this tile
   constexpr int kRPT = static_cast<int>(kTR / kTileThreads), kSPW = kRPT / 8;
-  constexpr bool NOPARK = RPT_PART_NOPARK && K == 1 && TM == 1 && SP == 0 && DENSE;  // records stay in registers
+  constexpr bool NOPARK = RPT_PART_NOPARK && ((K == 1 && TM == 1) || TM == 2) && SP == 0 && DENSE;  // records stay in registers
   extern __shared__ uint32_t s_dyn[];
   const uint32_t n_slices = slice_mask + 1;
   const uint64_t tile_cap = tile_cap_for(n_slices, TM);
