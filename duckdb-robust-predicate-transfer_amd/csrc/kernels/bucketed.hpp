@@ -77,6 +77,12 @@ __device__ __forceinline__ void l1_flag_error(const L1Lists& L) {
   __hip_atomic_store(L.error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The scatter's row map (pos_out) leaves as one 2V-byte store per lane for dense keys (1), non-temporal like
+// the partition's (2), or as V strided u16 stores (0): scatter 2.967-3.006 -> 2.940-2.969 ms with 2, C5 share
+// 8.47-8.52 -> 8.44-8.47 ms (profiles/r04/ab_scatter_pos_pack.txt).
+#ifndef RPT_SCATTER_POS_PACK
+#define RPT_SCATTER_POS_PACK 2
+#endif
 // B1: one pass over a 16 Ki-row level-1 tile: hash every row (held in registers), rank it within its
 // bucket (LDS atomic), append each bucket's run to its list (see above), sort the tile's hashes by
 // bucket in LDS and copy them to their list positions as the level-2 kKeySplit layout: hash bits 0..31
@@ -173,7 +179,25 @@ __global__ __launch_bounds__(kTileThreads) void bucket_scatter_kernel(KeyArgs a,
       }
       pv[j] = static_cast<uint16_t>(p);
     }
-    if (pos_out != nullptr) {  // padded to whole tiles: rows >= n get don't-care values
+    if (pos_out == nullptr) {  // padded to whole tiles: rows >= n get don't-care values
+    } else if constexpr (DENSE && RPT_SCATTER_POS_PACK) {
+      // a lane's V adjacent rows leave as one 2V-byte store (one coalesced 128 / 256-B piece per
+      // instruction instead of V strided u16 stores that each half-fill their lines)
+      constexpr int V = KeyTraits<K>::kVec;
+#pragma unroll
+      for (int c = 0; c < 8 / V; c++) {
+        const uint64_t row0 = sbase + static_cast<uint64_t>(c) * 64 * V + static_cast<uint64_t>(lane) * V;
+        if constexpr (V == 2) {
+          part_store<RPT_SCATTER_POS_PACK == 2>(reinterpret_cast<uint32_t*>(pos_out + row0),
+                                                static_cast<uint32_t>(pv[c * 2]) | (static_cast<uint32_t>(pv[c * 2 + 1]) << 16));
+        } else {
+          part_store<RPT_SCATTER_POS_PACK == 2>(reinterpret_cast<uint64_t*>(pos_out + row0),
+                                                static_cast<uint64_t>(pv[c * 4]) | (static_cast<uint64_t>(pv[c * 4 + 1]) << 16) |
+                                                    (static_cast<uint64_t>(pv[c * 4 + 2]) << 32) |
+                                                    (static_cast<uint64_t>(pv[c * 4 + 3]) << 48));
+        }
+      }
+    } else {
 #pragma unroll
       for (int j = 0; j < 8; j++) pos_out[sbase + seg_row<K, DENSE>(j, lane)] = pv[j];
     }
