@@ -151,6 +151,26 @@ def test_large_filters_vs_oracle(rpt, strategy, log_nb):
     assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
 
 
+@pytest.mark.parametrize("log_nb", [21, 22, 24])
+@pytest.mark.parametrize("nulls", [False, True])
+def test_large_filters_int32_vs_oracle(rpt, log_nb, nulls):
+    """int32 keys through the partitioned probe at 128, 256 and 1024 slices (16 and 32 Ki-row tiles: the
+    partition keeps its records in registers for both), ragged last tile, optionally with NULL keys."""
+    rng = np.random.default_rng(log_nb + 100 * nulls)
+    build = rng.integers(-2**31, 2**31, size=250000, dtype=np.int64).astype(np.int32)
+    probe = np.concatenate([build[rng.integers(0, build.size, size=300000)],
+                            rng.integers(-2**31, 2**31, size=5 * 16384 * 2 + 12345, dtype=np.int64).astype(np.int32)])
+    rng.shuffle(probe)
+    vw = gu.validity_words(rng.random(probe.size) > 0.02) if nulls else None
+    bf = with_strategy(rpt.BloomFilter(log_num_blocks=log_nb), "partitioned")
+    bf.insert(dev(build))
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, build)
+    assert np.array_equal(bf.export_words(), w)
+    sel = bf.lookup_sel(dev(probe), validity=dev(vw) if nulls else None).cpu().numpy().view(np.uint32)
+    assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe, validity=vw))
+
+
 @pytest.mark.parametrize("strategy", list(STRATEGIES))
 def test_dictionary_validity_rowsel_vs_oracle(rpt, strategy):
     rng = np.random.default_rng(7)
