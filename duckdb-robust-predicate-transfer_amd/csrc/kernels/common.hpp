@@ -143,6 +143,12 @@ __device__ __forceinline__ bool valid_at(const uint64_t* validity, uint64_t idx)
 //  GENERAL (dictionary key_sel and/or row_sel):        row(c) = base + c*64 + lane.
 // MM: also fold the valid (non-NULL, in-range) key values into mm[0] = min, mm[1] = max (the build's
 // min/max dynamic filter, physical_create_bf.cpp:82-119, fused into the key read).
+// MM over a full NULL-free segment of the batched loads (the bucketed level-1 scatter of a build): a
+// tournament over the lane's 8 values instead of a guarded min and max per value (VGPRs 111 -> 86): C5
+// build 7.58-7.65 -> 7.43-7.50 ms on one box (profiles/r04/ab_mm_tournament.txt).
+#ifndef RPT_MM_TOURNAMENT
+#define RPT_MM_TOURNAMENT 1
+#endif
 template <int K, bool DENSE, bool MM = false, bool NT = false, bool BATCH = false>
 __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uint64_t n, uint32_t lane,
                                             uint64_t (&h)[8], bool (&ok)[8], int64_t* mm = nullptr) {
@@ -211,10 +217,38 @@ __device__ __forceinline__ void load_hashes(const KeyArgs& a, uint64_t base, uin
         if constexpr (K == kKeySplit) hv |= static_cast<uint64_t>((hi4[c] >> (8 * e)) & 0xFFu) << 32;
         if (Tr::kValues && !((vbits[c] >> e) & 1u)) hv = kNullHash;
         h[c * V + e] = hv;
-        if constexpr (MM && Tr::kValues) {
+        if constexpr (MM && Tr::kValues && !RPT_MM_TOURNAMENT) {
           if (off + e < rem && ((vbits[c] >> e) & 1u)) {
             mm[0] = min(mm[0], static_cast<int64_t>(v[c * V + e]));
             mm[1] = max(mm[1], static_cast<int64_t>(v[c * V + e]));
+          }
+        }
+      }
+    }
+    if constexpr (MM && Tr::kValues && RPT_MM_TOURNAMENT) {
+      if (rem == static_cast<uint32_t>(kSegRows) && vb == nullptr) {
+        // a full segment without NULLs (uniform): the 8 values' min and max by a tournament (one compare
+        // per pair yields both, then 3 + 3), instead of a guarded min and max per value
+        int64_t lo[4], hi[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int64_t x = static_cast<int64_t>(v[2 * q]), y = static_cast<int64_t>(v[2 * q + 1]);
+          const bool lt = x < y;
+          lo[q] = lt ? x : y;
+          hi[q] = lt ? y : x;
+        }
+        mm[0] = min(mm[0], min(min(lo[0], lo[1]), min(lo[2], lo[3])));
+        mm[1] = max(mm[1], max(max(hi[0], hi[1]), max(hi[2], hi[3])));
+      } else {
+#pragma unroll
+        for (int c = 0; c < C; c++) {
+          const uint32_t off = static_cast<uint32_t>(c * 64 * V) + lane * V;
+#pragma unroll
+          for (int e = 0; e < V; e++) {
+            if (off + e < rem && ((vbits[c] >> e) & 1u)) {
+              mm[0] = min(mm[0], static_cast<int64_t>(v[c * V + e]));
+              mm[1] = max(mm[1], static_cast<int64_t>(v[c * V + e]));
+            }
           }
         }
       }

@@ -70,7 +70,8 @@ static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG 
 static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
                   RPT_NT_REC_LOADS == 0 && RPT_NT_SLICE_LOADS == 1 && RPT_PARK_LANE_MAJOR == 1 && RPT_SLICE_XCD_MAP == 1 &&
                   RPT_PARTITION_SMALL_P == 1 && RPT_VALU_INTERLEAVE == 1 && RPT_SEL_BALLOT_EXPAND == 1 &&
-                  RPT_DPP_MINMAX == 1 && RPT_DPP_SCAN == 1 && RPT_PART_NOPARK == 1 && RPT_SCATTER_POS_PACK == 2,
+                  RPT_DPP_MINMAX == 1 && RPT_DPP_SCAN == 1 && RPT_PART_NOPARK == 1 && RPT_SCATTER_POS_PACK == 2 &&
+                  RPT_MM_TOURNAMENT == 1,
               "product build: tuning switches must keep their tested defaults (use tools/build_variants.sh)");
 #endif
 
