@@ -20,13 +20,15 @@ is OR-merged through the C-ABI's rpt_bf_allreduce_or over an RCCL communicator t
 (the product path a C++ caller gets), checked bit-identical to a single-GPU build of all rows, and
 every rank probes its own 1e9-row slice of the global probe column (weak scaling, no data-path
 collective in the probe). A communicator that cannot be built ends the run with a non-zero exit on
-every rank. RPT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (the merge then runs the
-torch.distributed composition over host memory, reported as torch_merge_ms).
+every rank. RPT_BENCH_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share devices; every merge,
+the C5 section's included, then runs the torch.distributed composition over host memory, reported as
+torch_merge_ms, never as or_merge_ms).
 
 At N > 1 (and with --c5-merge at N = 1) the line also carries `c5_merge`: the north_star's C5 pipeline at
 this node's N, after the headline is timed: every rank inserts its 1e9-row shard into an 8 GiB filter sized
 for 8e9 rows, rpt_bf_allreduce_or_ws OR-merges the partials over RCCL (xGMI), the merged filter is checked
-bit-identical to a single build of all N * 1e9 rows, and every rank probes its 1e9-row slice against it.
+bit-identical to a single build of all N * 1e9 rows, and every rank probes its 1e9-row slice against it. The
+record carries each rank's peak device memory over the section (hipMemGetInfo) and the section's wall time.
 
 Prints ONE JSON line on rank 0. `roofline` prices the dominant kernel from HIP events the library
 records on the launch stream (rpt_profiling_*) and its PMC traffic from profiles/pmc/<config>.json
@@ -134,38 +136,84 @@ def algorithmic_bytes(kernel: str, n: int, survivors: int, key_bytes: int = KEY_
 
 
 def c5_merge_record(world: int, filter_bytes: int, rows_per_rank: int, insert_ms: float, merge_ms: list,
-                    probe_ms: float, survivors: int, merge_check: str, timeout_ms: int) -> dict:
+                    probe_ms: float, survivors: int, merge_check: str, timeout_ms, native: bool = True,
+                    merge_path: str = "", mem: dict = None, wall_s: float = None) -> dict:
     """The `c5_merge` object of the bench line (times are the max over ranks). The merge moves 2 (W-1)/W of
-    the filter per GPU, 2 S / W over each of its W-1 point-to-point xGMI links."""
+    the filter per GPU, 2 S / W over each of its W-1 point-to-point xGMI links. Only the product
+    merge (rpt_bf_allreduce_or_ws over RCCL, native=True) reports or_merge_*; the torch.distributed
+    composition (the gloo rehearsal, --merge torch) reports torch_merge_ms instead."""
     t = statistics.median(merge_ms) if merge_ms else None
-    return {
+    rec = {
         "what": ("BASELINE config 4 (C5) at this node's N: every rank inserts its shard of the N x rows_per_rank "
-                 "build column into a filter sized for 8e9 rows, rpt_bf_allreduce_or_ws OR-merges the partials "
-                 "over RCCL, every rank probes its rows_per_rank-row slice against the merged filter"),
+                 "build column into a filter sized for 8e9 rows, the partials are OR-merged, every rank probes "
+                 "its rows_per_rank-row slice against the merged filter"),
         "n_gpus": world,
         "filter_bytes": filter_bytes,
         "rows_per_rank": rows_per_rank,
         "build_rows": world * rows_per_rank,
         "insert_ms": insert_ms,
-        "or_merge_ms": t * 1e3 if t else None,
-        "or_merge_ms_reps": [m * 1e3 for m in merge_ms],
-        "or_merge_GBps_per_gpu": 2 * (world - 1) / world * filter_bytes / t / 1e9 if t and world > 1 else None,
-        "or_merge_GBps_per_link": 2 / world * filter_bytes / t / 1e9 if t and world > 1 else None,
+        "merge_path": merge_path,
+        "or_merge_ms": t * 1e3 if t and native else None,
+        "or_merge_ms_reps": [m * 1e3 for m in merge_ms] if native else None,
+        "or_merge_GBps_per_gpu": 2 * (world - 1) / world * filter_bytes / t / 1e9 if t and world > 1 and native else None,
+        "or_merge_GBps_per_link": 2 / world * filter_bytes / t / 1e9 if t and world > 1 and native else None,
+        "torch_merge_ms": t * 1e3 if t and not native else None,
+        "torch_merge_ms_reps": [m * 1e3 for m in merge_ms] if not native else None,
         "probe_ms": probe_ms,
         "probe_keys_per_s_node": world * rows_per_rank / (probe_ms * 1e-3) if probe_ms else None,
         "survivors_rank0": survivors,
         "merge_check": merge_check,
         "collective_timeout_ms": timeout_ms,
     }
+    if mem is not None:
+        rec["device_memory"] = mem
+    if wall_s is not None:
+        rec["wall_s"] = wall_s
+    return rec
 
 
-def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max, all_ok) -> dict:
-    """C5 build + product merge + probe (see the module docstring). Collective: every rank runs it."""
+class DeviceMemTracker:
+    """Peak device memory in use (hipMemGetInfo through torch.cuda.mem_get_info: total - free, so it counts the
+    library's own hipMalloc'd filters as well as torch's cached blocks) sampled at the phase boundaries of the
+    C5 section. On a device shared by several ranks (the gloo rehearsal) the figure is the device's, not the
+    rank's."""
+
+    def __init__(self, device, progress: bool = False):
+        import torch
+
+        self._torch = torch
+        self.progress = progress  # rank 0: one stderr line per phase (a long rehearsal shows it is alive)
+        self.t0 = time.perf_counter()
+        self.device = device
+        free, self.total = torch.cuda.mem_get_info(device)
+        self.base = self.total - free
+        self.peak = self.base
+        self.phases = {}
+
+    def sample(self, phase: str) -> None:
+        self._torch.cuda.synchronize(self.device)
+        free, _ = self._torch.cuda.mem_get_info(self.device)
+        used = self.total - free
+        self.phases[phase] = used
+        self.peak = max(self.peak, used)
+        if self.progress:
+            print(f"[bench c5] {phase} done at {time.perf_counter() - self.t0:.1f} s, device memory in use "
+                  f"{used / 2**30:.1f} GiB", file=sys.stderr, flush=True)
+
+
+def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max, all_ok, gather_ints,
+                 merge_path: str, shared_device_ranks: int = 1) -> dict:
+    """C5 build + merge + probe (see the module docstring). Collective: every rank runs it. `comm` is the
+    RcclComm of the product merge (rpt_bf_allreduce_or_ws), or None for the torch.distributed composition
+    (the gloo rehearsal / --merge torch; reported as torch_merge_ms)."""
     import torch
 
     import rpt_amd
-    from rpt_amd.distributed import allreduce_or_native, allreduce_workspace
+    from rpt_amd.distributed import allreduce_or_filter, allreduce_or_native, allreduce_workspace
 
+    t_section = time.perf_counter()
+    mem = DeviceMemTracker(device, progress=rank == 0)
+    native = comm is not None
     rows = int(args.c5_rows_per_rank)
     bf = rpt_amd.BloomFilter(C5_FILTER_ROWS, device=device)
     keys = rpt_amd.synth_build_keys(rows, start=rank * rows, device=device)
@@ -177,14 +225,25 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
     bf.insert(keys)
     torch.cuda.synchronize()
     insert_s = time.perf_counter() - t0
-    ws = allreduce_workspace(bf, comm)
-    allreduce_or_native(bf, comm, workspace=ws)  # warm-up merge: OR is idempotent, the words do not change
+    mem.sample("insert")
+    if native:
+        ws = allreduce_workspace(bf, comm)
+
+        def merge():
+            allreduce_or_native(bf, comm, workspace=ws)
+    else:
+        ws = None
+
+        def merge():
+            allreduce_or_filter(bf)
+    merge()  # warm-up merge: OR is idempotent, the words do not change
+    mem.sample("merge")
     merge_s = []
     for _ in range(args.c5_merge_reps):
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
-        allreduce_or_native(bf, comm, workspace=ws)
+        merge()
         torch.cuda.synchronize()
         merge_s.append(time.perf_counter() - t0)
     del ws
@@ -199,6 +258,7 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
     bf.copy_words_to(a)
     ref.copy_words_to(b)
     same = bool(torch.equal(a, b)) and bf.minmax() == ref.minmax() and not bf.is_empty()
+    mem.sample("merge_check")
     del a, b, ref
     torch.cuda.empty_cache()
     ok = all_ok(same)
@@ -220,13 +280,25 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
         bf.probe_async(pkeys, n=n_probe, out_sel=out_sel, out_count=out_count, workspace=pws)
     torch.cuda.synchronize()
     probe_s = (time.perf_counter() - t0) / reps
+    mem.sample("probe")
     survivors = int(out_count.item())
     nbytes = bf.num_blocks * 8
     del pkeys, out_sel, pws, bf
     torch.cuda.empty_cache()
     insert_s, probe_s, *merge_s = reduce_max([insert_s, probe_s] + merge_s)
+    peaks = gather_ints([mem.peak - mem.base, mem.peak])
+    wall_s = reduce_max([time.perf_counter() - t_section])[0]
+    mem_rec = {
+        "source": "hipMemGetInfo (torch.cuda.mem_get_info): total - free, sampled after each phase",
+        "device_total_bytes": mem.total,
+        "rank0_phase_used_bytes": mem.phases,
+        "section_peak_bytes_per_rank": [p[0] for p in peaks],
+        "device_peak_used_bytes_per_rank": [p[1] for p in peaks],
+        "ranks_per_device": shared_device_ranks,
+    }
     rec = c5_merge_record(world, nbytes, rows, insert_s * 1e3, merge_s, probe_s * 1e3, survivors, check,
-                          args.collective_timeout_ms or rpt_amd.load().rpt_collective_timeout_ms())
+                          (args.collective_timeout_ms or rpt_amd.load().rpt_collective_timeout_ms()) if native else None,
+                          native=native, merge_path=merge_path, mem=mem_rec, wall_s=wall_s)
     if not ok:
         raise SystemExit("C5: OR-merged filter differs from the single-GPU build")
     return rec
@@ -318,6 +390,13 @@ def main():
         world = 1
     if world != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch with --nproc-per-node {args.gpus}")
+
+    # stdout carries exactly ONE line, the JSON record: native libraries print banners there (RCCL prints its
+    # version block at communicator init), so this rank's fd 1 goes to stderr and the record is written to a
+    # duplicate of the original stdout
+    record_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch
     import torch.distributed as dist
@@ -482,26 +561,44 @@ def main():
     elapsed, insert_s, merge_s = t.tolist()
 
     # ---- C5 build + product merge + probe (after the headline; N > 1 by default, --c5-merge at N = 1) ----
+    # At N > 1 it runs whatever the merge path: the product merge over RCCL, or the torch.distributed
+    # composition (the gloo rehearsal on a box with fewer GPUs than ranks, --merge torch), so bench's sharding,
+    # merge check, reductions and record assembly run before the driver's multi-GPU run does them.
     c5 = None
-    if (world > 1 and comm is not None and not args.no_c5_merge) or (world == 1 and args.c5_merge):
+    if (world > 1 and not args.no_c5_merge) or (world == 1 and args.c5_merge):
         del keys, out_sel, ws
         torch.cuda.empty_cache()
-        c5_comm = comm if comm is not None else RcclComm.single(device)
+        c5_comm = comm if comm is not None else (RcclComm.single(device) if world == 1 else None)
+        coll_dev = device if backend == "nccl" else "cpu"
 
         def reduce_max(vals):
-            v = torch.tensor(vals, dtype=torch.float64, device=device)
+            v = torch.tensor(vals, dtype=torch.float64, device=coll_dev)
             if world > 1:
                 dist.all_reduce(v, op=dist.ReduceOp.MAX)
             return v.tolist()
 
         def all_ok(flag):
-            v = torch.tensor([1 if flag else 0], dtype=torch.int64, device=device)
+            v = torch.tensor([1 if flag else 0], dtype=torch.int64, device=coll_dev)
             if world > 1:
                 dist.all_reduce(v, op=dist.ReduceOp.MIN)
             return bool(v.item())
 
-        c5 = run_c5_merge(args, rank, world, device, c5_comm, barrier, reduce_max, all_ok)
-        if c5_comm is not comm:
+        def gather_ints(vals):
+            v = torch.tensor(vals, dtype=torch.int64, device=coll_dev)
+            if world == 1:
+                return [v.tolist()]
+            out = [torch.empty_like(v) for _ in range(world)]
+            dist.all_gather(out, v)
+            return [o.tolist() for o in out]
+
+        shared = -(-world // max(1, torch.cuda.device_count())) if backend == "gloo" else 1
+        c5_path = ("rpt_bf_allreduce_or_ws (C-ABI: RCCL grouped send/recv reduce-scatter in 32 MiB rounds, OR kernel "
+                   "on a helper stream, all-gather)" if c5_comm is not None else
+                   "torch.distributed all_to_all + all_gather in 256 MiB rounds ("
+                   + ("gloo rehearsal, host-staged, ranks sharing GPUs" if backend == "gloo" else "--merge torch") + ")")
+        c5 = run_c5_merge(args, rank, world, device, c5_comm, barrier, reduce_max, all_ok, gather_ints, c5_path,
+                          shared_device_ranks=max(1, shared))
+        if c5_comm is not None and c5_comm is not comm:
             c5_comm.close()
 
     if rank == 0:
@@ -604,7 +701,7 @@ def main():
             if sample == n_probe:  # same rows, same filter: a full-size cross-check of the survivor count
                 cb["survivors_match_gpu"] = cb["survivors"] == survivors
             line["cpu_baseline"] = cb
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=record_out, flush=True)
 
     if comm is not None:
         comm.close()

@@ -228,17 +228,60 @@ const char* inst_name(const char* base) {
   return names.back().second.c_str();
 }
 
+bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// Writes captured into a graph. A graph replays its kernels, not this library's host-side
+// bookkeeping, so a captured write must not depend on host state that changes between replays:
+// * a deferred clear (clear_pending) would be settled by a memset (or whole-slice stores) recorded in the
+//   graph and dropped once, at capture time: every replay would then wipe the bits inserted since the last
+//   one. A capture that would have to settle it is refused; rpt_bf_settle() before capturing settles it;
+// * rpt_bf_clear itself only flips that flag, which a replay cannot redo: refused inside a capture;
+// * the cross-stream write order (order_ev) cannot be waited on from inside the capture, so an earlier
+//   write still in flight refuses the capture too (synchronize it first). A captured write takes no part in
+//   that order: replays are ordered by the stream the caller launches the graph on;
+// * the slice insert's plain-store merges rely on the words being zero (pristine / store-all): inside a
+//   capture it merges with atomics, correct whatever the words hold at replay time.
+// The C-ABI entry points that write words call this before enqueueing anything.
+int refuse_capture_write(rpt_bf* bf, hipStream_t s, const char* what) {
+  if (!stream_capturing(s)) return RPT_OK;
+  if (bf->clear_pending.load() || bf->zero_unsynced.load())
+    return fail(RPT_ERR_INVALID_ARGUMENT,
+                "%s of a cleared filter inside stream capture: call rpt_bf_settle() before capturing", what);
+  std::lock_guard<std::mutex> lk(bf->order_mu);
+  if (bf->order_pending && hipEventQuery(bf->order_ev) != hipSuccess)
+    return fail(RPT_ERR_INVALID_ARGUMENT,
+                "%s inside stream capture while an earlier write to the filter is in flight: synchronize it (or "
+                "call rpt_bf_settle()) before capturing", what);
+  return RPT_OK;
+}
+#define RPT_REFUSE_CAPTURE_WRITE(bf, s, what)                  \
+  do {                                                         \
+    const int st_cap_ = refuse_capture_write(bf, s, what);     \
+    if (st_cap_ != RPT_OK) return st_cap_;                     \
+  } while (0)
+
 // Scope of one word-writing operation on a filter (see rpt_bf::order_mu): waits on `s` for the previous
-// write's completion event, and records this one's when done() is called (after the launches).
+// write's completion event, and records this one's when done() is called (after the launches). Inside a
+// stream capture (refuse_capture_write has checked the previous write completed) it neither waits nor
+// records: the graph's replays are ordered by the caller's stream.
 struct WriteOrder {
   rpt_bf* bf;
   hipStream_t s;
   std::unique_lock<std::mutex> lk;
-  WriteOrder(rpt_bf* b, hipStream_t st) : bf(b), s(st), lk(b->order_mu) {
-    if (bf->order_pending) (void)hipStreamWaitEvent(s, bf->order_ev, 0);
+  bool captured;
+  WriteOrder(rpt_bf* b, hipStream_t st) : bf(b), s(st), lk(b->order_mu), captured(stream_capturing(st)) {
+    if (bf->order_pending && !captured) (void)hipStreamWaitEvent(s, bf->order_ev, 0);
   }
   // pristine_after: every word is zero once this operation completes
   void done(bool pristine_after) {
+    if (captured) {
+      bf->order_pending = false;  // the previous write completed (refuse_capture_write); nothing recorded
+      bf->pristine = false;       // a replay may run at any later time
+      return;
+    }
     if (!bf->order_ev && hipEventCreateWithFlags(&bf->order_ev, hipEventDisableTiming) != hipSuccess) bf->order_ev = nullptr;
     bf->order_pending = bf->order_ev != nullptr && hipEventRecord(bf->order_ev, s) == hipSuccess;
     if (!bf->order_pending) (void)hipStreamSynchronize(s);  // no event: order by waiting here
@@ -1053,6 +1096,8 @@ int rpt_bf_set_has_data(rpt_bf* bf, int value) {
 int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
   RPT_ON_DEVICE(bf->device);
+  if (stream_capturing(as_stream(stream)))  // the deferred clear is a host-side flag a replay cannot redo
+    return fail(RPT_ERR_INVALID_ARGUMENT, "rpt_bf_clear inside stream capture: clear outside the capture");
   WriteOrder order(bf, as_stream(stream));
   // the words are zeroed by the next operation on them (rpt_bf::clear_pending): a slice insert that
   // stores every slice whole needs no separate pass over the filter (8 GiB C5 filter: 1.35 ms)
@@ -1108,6 +1153,7 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
   int st = check_col(col);
   if (st != RPT_OK) return st;
   RPT_ON_DEVICE(bf->device);
+  RPT_REFUSE_CAPTURE_WRITE(bf, as_stream(stream), "insert");
   bf->has_data.store(1);  // bloom_filter.cpp:75
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const unsigned grid = persistent_grid(bf->device, n_segs);
@@ -1181,14 +1227,17 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   if (!workspace || workspace_bytes < need)
     return fail(RPT_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   RPT_ON_DEVICE(bf->device);
+  hipStream_t s = as_stream(stream);
+  RPT_REFUSE_CAPTURE_WRITE(bf, s, "insert");
+  const bool captured = stream_capturing(s);
   bf->has_data.store(1);  // bloom_filter.cpp:75
   InsertWorkspace ws;
   insert_workspace_layout(n, L, strategy, workspace, &ws);
-  hipStream_t s = as_stream(stream);
   // the first kernels below fold the keys' min/max into bf->stats: they must land after the filter's
   // previous write (e.g. a clear's stats reset enqueued on another stream), so wait for its event now;
-  // only the slice merge at the end takes the write order for the words
-  {
+  // only the slice merge at the end takes the write order for the words (inside a capture the previous
+  // write has completed: refuse_capture_write)
+  if (!captured) {
     std::lock_guard<std::mutex> lk(bf->order_mu);
     if (bf->order_pending) RPT_HIP(hipStreamWaitEvent(s, bf->order_ev, 0));
   }
@@ -1232,13 +1281,14 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
   // one workgroup per slice: every slice stored whole (a deferred clear), plain stores of the non-zero
   // pieces (a pristine filter) or a per-slice choice of read-modify-write vs atomic ORs; several
   // workgroups per slice must merge with atomics (after the deferred clear's memset, if any)
-  const bool store_all = splits == 1 && bf->clear_pending.load();
+  // (inside a stream capture: atomics, whatever the words hold when the graph replays; no clear is pending)
+  const bool store_all = splits == 1 && bf->clear_pending.load() && !captured;
   if (!store_all) {
     const hipError_t ez = zero_pending_locked(bf, s);
     if (ez != hipSuccess) return fail(RPT_ERR_HIP, "hipMemsetAsync failed: %s", hipGetErrorString(ez));
   }
   const int mode = store_all ? rpt::kSliceMergeStoreAll
-                   : splits > 1 ? rpt::kSliceMergeAtomic
+                   : (splits > 1 || captured) ? rpt::kSliceMergeAtomic
                                 : (bf->pristine ? rpt::kSliceMergeStore : rpt::kSliceMergeAdaptive);
   ProfScope prof_i("slice_insert_kernel", s);
   hipLaunchKernelGGL(rpt::slice_insert_kernel, dim3(grid_slices * splits), dim3(rpt::kSliceThreads), 0, s, bf->words, splits,
@@ -1567,6 +1617,7 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
     return fail(RPT_ERR_SHAPE_MISMATCH, "merge of log_num_blocks %d (dev %d) with %d (dev %d)", dst->log_num_blocks,
                 dst->device, src->log_num_blocks, src->device);
   RPT_ON_DEVICE(dst->device);
+  RPT_REFUSE_CAPTURE_WRITE(dst, as_stream(stream), "merge");
   if (src != dst) RPT_SETTLE(src, as_stream(stream));
   WriteOrder order(dst, as_stream(stream));
   const hipError_t ez = zero_pending_locked(dst, as_stream(stream));
@@ -1622,6 +1673,8 @@ std::shared_ptr<const RcclApi> load_librccl() {
   sym(a->fn.comm_abort, "ncclCommAbort");
   sym(a->fn.get_async_error, "ncclCommGetAsyncError");
   sym(a->fn.comm_init_rank_config, "ncclCommInitRankConfig");
+  // optional: only rpt_rccl_comm_destroy of a non-blocking communicator uses it (abort if absent)
+  a->fn.comm_finalize = reinterpret_cast<decltype(a->fn.comm_finalize)>(dlsym(h, "ncclCommFinalize"));
   return a;
 }
 
@@ -1718,9 +1771,14 @@ void give_helper(MergeHelper* h) {
 // timeout aborts the communicator (ncclCommAbort: RCCL's kernels leave), then drains the streams, bounded too.
 constexpr int kNcclInProgress = 7;  // rccl.h ncclInProgress (a non-blocking communicator's pending call)
 std::atomic<uint64_t> g_coll_timeout_ms{RPT_COLLECTIVE_TIMEOUT_MS_DEFAULT};
-// Communicators this library aborted: ncclCommAbort frees them, so rpt_rccl_comm_destroy must not.
+// Communicators this library made (rpt_rccl_comm_init_rank[_nonblocking]; the flag: non-blocking), and
+// those of them a failed merge aborted: ncclCommAbort frees a communicator, so rpt_rccl_comm_destroy must
+// not. A caller-owned communicator (one the caller made and passed in) is never recorded: the merge tells
+// its owner by RPT_ERR_COMM_ABORTED, and nothing here grows with such failures.
 std::mutex g_aborted_mu;
 std::vector<void*> g_aborted;
+std::vector<std::pair<void*, bool>> g_made;
+std::atomic<int> g_abort_on_error{1};  // rpt_collective_set_abort_on_error
 
 using Clock = std::chrono::steady_clock;
 Clock::time_point coll_deadline() { return Clock::now() + std::chrono::milliseconds(g_coll_timeout_ms.load()); }
@@ -1784,7 +1842,11 @@ int settle_nccl(const rpt_rccl_api_table& api, void* comm, int rc, Clock::time_p
 void abort_comm(const rpt_rccl_api_table& api, void* comm) {
   {
     std::lock_guard<std::mutex> lk(g_aborted_mu);
-    g_aborted.push_back(comm);
+    for (const auto& m : g_made)
+      if (m.first == comm) {
+        g_aborted.push_back(comm);
+        break;
+      }
   }
   (void)api.comm_abort(comm);
 }
@@ -1795,6 +1857,30 @@ bool take_aborted(void* comm) {
   if (it == g_aborted.end()) return false;
   g_aborted.erase(it);
   return true;
+}
+
+// A communicator made here: (re)registered at its address (a new one at an aborted one's address is live).
+void note_made(void* comm, bool nonblocking) {
+  std::lock_guard<std::mutex> lk(g_aborted_mu);
+  g_aborted.erase(std::remove(g_aborted.begin(), g_aborted.end(), comm), g_aborted.end());
+  for (auto& m : g_made)
+    if (m.first == comm) {
+      m.second = nonblocking;
+      return;
+    }
+  g_made.emplace_back(comm, nonblocking);
+}
+
+// Forget a communicator made here; returns {was made here, non-blocking}.
+std::pair<bool, bool> forget_made(void* comm) {
+  std::lock_guard<std::mutex> lk(g_aborted_mu);
+  for (size_t i = 0; i < g_made.size(); i++)
+    if (g_made[i].first == comm) {
+      const bool nb = g_made[i].second;
+      g_made.erase(g_made.begin() + static_cast<long>(i));
+      return {true, nb};
+    }
+  return {false, false};
 }
 }  // namespace
 extern "C" {
@@ -1843,6 +1929,8 @@ int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t 
     return fail(RPT_ERR_WORKSPACE, "all-reduce workspace %zu bytes < required %zu", workspace_bytes, g.workspace_bytes());
   int64_t* v = static_cast<int64_t*>(workspace);  // {min, ~max, ~has} then has_data (as int) in v[3]
   uint64_t* stage = reinterpret_cast<uint64_t*>(static_cast<char*>(workspace) + 256);
+  if (stream_capturing(s))  // it polls the stream from the host: nothing of it can be replayed
+    return fail(RPT_ERR_INVALID_ARGUMENT, "rpt_bf_allreduce_or inside stream capture");
   MergeHelper* h = nullptr;
   WriteOrder order(bf, s);
   if (zero_pending_locked(bf, s) != hipSuccess) {
@@ -1927,10 +2015,11 @@ int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t 
   int st = run();
   const std::string err = t_last_error;
   bool drained = true;
-  if (st != RPT_OK && posted) {
+  if (st != RPT_OK && posted && g_abort_on_error.load()) {
     // peers may be blocked on this rank, or this rank on a dead peer: the communicator cannot be reused.
     // Abort it (RCCL's kernels on s leave), then drain s and the helper stream, bounded again, so the
-    // workspace is free on return.
+    // workspace is free on return. The distinct status tells a caller that owns the communicator that it
+    // is gone (ncclCommAbort freed it: never destroy or use it again).
     abort_comm(api, nccl_comm);
     (void)join_helper();
     std::string why;
@@ -1939,6 +2028,17 @@ int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t 
     t_merge_stuck = !drained;
     t_last_error = err + "; communicator aborted" +
                    (drained ? "" : "; streams did not drain (" + why + "): the workspace is still in use");
+    st = RPT_ERR_COMM_ABORTED;
+  } else if (st != RPT_OK && posted) {
+    // rpt_collective_set_abort_on_error(0): the communicator stays its owner's to abort. RCCL's kernels may
+    // still hold `stream` (a dead peer): until the owner aborts the communicator, the stream, the helper
+    // stream and the workspace stay in use, so none of them is released here.
+    (void)join_helper();
+    drained = hipStreamQuery(s) == hipSuccess && (!h || hipStreamQuery(h->s) == hipSuccess);
+    t_merge_stuck = !drained;
+    t_last_error = err + "; communicator NOT aborted (rpt_collective_set_abort_on_error(0))" +
+                   (drained ? "" : ": the streams are still blocked; abort the communicator (ncclCommAbort) "
+                                   "before reusing the stream, the workspace or the filter");
   } else if (h) {
     // on an error before any collective call the helper may still hold OR kernels: the caller's stream
     // waits for them, so the workspace is free once `stream` is
@@ -1956,6 +2056,13 @@ int rpt_collective_set_timeout_ms(uint64_t ms) {
 }
 
 uint64_t rpt_collective_timeout_ms(void) { return g_coll_timeout_ms.load(); }
+
+int rpt_collective_set_abort_on_error(int abort_on_error) {
+  g_abort_on_error.store(abort_on_error ? 1 : 0);
+  return RPT_OK;
+}
+
+int rpt_collective_abort_on_error(void) { return g_abort_on_error.load(); }
 
 int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream) {
   if (!bf || !nccl_comm) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
@@ -2009,7 +2116,7 @@ int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, 
   std::memcpy(uid.internal, id, RPT_RCCL_UNIQUE_ID_BYTES);
   void* comm = nullptr;
   RPT_NCCL(api.comm_init_rank(&comm, world, uid, rank));
-  (void)take_aborted(comm);  // a new communicator at an aborted one's address is live
+  note_made(comm, false);  // (a new communicator at an aborted one's address is live)
   *out_comm = comm;
   return RPT_OK;
 }
@@ -2033,19 +2140,35 @@ int rpt_rccl_comm_init_rank_nonblocking(int device, int world, const uint8_t* id
     return fail(RPT_ERR_COLLECTIVE, "ncclCommInitRankConfig (non-blocking): %s",
                 rc == kNcclInProgress ? "no completion within the collective timeout" : api.error_string(rc));
   }
-  (void)take_aborted(comm);
+  note_made(comm, true);
   *out_comm = comm;
   return RPT_OK;
 }
 
 int rpt_rccl_comm_destroy(void* comm) {
   if (!comm) return RPT_OK;
-  if (take_aborted(comm)) return RPT_OK;  // a failed merge aborted it: ncclCommAbort already freed it
+  const bool aborted = take_aborted(comm);
+  const std::pair<bool, bool> made = forget_made(comm);
+  if (aborted) return RPT_OK;  // a failed merge aborted it: ncclCommAbort already freed it
   const std::shared_ptr<const RcclApi> api_p = rccl_api();
   const rpt_rccl_api_table& api = api_p->fn;
   if (!api_p->load_error.empty()) return fail(RPT_ERR_COLLECTIVE, "RCCL unavailable: %s", api_p->load_error.c_str());
+  if (made.second) {
+    // non-blocking: ncclCommDestroy would return ncclInProgress and tear down in the background,
+    // so the caller could exit or reuse the device under it. Finalize first and poll it to completion, bounded
+    // by the collective timeout; a finalize that does not complete (or a library without ncclCommFinalize)
+    // ends in an abort, which tears down synchronously.
+    int rc = api.comm_finalize ? settle_nccl(api, comm, api.comm_finalize(comm), coll_deadline()) : kNcclInProgress;
+    if (rc != 0) {
+      (void)api.comm_abort(comm);
+      if (api.comm_finalize)
+        return fail(RPT_ERR_COLLECTIVE, "ncclCommFinalize: %s; communicator aborted",
+                    rc == kNcclInProgress ? "no completion within the collective timeout" : api.error_string(rc));
+      return RPT_OK;
+    }
+  }
   const int rc = api.comm_destroy(comm);
-  if (rc != 0 && rc != kNcclInProgress)  // a non-blocking communicator finishes tearing down on its own
+  if (rc != 0 && !(made.second && rc == kNcclInProgress))
     return fail(RPT_ERR_COLLECTIVE, "ncclCommDestroy: %s", api.error_string(rc));
   return RPT_OK;
 }
@@ -2179,6 +2302,7 @@ int rpt_bf_copy_words_from(rpt_bf* bf, const uint64_t* src_dev, uint64_t n_words
     return fail(RPT_ERR_SHAPE_MISMATCH, "copy of %llu words into a %llu-word filter", (unsigned long long)n_words,
                 (unsigned long long)(1ULL << bf->log_num_blocks));
   RPT_ON_DEVICE(bf->device);
+  RPT_REFUSE_CAPTURE_WRITE(bf, as_stream(stream), "copy into the filter");
   WriteOrder order(bf, as_stream(stream));
   const hipError_t e = hipMemcpyAsync(bf->words, src_dev, n_words * 8, hipMemcpyDeviceToDevice, as_stream(stream));
   if (e == hipSuccess) bf->clear_pending.store(false);  // every word is overwritten

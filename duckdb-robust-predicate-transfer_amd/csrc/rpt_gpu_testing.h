@@ -44,6 +44,7 @@ typedef struct rpt_rccl_api_table {
   int (*get_async_error)(void* comm, int* async_error);                            /* ncclCommGetAsyncError */
   int (*comm_init_rank_config)(void** comm, int nranks, rpt_rccl_unique_id id, int rank,
                                void* config);                                      /* ncclCommInitRankConfig */
+  int (*comm_finalize)(void* comm);                                                /* ncclCommFinalize */
 } rpt_rccl_api_table;
 
 #ifdef RPT_TESTING_HOOKS

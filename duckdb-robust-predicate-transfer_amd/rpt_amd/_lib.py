@@ -20,6 +20,7 @@ RPT_ERR_OUT_OF_MEMORY = 3
 RPT_ERR_WORKSPACE = 4
 RPT_ERR_SHAPE_MISMATCH = 5
 RPT_ERR_COLLECTIVE = 6
+RPT_ERR_COMM_ABORTED = 7
 
 RPT_PROBE_AUTO = 0
 RPT_PROBE_GATHER = 1
@@ -127,6 +128,8 @@ SIGNATURES = {
     "rpt_allreduce_workspace_bytes": (c_size_t, [c_int, c_int]),
     "rpt_collective_set_timeout_ms": (c_int, [c_uint64]),
     "rpt_collective_timeout_ms": (c_uint64, []),
+    "rpt_collective_set_abort_on_error": (c_int, [c_int]),
+    "rpt_collective_abort_on_error": (c_int, []),
     "rpt_rccl_available": (c_int, [c_int]),
     "rpt_rccl_get_unique_id": (c_int, [c_void_p]),
     "rpt_rccl_comm_init_rank": (c_int, [c_int, c_int, c_void_p, c_int, POINTER(c_void_p)]),
@@ -176,9 +179,11 @@ def load_variant(path: str) -> ctypes.CDLL:
     return _bind(path)
 
 
-def check(status: int) -> None:
+def check(status: int, lib=None) -> None:
+    """Raise RptError for a non-OK status with the message of `lib` (the library that returned it; default the
+    product library)."""
     if status != RPT_OK:
-        lib = load()
+        lib = lib if lib is not None else load()
         raise RptError(status, lib.rpt_last_error().decode(errors="replace"))
 
 

@@ -68,6 +68,7 @@ def or_allreduce_words(full: torch.Tensor, group=None, or_slices: Optional[OrSli
     dist.all_to_all_single(recv, full, group=group)  # recv[j] = peer j's slice <my rank>
     mine = torch.empty(slice_words, dtype=full.dtype, device=full.device)
     or_slices(mine, recv, world, slice_words)
+    del recv
     dist.all_gather_into_tensor(full, mine, group=group)
 
 
@@ -86,6 +87,7 @@ class RcclComm:
 
         self._lib = load()
         self.handle = None
+        self.aborted = False
         self.device = torch.device(device)
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
@@ -131,6 +133,7 @@ class RcclComm:
         self = cls.__new__(cls)
         self._lib = load()
         self.handle = None
+        self.aborted = False
         self.device = torch.device(device)
         self.world, self.rank = 1, 0
         dev = self.device.index if self.device.index is not None else torch.cuda.current_device()
@@ -150,6 +153,12 @@ class RcclComm:
             self._lib.rpt_rccl_comm_destroy(self.handle)
         self.handle = None
 
+    def mark_aborted(self) -> None:
+        """A failed merge aborted this communicator (ncclCommAbort freed it): release the library's record of it
+        (rpt_rccl_comm_destroy does nothing else for an aborted one) and drop the handle."""
+        self.aborted = True
+        self.close()
+
     def __del__(self):
         try:
             self.close()
@@ -164,35 +173,75 @@ def allreduce_workspace(bf, comm: RcclComm) -> torch.Tensor:
     return torch.empty(n, dtype=torch.uint8, device=bf.device)
 
 
+# Workspaces of merges whose aborted streams did not drain: RCCL / OR kernels may still write them, so they
+# are never returned to the caching allocator (the C wrapper rpt_bf_allreduce_or leaks its own the same way).
+_STUCK_WORKSPACES: list = []
+
+
 def allreduce_or_native(bf, comm: RcclComm, stream=None, workspace: Optional[torch.Tensor] = None) -> None:
     """CREATE_BF Combine across GPUs through the C-ABI (rpt_bf_allreduce_or_ws): words OR-merged in place,
-    key min/max and has_data reduced; returns once has_data is known (one stream sync)."""
-    from ._lib import check
+    key min/max and has_data reduced; returns once has_data is known (one stream sync).
+
+    A merge that fails after its first collective call aborts the communicator (RPT_ERR_COMM_ABORTED): the
+    RcclComm is then marked dead (its handle dropped, the library's record of it released), so a later merge
+    on it raises at once instead of handing RCCL a freed communicator."""
+    from ._lib import RPT_ERR_COLLECTIVE, RPT_ERR_COMM_ABORTED, RptError, check
     from .bloom import _stream
 
+    if comm.handle is None or not comm.handle.value:
+        raise RptError(RPT_ERR_COLLECTIVE, "RcclComm is closed or was aborted by an earlier failed merge: make a "
+                                           "new communicator")
     ws = workspace if workspace is not None else allreduce_workspace(bf, comm)
-    check(bf._lib.rpt_bf_allreduce_or_ws(bf.handle, comm.handle, ws.data_ptr(), ws.numel(),
-                                         _stream(bf.device, stream)))
+    try:
+        check(bf._lib.rpt_bf_allreduce_or_ws(bf.handle, comm.handle, ws.data_ptr(), ws.numel(),
+                                             _stream(bf.device, stream)), bf._lib)
+    except RptError as e:
+        if "did not drain" in str(e) or "still blocked" in str(e):
+            _STUCK_WORKSPACES.append(ws)
+        if e.status == RPT_ERR_COMM_ABORTED:
+            comm.mark_aborted()
+        raise
 
 
-def allreduce_or_filter(bf, group=None) -> None:
+TORCH_MERGE_ROUND_WORDS = 32 << 20  # 256 MiB of words per round of the torch composition
+
+
+def or_allreduce_words_rounds(full: torch.Tensor, group=None, round_words: int = TORCH_MERGE_ROUND_WORDS) -> None:
+    """or_allreduce_words over `full` in rounds of at most round_words words (rounded down to a multiple of the
+    world size, at least one word per rank). A CUDA tensor under a gloo group is staged through host memory one
+    round at a time; a CPU tensor is reduced in place."""
+    world = dist.get_world_size(group)
+    total = full.numel()
+    if total % world:
+        raise ValueError("word count must be a multiple of the world size (use padded_words)")
+    stage = full.is_cuda and dist.get_backend(group) == "gloo"
+    step = max(world, (int(round_words) // world) * world)
+    for lo in range(0, total, step):
+        view = full[lo: min(total, lo + step)]  # a multiple of world words: total and step both are
+        if stage:
+            host = view.cpu()
+            or_allreduce_words(host, group, or_slices=cpu_or_slices)
+            view.copy_(host)
+        else:
+            or_allreduce_words(view, group)
+
+
+def allreduce_or_filter(bf, group=None, round_words: int = TORCH_MERGE_ROUND_WORDS) -> None:
     """OR-merge a BloomFilter across all ranks (all ranks must hold the same log_num_blocks), and
     reduce its has_data flag and key min/max (CreateBF Combine, physical_create_bf.cpp:244-275).
 
+    The words go through the all-reduce in rounds of at most `round_words` (rounded down to a multiple of
+    the world size; every rank derives the same rounds from the same block count), so the receive buffers
+    and, for gloo, the host staging stay bounded whatever the filter size (C5's 8 GiB filter included).
     With RCCL the words stay on the device. A gloo group (CPU collectives; used to rehearse the
-    multi-rank path on a box with fewer GPUs than ranks) stages the words through host memory."""
+    multi-rank path on a box with fewer GPUs than ranks) stages each round through host memory."""
     world = dist.get_world_size(group)
-    nw = bf.num_blocks
-    buf = torch.zeros(padded_words(nw, world), dtype=torch.int64, device=bf.device)
+    buf = torch.zeros(padded_words(bf.num_blocks, world), dtype=torch.int64, device=bf.device)
     bf.copy_words_to(buf)
     on_device = dist.get_backend(group) != "gloo"
-    if on_device:
-        or_allreduce_words(buf, group)
-    else:
-        host = buf.cpu()
-        or_allreduce_words(host, group, or_slices=cpu_or_slices)
-        buf.copy_(host)
+    or_allreduce_words_rounds(buf, group, round_words)
     bf.copy_words_from(buf)
+    del buf
     mm, has = allreduce_minmax_flag(bf.minmax(), not bf.is_empty(), group,
                                     device=bf.device if on_device else torch.device("cpu"))
     bf.set_minmax(mm)

@@ -40,7 +40,9 @@ typedef enum rpt_status {
   RPT_ERR_OUT_OF_MEMORY = 3,    /* device allocation failed */
   RPT_ERR_WORKSPACE = 4,        /* caller workspace smaller than rpt_probe_workspace_bytes() */
   RPT_ERR_SHAPE_MISMATCH = 5,   /* merge of filters with different log_num_blocks / devices */
-  RPT_ERR_COLLECTIVE = 6        /* librccl could not be loaded, or an RCCL call failed */
+  RPT_ERR_COLLECTIVE = 6,       /* librccl could not be loaded, or an RCCL call failed */
+  RPT_ERR_COMM_ABORTED = 7      /* an OR all-reduce failed after its first collective call and ABORTED the
+                                   communicator (ncclCommAbort freed it: never use or destroy it again) */
 } rpt_status;
 
 typedef enum rpt_key_type {
@@ -155,9 +157,16 @@ size_t rpt_bf_probe_workspace_bytes(const rpt_bf* bf, uint64_t n_rows);
  * rpt_bf_info::words can see the words before that. */
 int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
 /* Settle a deferred clear now: zero the words on `stream` and wait until that zeroing has completed (a
- * no-op if no clear is pending). Needed before a stream capture (graph) reads a cleared filter: a read
- * inside a capture that would have to settle the clear is refused with RPT_ERR_INVALID_ARGUMENT (the
- * zeroing would be replayed with the graph). Synchronous. */
+ * no-op if no clear is pending). Needed before a stream capture (graph) reads or writes a cleared filter:
+ * a read or write inside a capture that would have to settle the clear is refused with
+ * RPT_ERR_INVALID_ARGUMENT (the zeroing would be replayed with the graph, wiping what was inserted between
+ * replays). Synchronous.
+ * Stream capture in general: probes capture freely once no clear is pending. A write (insert, merge, copy
+ * into the filter) captures when no clear is pending and the filter's previous write has completed
+ * (otherwise RPT_ERR_INVALID_ARGUMENT: synchronize first); a captured insert merges with atomics, so each
+ * replay ORs its keys in whatever the filter holds by then, and replays are ordered by the stream the
+ * graph is launched on (a captured write takes no part in the filter's cross-stream write order).
+ * rpt_bf_clear and rpt_bf_allreduce_or[_ws] are refused inside a capture. */
 int rpt_bf_settle(rpt_bf* bf, rpt_stream_t stream);
 
 /* ---- build ------------------------------------------------------------------------------- */
@@ -267,12 +276,19 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream);
  * communicator's ncclInProgress results are polled against the same deadline. A peer that dies mid-merge
  * never posts its side, so its peers' streams would wait forever: on a timeout, an asynchronous RCCL error
  * or any error after the first collective call, the call ABORTS the communicator (ncclCommAbort, which
- * frees it: do not use it again; rpt_rccl_comm_destroy accepts it and does nothing), drains the streams
- * (bounded again) and returns RPT_ERR_COLLECTIVE. The filter then holds its own partial plus possibly some
- * peers' bits (never fewer bits than before the call): rebuild it, or merge again on a new communicator.
+ * frees it), drains the streams (bounded again) and returns RPT_ERR_COMM_ABORTED: never use the
+ * communicator again, and do not ncclCommDestroy it (rpt_rccl_comm_destroy accepts one this library made
+ * and does nothing). An error before any collective call returns RPT_ERR_COLLECTIVE (or another status)
+ * with the communicator intact. The filter then holds its own partial plus possibly some peers' bits
+ * (never fewer bits than before the call): rebuild it, or merge again on a new communicator.
  * If even the aborted streams do not drain by the second deadline, the message says "streams did not
  * drain": the workspace, `stream` and the filter stay in use by work that may never finish (later work
- * ordered after them may never run; rpt_bf_allreduce_or then leaks its workspace rather than free it). */
+ * ordered after them may never run; rpt_bf_allreduce_or then leaks its workspace rather than free it).
+ * A caller that owns its communicator and wants to abort it itself sets rpt_collective_set_abort_on_error(0):
+ * the merge then never aborts; after a failure past the first collective call it returns
+ * RPT_ERR_COLLECTIVE with the communicator untouched, and, when RCCL's kernels still hold the streams (the
+ * message says "streams are still blocked"), `stream`, the workspace and the filter stay in use until the
+ * owner calls ncclCommAbort. Not inside a stream capture (RPT_ERR_INVALID_ARGUMENT): it waits on the host. */
 #define RPT_ALLREDUCE_ROUND_WORDS (4ULL << 20)
 size_t rpt_allreduce_workspace_bytes(int world, int log_num_blocks);
 int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t workspace_bytes,
@@ -284,6 +300,10 @@ int rpt_bf_allreduce_or(rpt_bf* bf, void* nccl_comm, rpt_stream_t stream);
 #define RPT_COLLECTIVE_TIMEOUT_MS_DEFAULT 120000ULL
 int rpt_collective_set_timeout_ms(uint64_t ms);
 uint64_t rpt_collective_timeout_ms(void);
+/* Process-wide: 1 (default) = a failed merge aborts its communicator (RPT_ERR_COMM_ABORTED above); 0 = it
+ * leaves the communicator to its owner (RPT_ERR_COLLECTIVE). */
+int rpt_collective_set_abort_on_error(int abort_on_error);
+int rpt_collective_abort_on_error(void);
 /* RCCL communicator for callers that bring none (bench.py, tests; a DuckDB shim that owns an
  * ncclComm_t passes it to rpt_bf_allreduce_or directly). Rank 0 calls rpt_rccl_get_unique_id, the
  * caller broadcasts the RPT_RCCL_UNIQUE_ID_BYTES bytes out of band (torch.distributed, MPI, a file),
@@ -301,6 +321,9 @@ int rpt_rccl_comm_init_rank(int device, int world, const uint8_t* id, int rank, 
  * timeout, so even RCCL's host-side connection setup with a peer that died cannot block the caller past the
  * bound (a blocking communicator's ncclGroupEnd can). Init itself completes within the timeout or fails. */
 int rpt_rccl_comm_init_rank_nonblocking(int device, int world, const uint8_t* id, int rank, void** out_comm);
+/* Destroy a communicator made by rpt_rccl_comm_init_rank[_nonblocking] (one a failed merge aborted: nothing to
+ * do). A non-blocking one is finalized first (ncclCommFinalize, polled to completion against the collective
+ * timeout; aborted if it does not complete), so its teardown has finished when this returns. */
 int rpt_rccl_comm_destroy(void* comm);
 /* dst[i] |= src[i] for n_words words (device pointers): the local step of the multi-GPU
  * OR all-reduce (reduce-scatter slices). */

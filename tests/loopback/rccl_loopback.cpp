@@ -18,6 +18,7 @@
 //   ncclCommInitRankConfig   config->blocking == 0 makes a NON-BLOCKING communicator: init, ncclGroupEnd and
 //       ncclAllReduce do their work as above but return ncclInProgress, and ncclCommGetAsyncError reports
 //       ncclInProgress for two more polls before the call's result (so a caller's polling path runs)
+//   ncclCommFinalize   as a non-blocking call (above) on a non-blocking communicator; success at once otherwise
 //   ncclCommAbort / ncclCommGetAsyncError   rank-local, as in RCCL: an abort frees that rank's communicator and
 //       releases only that rank's blocked streams (below); the asynchronous error is the world's (0 unless a
 //       silent peer was set to report)
@@ -391,6 +392,18 @@ int ncclCommDestroy(void* comm) {
   if (!c) return kInvalidArgument;
   return release_comm(c, false);
 }
+
+// Finalize before destroy (non-blocking communicators: reports ncclInProgress for two polls, then success,
+// or forever under rpt_loopback_stuck). Counted so a test can see that rpt_rccl_comm_destroy finalized one.
+static std::atomic<int> g_finalized{0};
+int ncclCommFinalize(void* comm) {
+  Comm* c = static_cast<Comm*>(comm);
+  if (!c) return kInvalidArgument;
+  g_finalized.fetch_add(1);
+  return complete(c, kSuccess);
+}
+
+int rpt_loopback_finalize_count() { return g_finalized.load(); }
 
 // Rank-local, as RCCL's: frees this rank's communicator and releases this rank's blocked streams only.
 int ncclCommAbort(void* comm) {

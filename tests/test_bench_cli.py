@@ -85,6 +85,15 @@ def test_c5_merge_record_schema():
     json.dumps(rec)
     one = bench.c5_merge_record(1, S, 10**7, 1.0, [0.001], 2.0, 1, "bit-identical", 1000)
     assert one["or_merge_GBps_per_gpu"] is None and one["or_merge_GBps_per_link"] is None  # no peer traffic
+    # the torch composition (gloo rehearsal, --merge torch): torch_merge_ms only, never an or_merge number
+    t = bench.c5_merge_record(2, S, 2 * 10**7, 1.0, [3.0], 2.0, 5, "bit-identical", None, native=False,
+                              merge_path="torch (gloo rehearsal)", mem={"ranks_per_device": 2}, wall_s=40.0)
+    assert t["torch_merge_ms"] == pytest.approx(3000.0) and t["torch_merge_ms_reps"] == [3000.0]
+    for k in ("or_merge_ms", "or_merge_ms_reps", "or_merge_GBps_per_gpu", "or_merge_GBps_per_link"):
+        assert t[k] is None, k
+    assert t["device_memory"] == {"ranks_per_device": 2} and t["wall_s"] == 40.0
+    assert rec["torch_merge_ms"] is None and "device_memory" not in rec
+    json.dumps(t)
 
 
 def test_c5_merge_flags(monkeypatch):

@@ -87,6 +87,51 @@ def test_shard_range_partitions_rows():
     assert padded_words(1 << 21, 8) == 1 << 21 and padded_words(16, 3) == 18
 
 
+def _rounds_worker(rank, world, port, q):
+    import sys
+
+    sys.path.insert(0, PKG)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rpt_amd.distributed import or_allreduce_words_rounds, padded_words
+
+        out = []
+        for nw, round_words in [(1000, 7), (1000, 1), (4096, 10**9), (96, 64)]:
+            g = torch.Generator().manual_seed(1000 * rank + nw)
+            words = torch.randint(-(1 << 62), 1 << 62, (padded_words(nw, world),), generator=g, dtype=torch.int64)
+            words[nw:] = 0
+            mine = words.clone()
+            or_allreduce_words_rounds(mine, round_words=round_words)
+            out.append((words.numpy(), mine.numpy()))
+        with pytest.raises(ValueError):
+            or_allreduce_words_rounds(torch.zeros(world + 1, dtype=torch.int64))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_or_allreduce_in_bounded_rounds(world):
+    """The torch composition of the OR all-reduce in rounds (what bench's gloo rehearsal and --merge torch run on
+    C5's 8 GiB filter: 256 MiB rounds): every round size, including one word per rank and one round over
+    everything, gives every rank the OR of all ranks' words."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rounds_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for case in range(4):
+        want = np.bitwise_or.reduce([res[r][case][0] for r in range(world)])
+        for r in range(world):
+            assert np.array_equal(res[r][case][1], want), (case, r)
+
+
 def _minmax_worker(rank, world, port, q):
     import sys
 

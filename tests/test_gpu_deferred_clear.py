@@ -262,3 +262,71 @@ def test_graph_capture_of_a_cleared_filter(rpt, log_nb, n):
         assert np.array_equal(out_sel[:cnt].cpu().numpy().view(np.uint32), want)
     assert np.array_equal(bf.export_words(), ref)
     assert hip.hipGraphExecDestroy(exe) == 0 and hip.hipGraphDestroy(graph) == 0
+
+
+@pytest.mark.parametrize("strategy,log_nb", [(INS_ATOMIC, 22), (INS_PARTITIONED, 21), (INS_PARTITIONED, 24),
+                                             (INS_BUCKETED, 25)])
+def test_graph_capture_of_inserts(rpt, strategy, log_nb):
+    """writes captured into a HIP graph. (1) An insert captured after a clear is refused (its
+    settling memset / whole-slice stores would replay with the graph and wipe what was inserted between
+    replays), and so is a clear inside a capture; each capture stays valid. (2) After rpt_bf_settle the insert
+    captures (every strategy, through rpt_bf_insert_ws with a workspace that outlives the graph); each replay
+    ORs its keys into whatever the filter holds by then: inserts made between replays survive, replays are
+    idempotent, words == the oracle's filter of every key inserted."""
+    import ctypes
+
+    from rpt_amd._lib import check
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    for fn in ("hipStreamBeginCapture", "hipStreamEndCapture", "hipGraphInstantiate", "hipGraphLaunch",
+               "hipGraphExecDestroy", "hipGraphDestroy"):
+        getattr(hip, fn).restype = ctypes.c_int
+    bf = filled(rpt, log_nb)
+    lib = bf._lib
+    n = 3_000_000 if strategy != INS_ATOMIC else 200_000
+    b, c, d = keys(n, 11), keys(200_000, 12), keys(200_000, 13)
+    kb = dev(b)
+    col = rpt.make_column(kb)
+    check(lib.rpt_bf_set_insert_strategy(bf.handle, strategy), lib)
+    ws_bytes = max(int(lib.rpt_bf_insert_workspace_bytes(bf.handle, n)), 256)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device="cuda:0")  # lives as long as the graph
+    s = torch.cuda.Stream(device="cuda:0")
+    sh = ctypes.c_void_p(s.cuda_stream)
+    graph, exe = ctypes.c_void_p(), ctypes.c_void_p()
+
+    def capture(op):
+        torch.cuda.synchronize()
+        assert hip.hipStreamBeginCapture(sh, 2) == 0  # hipStreamCaptureModeRelaxed
+        st = op()
+        assert hip.hipStreamEndCapture(sh, ctypes.byref(graph)) == 0  # still a valid capture
+        return st
+
+    def insert_b():
+        return lib.rpt_bf_insert_ws(bf.handle, ctypes.byref(col), n, ws.data_ptr(), ws_bytes, sh)
+
+    bf.clear()
+    assert capture(insert_b) == 1 and "rpt_bf_settle" in lib.rpt_last_error().decode()
+    assert hip.hipGraphDestroy(graph) == 0
+    assert capture(lambda: lib.rpt_bf_clear(bf.handle, sh)) == 1
+    assert "clear outside the capture" in lib.rpt_last_error().decode()
+    assert hip.hipGraphDestroy(graph) == 0
+    bf.settle()
+    bf.insert(dev(c))
+    assert capture(insert_b) == 0, lib.rpt_last_error().decode()
+    assert hip.hipGraphInstantiate(ctypes.byref(exe), graph, None, None, ctypes.c_size_t(0)) == 0
+    ref = orc.new_words(log_nb)
+    orc.insert_keys(ref, log_nb, c)  # the clear dropped the filled keys; the capture inserted nothing yet
+    torch.cuda.synchronize()
+    assert np.array_equal(bf.export_words(), ref)
+    orc.insert_keys(ref, log_nb, b)
+    for extra in (None, d, None):
+        if extra is not None:  # an insert between replays: kept by the next replay
+            bf.insert(dev(extra))
+            orc.insert_keys(ref, log_nb, extra)
+        torch.cuda.synchronize()
+        assert hip.hipGraphLaunch(exe, sh) == 0
+        s.synchronize()
+        assert np.array_equal(bf.export_words(), ref)
+    probe = np.concatenate([b[:20_000], keys(20_000, 14), d[:1000]])
+    assert np.array_equal(bf.lookup_sel(dev(probe)).cpu().numpy().astype(np.uint32), orc.probe_keys(ref, log_nb, probe))
+    assert hip.hipGraphExecDestroy(exe) == 0 and hip.hipGraphDestroy(graph) == 0

@@ -14,14 +14,20 @@ key min/max and has_data must be reduced:
   (slices over RPT_ALLREDUCE_ROUND_WORDS words), an empty rank, all ranks empty, a filter smaller than
   one 32-word slice granule;
 * C5's geometry: the 8 GiB / 2^30-block filter sized for 8e9 rows, W = 4;
-* an error injected inside a group: every rank fails with RPT_ERR_COLLECTIVE, every group is closed,
-  and the filters stay usable;
+* an error injected inside a group: every rank fails with RPT_ERR_COMM_ABORTED (the communicator was
+  aborted), every group is closed, and the filters stay usable;
 * non-blocking communicators (rpt_rccl_comm_init_rank_nonblocking): every grouped call and the all-reduce
   return ncclInProgress and the merge polls them to completion; results as with blocking ones;
 * a silent peer (a rank that dies mid-merge without posting its side): the surviving ranks' grouped calls
   "succeed" and their streams block, as with RCCL, so only the merge's bounded wait ends them: every
-  surviving rank aborts its communicator and returns RPT_ERR_COLLECTIVE within the collective timeout (at
-  once when RCCL reports the peer's death asynchronously), and no thread hangs.
+  surviving rank aborts its communicator and returns RPT_ERR_COMM_ABORTED within the collective timeout (at
+  once when RCCL reports the peer's death asynchronously), and no thread hangs;
+* the owner-aborts mode (rpt_collective_set_abort_on_error(0)) for a caller that owns its communicator: the
+  same failures return RPT_ERR_COLLECTIVE with every communicator untouched, and the owner's abort releases
+  the blocked streams;
+* the Python binding: an RcclComm whose merge aborted it is marked dead, and a second merge on it raises at
+  once (no freed communicator reaches RCCL);
+* rpt_rccl_comm_destroy of a non-blocking communicator finalizes it (ncclCommFinalize polled to completion).
 """
 import ctypes
 import os
@@ -40,12 +46,13 @@ pytestmark = pytest.mark.gpu
 LOOP_DIR = os.path.join(REPO, "tests", "loopback", "build")
 API_FIELDS = ["get_unique_id", "comm_init_rank", "comm_destroy", "group_start", "group_end", "send", "recv",
               "all_reduce", "comm_count", "comm_user_rank", "error_string", "comm_abort", "get_async_error",
-              "comm_init_rank_config"]
+              "comm_init_rank_config", "comm_finalize"]
 LOOP_SYMBOLS = ["ncclGetUniqueId", "ncclCommInitRank", "ncclCommDestroy", "ncclGroupStart", "ncclGroupEnd",
                 "ncclSend", "ncclRecv", "ncclAllReduce", "ncclCommCount", "ncclCommUserRank", "ncclGetErrorString",
-                "ncclCommAbort", "ncclCommGetAsyncError", "ncclCommInitRankConfig"]
+                "ncclCommAbort", "ncclCommGetAsyncError", "ncclCommInitRankConfig", "ncclCommFinalize"]
 ROUND_WORDS = 4 << 20  # RPT_ALLREDUCE_ROUND_WORDS
 RPT_ERR_COLLECTIVE = 6
+RPT_ERR_COMM_ABORTED = 7  # a merge that failed after its first collective call aborted the communicator
 
 
 class ApiTable(ctypes.Structure):  # rpt_rccl_api_table (csrc/rpt_gpu_testing.h)
@@ -69,6 +76,8 @@ def env():
     loop.rpt_loopback_stuck.argtypes = [ctypes.c_int]
     loop.rpt_loopback_group_depth.restype = ctypes.c_int
     loop.rpt_loopback_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+    loop.rpt_loopback_finalize_count.restype = ctypes.c_int
+    loop.ncclCommAbort.argtypes = [ctypes.c_void_p]
     table = ApiTable(*[ctypes.cast(getattr(loop, s), ctypes.c_void_p) for s in LOOP_SYMBOLS])
     assert tlib.rpt_testing_set_rccl_api(ctypes.byref(table)) == 0, tlib.rpt_last_error()
     yield tlib, loop
@@ -239,7 +248,7 @@ def test_loopback_allreduce_c5_geometry(env):
 @pytest.mark.parametrize("fail_rank,fail_op", [(1, 1), (0, 0), (2, 9)])
 def test_loopback_error_inside_group(env, fail_rank, fail_op):
     """An RCCL call failing inside a group: the failing rank closes its group before returning, every
-    rank's all-reduce returns RPT_ERR_COLLECTIVE (none hangs), no group stays open on any thread, and
+    rank's all-reduce returns RPT_ERR_COMM_ABORTED (none hangs), no group stays open on any thread, and
     each filter is still usable afterwards (its write order was released)."""
     tlib, loop = env
     world, log_nb = 3, 25  # 2^25 / 3 words per slice: 3 rounds, so op 9 lands in a later round
@@ -260,7 +269,7 @@ def test_loopback_error_inside_group(env, fail_rank, fail_op):
     finally:
         loop.rpt_loopback_fail_op(-1, -1)
     torch.cuda.synchronize()
-    assert st == [RPT_ERR_COLLECTIVE] * world
+    assert st == [RPT_ERR_COMM_ABORTED] * world
     assert depth == [0] * world
     for bf in bfs:  # still usable: a write after the failed merge and an export both complete
         bf.insert(torch.arange(1000, dtype=torch.int64, device="cuda:0"))
@@ -290,7 +299,7 @@ def test_loopback_silent_peer_is_bounded(env, silent_rank, silent_op, report):
     """A rank fails inside a group and goes silent (rpt_loopback_silent_peer): it never posts the rest of
     its sends and tells nobody. The surviving ranks' ncclGroupEnd / ncclAllReduce return success and their
     streams block, as RCCL's kernels would wait for the dead peer. rpt_bf_allreduce_or_ws must not wait
-    blindly: every rank returns RPT_ERR_COLLECTIVE, the survivors within the collective timeout (promptly
+    blindly: every rank returns RPT_ERR_COMM_ABORTED, the survivors within the collective timeout (promptly
     when ncclCommGetAsyncError reports the death), each communicator aborted (rpt_rccl_comm_destroy then
     does nothing), no thread left hanging, and the filters usable afterwards."""
     tlib, loop = env
@@ -319,7 +328,7 @@ def test_loopback_silent_peer_is_bounded(env, silent_rank, silent_op, report):
         loop.rpt_loopback_silent_peer(-1, -1, 0)
         assert tlib.rpt_collective_set_timeout_ms(prev) == 0
     torch.cuda.synchronize()  # every stream drained: the aborts released the blocked ones
-    assert st == [RPT_ERR_COLLECTIVE] * world, err
+    assert st == [RPT_ERR_COMM_ABORTED] * world, err
     assert depth == [0] * world
     for r in range(world):
         assert "communicator aborted" in err[r], err[r]
@@ -344,7 +353,7 @@ def test_loopback_nonblocking_comms(env, world, log_nb, n_build):
     """Non-blocking communicators: init, every ncclGroupEnd and the all-reduce return ncclInProgress and
     report it twice more through ncclCommGetAsyncError (the loopback's emulation), so the merge's polling of
     in-progress calls runs for every group; the merged filters equal the oracle's as with blocking ones."""
-    tlib, _loop = env
+    tlib, loop = env
     comms = make_comms(tlib, world, nonblocking=True)
     bfs, keys = build_partials(tlib, world, log_nb, n_build, set())
     st, _need = allreduce_all(tlib, bfs, comms)
@@ -354,7 +363,9 @@ def test_loopback_nonblocking_comms(env, world, log_nb, n_build):
     for r, bf in enumerate(bfs):
         assert np.array_equal(bf.export_words(), ref), f"rank {r} words"
         assert bf.minmax() == orc.minmax(keys)
-    destroy_comms(tlib, comms)
+    f0 = loop.rpt_loopback_finalize_count()
+    destroy_comms(tlib, comms)  # non-blocking: finalized (polled through ncclInProgress) before destroyed
+    assert loop.rpt_loopback_finalize_count() - f0 == world
     for bf in bfs:
         bf.close()
 
@@ -362,7 +373,7 @@ def test_loopback_nonblocking_comms(env, world, log_nb, n_build):
 def test_loopback_inprogress_forever_is_bounded(env):
     """A non-blocking communicator whose grouped call never leaves ncclInProgress (one rank, so nothing else
     waits): the merge polls it until the collective timeout, aborts the communicator and returns
-    RPT_ERR_COLLECTIVE; the filter stays usable and rpt_rccl_comm_destroy accepts the aborted handle."""
+    RPT_ERR_COMM_ABORTED; the filter stays usable and rpt_rccl_comm_destroy accepts the aborted handle."""
     tlib, loop = env
     bound_ms = 1500
     prev = tlib.rpt_collective_timeout_ms()
@@ -380,10 +391,100 @@ def test_loopback_inprogress_forever_is_bounded(env):
     finally:
         loop.rpt_loopback_stuck(0)
         assert tlib.rpt_collective_set_timeout_ms(prev) == 0
-    assert st == RPT_ERR_COLLECTIVE and "communicator aborted" in err, err
+    assert st == RPT_ERR_COMM_ABORTED and "communicator aborted" in err, err
     assert bound_ms / 1000 * 0.9 <= took < bound_ms / 1000 + 10, took
     torch.cuda.synchronize()
     bfs[0].insert(torch.arange(1000, dtype=torch.int64, device="cuda:0"))
     assert bfs[0].export_words().any()
     destroy_comms(tlib, comms)
     bfs[0].close()
+
+
+@pytest.mark.parametrize("silent_op,report", [(1, 0), (4, 1)])
+def test_loopback_owner_aborts_mode(env, silent_op, report):
+    """rpt_collective_set_abort_on_error(0), for a caller that owns its communicator: a silent peer
+    still ends every rank's merge within the bound, but with RPT_ERR_COLLECTIVE and the communicator NOT
+    aborted; the survivors' streams stay blocked in RCCL until the owner calls ncclCommAbort, which releases
+    them; the filters are usable afterwards."""
+    tlib, loop = env
+    world, log_nb, bound_ms, silent_rank = 3, 25, 2000, 1
+    prev = tlib.rpt_collective_timeout_ms()
+    assert tlib.rpt_collective_abort_on_error() == 1  # the default
+    assert tlib.rpt_collective_set_timeout_ms(bound_ms) == 0
+    assert tlib.rpt_collective_set_abort_on_error(0) == 0 and tlib.rpt_collective_abort_on_error() == 0
+    comms = make_comms(tlib, world)
+    bfs, _keys = build_partials(tlib, world, log_nb, 300_000, set())
+    need = tlib.rpt_allreduce_workspace_bytes(world, log_nb)
+    wss = [torch.empty(need, dtype=torch.uint8, device="cuda:0") for _ in range(world)]
+    streams = [torch.cuda.Stream(device="cuda:0") for _ in range(world)]
+    st, took, err = [None] * world, [None] * world, [None] * world
+
+    def run(r):
+        t0 = time.monotonic()
+        st[r] = tlib.rpt_bf_allreduce_or_ws(bfs[r].handle, comms[r], wss[r].data_ptr(), need, streams[r].cuda_stream)
+        took[r] = time.monotonic() - t0
+        err[r] = tlib.rpt_last_error().decode(errors="replace")
+
+    loop.rpt_loopback_silent_peer(silent_rank, silent_op, report)
+    try:
+        in_threads(world, run, join_timeout=bound_ms / 1000 * 4 + 30)
+    finally:
+        loop.rpt_loopback_silent_peer(-1, -1, 0)
+        assert tlib.rpt_collective_set_abort_on_error(1) == 0
+        assert tlib.rpt_collective_set_timeout_ms(prev) == 0
+    assert st == [RPT_ERR_COLLECTIVE] * world, err
+    for r in range(world):
+        assert "NOT aborted" in err[r] and "communicator aborted" not in err[r], err[r]
+        if r != silent_rank:
+            assert took[r] < bound_ms / 1000 + 10, (r, took[r])
+            assert "still blocked" in err[r], err[r]  # RCCL's kernels hold the survivor's stream
+            assert streams[r].query() is False
+    for c in comms:  # the owner aborts its communicators: the blocked streams resume
+        assert loop.ncclCommAbort(c) == 0
+    torch.cuda.synchronize()
+    for bf in bfs:
+        bf.insert(torch.arange(1000, dtype=torch.int64, device="cuda:0"))
+        assert bf.export_words().any()
+        bf.close()
+    # (the owner aborted them: not handed to rpt_rccl_comm_destroy)
+
+
+def test_python_comm_marked_dead_after_abort(env):
+    """rpt_amd.distributed.allreduce_or_native on a communicator a failed merge aborted: the error
+    carries RPT_ERR_COMM_ABORTED, the RcclComm drops its handle, and a second merge on it raises at once with a
+    clear message instead of passing a freed communicator to RCCL; close() is then a no-op."""
+    from rpt_amd._lib import RptError
+    from rpt_amd.distributed import RcclComm, allreduce_or_native
+
+    tlib, loop = env
+    world, log_nb = 2, 20
+    comms = make_comms(tlib, world)
+    bfs, _keys = build_partials(tlib, world, log_nb, 100_000, set())
+    pcs = []
+    for r in range(world):
+        c = RcclComm.__new__(RcclComm)  # an RcclComm around a loopback communicator of the test library
+        c._lib, c.handle, c.aborted, c.device, c.world, c.rank = tlib, comms[r], False, torch.device("cuda", 0), world, r
+        pcs.append(c)
+    errs = [None] * world
+
+    def run(r):
+        try:
+            allreduce_or_native(bfs[r], pcs[r], stream=torch.cuda.Stream(device="cuda:0"))
+        except RptError as e:
+            errs[r] = e
+
+    loop.rpt_loopback_fail_op(1, 1)
+    try:
+        in_threads(world, run)
+    finally:
+        loop.rpt_loopback_fail_op(-1, -1)
+    torch.cuda.synchronize()
+    for r in range(world):
+        assert errs[r] is not None and errs[r].status == RPT_ERR_COMM_ABORTED, errs[r]
+        assert pcs[r].aborted and pcs[r].handle is None
+        with pytest.raises(RptError) as e2:
+            allreduce_or_native(bfs[r], pcs[r])
+        assert e2.value.status == RPT_ERR_COLLECTIVE and "aborted by an earlier failed merge" in str(e2.value)
+        pcs[r].close()
+    for bf in bfs:
+        bf.close()
