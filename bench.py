@@ -94,6 +94,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "0")) or None,
                     help="CPU-baseline threads (default: this process's CPU share, see cpu_share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-only", action="store_true",
+                    help="print only the cpu_baseline object for this config (no GPU; e.g. to put the CPU "
+                         "restatement at T threads beside the host-resident GPU path of tools/host_bench)")
     ap.add_argument("--merge", default="native", choices=["native", "torch"],
                     help="N > 1: the product merge rpt_bf_allreduce_or_ws over RCCL (default; a failing "
                          "communicator exits non-zero), or the torch.distributed composition (reported as "
@@ -383,6 +386,16 @@ def launch_ranks(n: int) -> int:
 
 def main():
     args = parse()
+    if args.cpu_baseline_only:
+        cfg = args.config or "C2"
+        n_build = int(args.build_rows) if args.build_rows else CONFIGS[cfg][0](1)
+        n_filter = int(args.filter_rows) if args.filter_rows else (CONFIGS[cfg][1](1) if not args.build_rows else n_build)
+        sample = int(args.cpu_sample) if args.cpu_sample else int(args.probe_rows)
+        threads = args.cpu_threads or cpu_share()
+        cb = cpu_baseline(n_build, n_filter, int(round(args.p * 1000)), sample, threads,
+                          "--cpu-threads" if args.cpu_threads else "this process's CPU share", args.key_type)
+        print(json.dumps({"cpu_baseline": cb, "config": cfg, "key_type": args.key_type}), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "0"))
     if world == 0:
         if args.gpus > 1:

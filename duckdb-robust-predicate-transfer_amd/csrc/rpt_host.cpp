@@ -5,7 +5,10 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <exception>
 #include <limits>
 #include <thread>
 #include <utility>
@@ -151,6 +154,35 @@ bool flatten_converted(const Vector& v, uint64_t count, uint8_t* keys, uint64_t*
   return any_null;
 }
 
+// A DICTIONARY vector's keys gathered through its selection (element type T: the column's own width), 64 rows
+// per step: the index bound is checked once per step (the largest index), NULLs only when the dictionary has a
+// validity mask.
+template <typename T>
+bool flatten_dictionary(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* valid_words, uint64_t row0) {
+  const T* src = static_cast<const T*>(v.data);
+  T* dst = reinterpret_cast<T*>(keys);
+  bool any_null = false;
+  for (uint64_t r = 0; r < count; r += 64) {
+    const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));
+    const uint32_t* sel = v.sel + r;
+    uint32_t kmax = 0;
+    for (uint32_t e = 0; e < n; e++) kmax = std::max(kmax, sel[e]);
+    if (kmax >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
+    for (uint32_t e = 0; e < n; e++) {
+      T x;
+      std::memcpy(&x, src + sel[e], sizeof(T));
+      std::memcpy(dst + r + e, &x, sizeof(T));
+    }
+    if (v.validity) {
+      uint64_t nulls = 0;
+      for (uint32_t e = 0; e < n; e++) nulls |= static_cast<uint64_t>(!valid_bit(v.validity, sel[e])) << e;
+      any_null |= nulls != 0;
+      clear_bits(valid_words, row0 + r, nulls, n);
+    }
+  }
+  return any_null;
+}
+
 // Flatten one column of `chunk` (FLAT / CONSTANT / DICTIONARY / SEQUENCE) into `keys` and clear the bits of
 // its NULL rows at row offset `row0` of `valid_words` (preset to all-valid: a chunk without NULLs touches
 // no validity word), 64 rows per step. Returns true if any row was NULL. to_device: keys are device values
@@ -181,22 +213,14 @@ bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* va
       }
       break;
     }
-    case VectorType::DICTIONARY: {
-      const uint8_t* src = static_cast<const uint8_t*>(v.data);
-      for (uint64_t r = 0; r < count; r += 64) {
-        const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));
-        uint64_t nulls = 0;
-        for (uint32_t e = 0; e < n; e++) {
-          const uint32_t k = v.sel[r + e];
-          if (k >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
-          std::memcpy(keys + (r + e) * es, src + static_cast<uint64_t>(k) * es, es);
-          nulls |= static_cast<uint64_t>(!valid_bit(v.validity, k)) << e;
-        }
-        any_null |= nulls != 0;
-        clear_bits(valid_words, row0 + r, nulls, n);
+    case VectorType::DICTIONARY:
+      switch (es) {  // a fixed-size element per row: the gather compiles to plain loads and stores
+        case 1: any_null = flatten_dictionary<uint8_t>(v, count, keys, valid_words, row0); break;
+        case 2: any_null = flatten_dictionary<uint16_t>(v, count, keys, valid_words, row0); break;
+        case 4: any_null = flatten_dictionary<uint32_t>(v, count, keys, valid_words, row0); break;
+        default: any_null = flatten_dictionary<uint64_t>(v, count, keys, valid_words, row0); break;
       }
       break;
-    }
     case VectorType::SEQUENCE: {  // start + r * increment in two's complement (wraps as DuckDB's)
       uint64_t x = static_cast<uint64_t>(v.seq_start);
       const uint64_t inc = static_cast<uint64_t>(v.seq_increment);
@@ -241,28 +265,25 @@ Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, siz
     return nulls;
   };
   bool any_null = false;
-  const size_t n_threads = total >= (1u << 20) && n_chunks >= 16
-                               ? std::min<size_t>(std::max<size_t>(ctx.flatten_threads, 1),
-                                                  std::max(1u, std::thread::hardware_concurrency()))
-                               : 1;
-  if (n_threads <= 1) {
+  if (total < (1u << 20) || n_chunks < 16 || ctx.flatten_threads <= 1) {
     any_null = flatten_range(0, n_chunks);
   } else {
-    std::vector<std::thread> pool;
-    std::vector<char> nulls(n_threads, 0);
-    for (size_t t = 0; t < n_threads; t++) {
-      const size_t lo = n_chunks * t / n_threads, hi = n_chunks * (t + 1) / n_threads;
-      pool.emplace_back([&, t, lo, hi] { nulls[t] = flatten_range(lo, hi) ? 1 : 0; });
-    }
-    for (auto& th : pool) th.join();
+    // several ranges per worker thread, so uneven chunks (dictionaries, conversions) still balance
+    const size_t n_tasks = std::min<size_t>(n_chunks / 4, 4 * static_cast<size_t>(ctx.flatten_threads));
+    std::vector<char> nulls(n_tasks, 0);
+    ctx.parallel_for(n_tasks, [&](size_t t) {
+      nulls[t] = flatten_range(n_chunks * t / n_tasks, n_chunks * (t + 1) / n_tasks) ? 1 : 0;
+    });
     for (char c : nulls) any_null |= c != 0;
   }
   return Flattened{device_type(v0.key_type), hkeys, hvalid, any_null};
 }
 
-// Copy a flattened column to device buffers (dvalid is only written when the batch had NULLs).
-rpt_key_column copy_flattened(DeviceContext& ctx, const Flattened& f, uint64_t total, void* dkeys, void* dvalid) {
-  auto s = static_cast<hipStream_t>(ctx.stream());
+// Copy a flattened column to device buffers (dvalid is only written when the batch had NULLs), on `stream`
+// (default: the context's).
+rpt_key_column copy_flattened(DeviceContext& ctx, const Flattened& f, uint64_t total, void* dkeys, void* dvalid,
+                              void* stream = nullptr) {
+  auto s = static_cast<hipStream_t>(stream ? stream : ctx.stream());
   check_hip(hipMemcpyAsync(dkeys, f.keys, total * key_size(f.key_type), hipMemcpyHostToDevice, s), "stage keys");
   if (f.any_null)
     check_hip(hipMemcpyAsync(dvalid, f.valid, (total + 63) / 64 * 8, hipMemcpyHostToDevice, s), "stage validity");
@@ -371,14 +392,149 @@ struct PTBloomFilter::PipelineBuffers {
       d_cnt[b] = static_cast<uint64_t*>(ctx.dev(14 + b, 8));
     }
   }
-  // stage of buffer b copied to the device / probed (count on its way back) / sel back on the host
-  hipEvent_t staged(int b) { return static_cast<hipEvent_t>(ctx.event(b)); }
+  // stage of buffer b copied to the device (the pinned buffer may be refilled) / probed or inserted (the
+  // device key buffer may be overwritten; the count is on its way back) / sel back on the host
+  hipEvent_t copied(int b) { return static_cast<hipEvent_t>(ctx.event(b)); }
   hipEvent_t probed(int b) { return static_cast<hipEvent_t>(ctx.event(2 + b)); }
   hipEvent_t returned(int b) { return static_cast<hipEvent_t>(ctx.event(4 + b)); }
 };
 
 namespace {
+using Clock = std::chrono::steady_clock;
+
+// n empty selection vectors that keep the capacity a caller's earlier batch gave them: a caching operator
+// calls with the same vector every batch, and re-allocating ~16 Ki small vectors per call (then growing them
+// as survivors arrive) cost more than the copy of the batch itself (tools/host_bench: 21 ms of 35 per 2^25
+// rows on the GPU box, where fresh pages fault expensively).
+void reset_sels(std::vector<SelectionVector>& sels, size_t n) {
+  sels.resize(n);
+  for (SelectionVector& v : sels) v.clear();
+}
+double secs_since(Clock::time_point t0) { return std::chrono::duration<double>(Clock::now() - t0).count(); }
+
+// A stage's ascending sel (ids relative to the stage) -> per-chunk sels (ids relative to each chunk), over
+// the context's worker threads: each chunk's survivors are one contiguous range of the stage's sel.
+void split_sel(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, size_t c_lo, size_t c_hi,
+               const uint32_t* h_sel, uint64_t cnt, std::vector<SelectionVector>& sels) {
+  const size_t n_chunks = c_hi - c_lo;
+  std::vector<uint64_t> start(n_chunks + 1, 0);
+  for (size_t c = 0; c < n_chunks; c++) start[c + 1] = start[c] + chunks[c_lo + c]->count;
+  const uint32_t* const end = h_sel + cnt;
+  // the first id >= bound at or after p: galloping from p (a chunk's survivors are a few hundred ids on,
+  // so the search stays on lines the copy reads anyway; a binary search over the whole rest of the stage
+  // missed the cache at nearly every step: 21 ms per 2^25 rows on the GPU box)
+  auto next_at_least = [end](const uint32_t* p, uint32_t bound) {
+    size_t step = 16;
+    while (static_cast<size_t>(end - p) > step && p[step] < bound) {
+      p += step;
+      step *= 2;
+    }
+    return std::lower_bound(p, static_cast<size_t>(end - p) > step ? p + step + 1 : end, bound);
+  };
+  auto range = [&](size_t lo, size_t hi) {
+    const uint32_t* p = std::lower_bound(h_sel, end, static_cast<uint32_t>(start[lo]));
+    for (size_t c = lo; c < hi; c++) {
+      const uint32_t* e = next_at_least(p, static_cast<uint32_t>(start[c + 1]));
+      SelectionVector& out = sels[c_lo + c];
+      out.resize(static_cast<size_t>(e - p));
+      const uint32_t base = static_cast<uint32_t>(start[c]);
+      for (size_t x = 0; x < out.size(); x++) out[x] = p[x] - base;
+      p = e;
+    }
+  };
+  if (cnt < (1u << 16) || n_chunks < 64 || ctx.flatten_threads <= 1) {
+    range(0, n_chunks);
+    return;
+  }
+  const size_t n_tasks = std::min<size_t>(n_chunks / 16, 4 * static_cast<size_t>(ctx.flatten_threads));
+  ctx.parallel_for(n_tasks, [&](size_t t) { range(n_chunks * t / n_tasks, n_chunks * (t + 1) / n_tasks); });
+}
 }  // namespace
+
+// Persistent worker threads of a DeviceContext (parallel_for): workers sleep on a condition variable
+// between jobs; a job hands out task indices through an atomic counter, the caller works too.
+struct DeviceContext::Pool {
+  explicit Pool(unsigned n_workers) {
+    for (unsigned i = 0; i < n_workers; i++) workers.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    wake.notify_all();
+    for (auto& t : workers) t.join();
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu);
+      wake.wait(lk, [&] { return stop || gen != seen; });
+      if (stop) return;
+      seen = gen;
+      lk.unlock();
+      work();
+      lk.lock();
+      if (--active == 0) done.notify_all();
+    }
+  }
+  void work() {
+    for (;;) {
+      const size_t t = next.fetch_add(1);
+      if (t >= n) return;
+      try {
+        (*fn)(t);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (!err) err = std::current_exception();
+      }
+    }
+  }
+  // every worker takes part in every job, so a job cannot start before the previous one is done
+  void run(size_t n_tasks, const std::function<void(size_t)>& f) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      fn = &f;
+      n = n_tasks;
+      next.store(0);
+      active = workers.size();
+      err = nullptr;
+      gen++;
+    }
+    wake.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu);
+    done.wait(lk, [&] { return active == 0; });
+    fn = nullptr;
+    if (err) {
+      std::exception_ptr e = err;
+      err = nullptr;
+      std::rethrow_exception(e);
+    }
+  }
+  std::vector<std::thread> workers;
+  std::mutex mu, err_mu;
+  std::condition_variable wake, done;
+  const std::function<void(size_t)>* fn = nullptr;
+  size_t n = 0, active = 0;
+  std::atomic<size_t> next{0};
+  uint64_t gen = 0;
+  bool stop = false;
+  std::exception_ptr err;
+};
+
+void DeviceContext::parallel_for(size_t n, const std::function<void(size_t)>& fn) {
+  const unsigned threads = std::min<unsigned>(std::max(flatten_threads, 1u), std::max(1u, std::thread::hardware_concurrency()));
+  if (n <= 1 || threads <= 1) {
+    for (size_t t = 0; t < n; t++) fn(t);
+    return;
+  }
+  if (!pool_ || pool_->workers.size() != threads - 1) {
+    pool_.reset();
+    pool_ = std::make_unique<Pool>(threads - 1);
+  }
+  pool_->run(n, fn);
+}
 
 // ---- DeviceContext -----------------------------------------------------------------------------
 DeviceContext::DeviceContext(int device) : device_(device) {
@@ -389,23 +545,25 @@ DeviceContext::DeviceContext(int device) : device_(device) {
 }
 
 DeviceContext::~DeviceContext() {
+  pool_.reset();
   DeviceScope ds(device_);
-  if (stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(stream_));
-  if (copy_stream_) (void)hipStreamSynchronize(static_cast<hipStream_t>(copy_stream_));
+  for (void* st : {stream_, copy_stream_, h2d_stream_})
+    if (st) (void)hipStreamSynchronize(static_cast<hipStream_t>(st));
   for (auto& b : host_)
     if (b.p) (void)hipHostFree(b.p);
   for (auto& b : dev_)
     if (b.p) (void)hipFree(b.p);
   for (void* e : events_)
     if (e) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
-  if (copy_stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(copy_stream_));
-  if (stream_) (void)hipStreamDestroy(static_cast<hipStream_t>(stream_));
+  for (void* st : {h2d_stream_, copy_stream_, stream_})
+    if (st) (void)hipStreamDestroy(static_cast<hipStream_t>(st));
 }
 
 void DeviceContext::synchronize() {
   DeviceScope ds(device_);
   check_hip(hipStreamSynchronize(static_cast<hipStream_t>(stream_)), "hipStreamSynchronize");
   if (copy_stream_) check_hip(hipStreamSynchronize(static_cast<hipStream_t>(copy_stream_)), "hipStreamSynchronize");
+  if (h2d_stream_) check_hip(hipStreamSynchronize(static_cast<hipStream_t>(h2d_stream_)), "hipStreamSynchronize");
 }
 
 void* DeviceContext::copy_stream() {
@@ -418,7 +576,18 @@ void* DeviceContext::copy_stream() {
   return copy_stream_;
 }
 
+void* DeviceContext::h2d_stream() {
+  if (!h2d_stream_) {
+    DeviceScope ds(device_);
+    hipStream_t s;
+    check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    h2d_stream_ = s;
+  }
+  return h2d_stream_;
+}
+
 void* DeviceContext::event(int i) {
+  if (i < 0 || i >= kEvents) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "event index out of range");
   void*& e = events_[i];
   if (!e) {
     DeviceScope ds(device_);
@@ -565,36 +734,54 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
   InsertDevice(ctx, stage_key(ctx, chunks, cols, total), total);
 }
 
-// Stage by stage: flatten stage i into pinned buffer i % 2 while stage i-1 is copied and inserted
-// (stream order keeps the inserts serial; a pinned buffer is refilled once its copy has finished).
+// Stage by stage: the host flattens stage i into pinned buffer i % 2 while the host-to-device stream copies
+// stage i-1 and the context's stream inserts stage i-2 (inserts stay serial in stream order). A pinned
+// buffer is refilled once its copy has finished, a device key buffer once the insert that read it has.
 void PTBloomFilter::InsertPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col) {
+  const Clock::time_point t_begin = Clock::now();
+  DeviceContext::PipelineStats& ps = ctx.stats;
   const std::vector<StageRange> st = pipeline_stages(chunks, col, ctx.pipeline_rows);
-  uint64_t max_rows = 0;
+  uint64_t max_rows = 0, total = 0;
   size_t ws_bytes = 0;
   for (const StageRange& r : st) {
     max_rows = std::max(max_rows, r.rows);
+    total += r.rows;
     ws_bytes = std::max(ws_bytes, rpt_bf_insert_workspace_bytes(bf_, r.rows));
   }
   const size_t es = key_size(device_type(chunks[st[0].c_lo]->data.at(col).key_type));
   PipelineBuffers pb(ctx, max_rows, es);
   void* ws = ws_bytes ? ctx.dev(6, ws_bytes) : nullptr;
   auto s = static_cast<hipStream_t>(ctx.stream());
+  auto h = static_cast<hipStream_t>(ctx.h2d_stream());
   try {
     for (size_t i = 0; i < st.size(); i++) {
       const int b = static_cast<int>(i & 1);
-      if (i >= 2) check_hip(hipEventSynchronize(pb.staged(b)), "hipEventSynchronize");
+      Clock::time_point t0 = Clock::now();
+      if (i >= 2) check_hip(hipEventSynchronize(pb.copied(b)), "hipEventSynchronize");
+      ps.wait_copy_s += secs_since(t0);
+      t0 = Clock::now();
       const Flattened f = flatten_pinned(ctx, chunks.data() + st[i].c_lo, st[i].c_hi - st[i].c_lo, col, st[i].rows,
                                          PipelineBuffers::kHostKeys + 2 * b);
-      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b]);
-      check_hip(hipEventRecord(pb.staged(b), s), "hipEventRecord");
+      ps.flatten_s += secs_since(t0);
+      t0 = Clock::now();
+      if (i >= 2) check_hip(hipStreamWaitEvent(h, pb.probed(b), 0), "hipStreamWaitEvent");  // insert i-2 read it
+      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b], h);
+      check_hip(hipEventRecord(pb.copied(b), h), "hipEventRecord");
+      check_hip(hipStreamWaitEvent(s, pb.copied(b), 0), "hipStreamWaitEvent");
       if (rpt_bf_insert_workspace_bytes(bf_, st[i].rows)) check(rpt_bf_insert_ws(bf_, &kc, st[i].rows, ws, ws_bytes, s));
       else check(rpt_bf_insert(bf_, &kc, st[i].rows, s));
+      check_hip(hipEventRecord(pb.probed(b), s), "hipEventRecord");
+      ps.enqueue_s += secs_since(t0);
     }
   } catch (...) {
-    (void)hipStreamSynchronize(s);  // nothing may still read the staging buffers
+    (void)hipStreamSynchronize(h);  // nothing may still read the staging buffers
+    (void)hipStreamSynchronize(s);
     throw;
   }
   ctx.synchronize();
+  ps.stages += st.size();
+  ps.rows += total;
+  ps.total_s += secs_since(t_begin);
 }
 
 void PTBloomFilter::InsertDevice(DeviceContext& ctx, const rpt_key_column& col, uint64_t n) {
@@ -616,7 +803,7 @@ uint64_t PTBloomFilter::LookupSel(DeviceContext& ctx, const DataChunk& chunk, Se
 
 void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                                    std::vector<SelectionVector>& sels, const std::vector<uint64_t>& cols) const {
-  sels.assign(chunks.size(), SelectionVector());
+  reset_sels(sels, chunks.size());
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:63-65
   if (cols.size() == 1 && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
@@ -649,14 +836,7 @@ void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const D
     ctx.synchronize();
     h_sel = hs;
   }
-  // split the batch-wide ascending sel into per-chunk sels
-  uint64_t k = 0, start = 0;
-  for (size_t i = 0; i < chunks.size(); i++) {
-    const uint64_t end = start + chunks[i]->count;
-    SelectionVector& out = sels[i];
-    while (k < cnt && h_sel[k] < end) out.push_back(static_cast<uint32_t>(h_sel[k++] - start));
-    start = end;
-  }
+  split_sel(ctx, chunks, 0, chunks.size(), h_sel, cnt, sels);  // batch-wide ascending sel -> per-chunk sels
 }
 
 // Per-vector calls (one fused kernel): the kernel reads the flattened keys straight from the pinned
@@ -689,17 +869,23 @@ void PTBloomFilter::LookupSelMapped(DeviceContext& ctx, const std::vector<const 
   }
 }
 
-// Three stages in flight: while the host flattens stage i into pinned buffer i % 2, the compute stream
-// copies and probes stage i-1 (then copies its count back), and the copy stream brings stage i-2's
-// selection vector back (its exact length is known once that stage's count has arrived). A stage's
-// device sel buffer is reused once its copy back has finished (the compute stream waits on it).
+// Four stages in flight on three streams: while the host flattens stage i into pinned buffer i % 2, the
+// host-to-device stream copies stage i-1 to the device, the context's stream probes it once it is there (and
+// copies its count back), and the copy stream brings stage i-2's selection vector back (its exact length is
+// known once that stage's count has arrived); the host splits each stage's sel into per-chunk sels. Copies
+// in the two directions and the probes overlap, so the copy engine feeding the device is the limit when the
+// host keeps up. A pinned buffer is refilled once its copy has finished, a device key buffer once the probe
+// that read it has, a device sel buffer once its copy back has.
 void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                                        std::vector<SelectionVector>& sels, uint64_t col) const {
+  const Clock::time_point t_begin = Clock::now();
+  DeviceContext::PipelineStats& ps = ctx.stats;
   const std::vector<StageRange> st = pipeline_stages(chunks, col, ctx.pipeline_rows);
-  uint64_t max_rows = 0;
+  uint64_t max_rows = 0, total = 0;
   size_t ws_bytes = 16;
   for (const StageRange& r : st) {
     max_rows = std::max(max_rows, r.rows);
+    total += r.rows;
     ws_bytes = std::max(ws_bytes, rpt_bf_probe_workspace_bytes(bf_, r.rows));
   }
   const size_t es = key_size(device_type(chunks[st[0].c_lo]->data.at(col).key_type));
@@ -707,10 +893,13 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
   void* ws = ctx.dev(2, ws_bytes);
   auto s = static_cast<hipStream_t>(ctx.stream());
   auto d = static_cast<hipStream_t>(ctx.copy_stream());
+  auto h = static_cast<hipStream_t>(ctx.h2d_stream());
   uint64_t counts[2] = {0, 0};
   auto count_arrived = [&](size_t j) {  // stage j's count is on the host: copy its sel back exactly
     const int b = static_cast<int>(j & 1);
+    const Clock::time_point t0 = Clock::now();
     check_hip(hipEventSynchronize(pb.probed(b)), "hipEventSynchronize");
+    ps.wait_count_s += secs_since(t0);
     counts[b] = *pb.h_cnt[b];
     if (counts[b]) {
       check_hip(hipStreamWaitEvent(d, pb.probed(b), 0), "hipStreamWaitEvent");
@@ -720,28 +909,33 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
   };
   auto split = [&](size_t j) {  // stage j's ascending sel -> per-chunk sels (ids relative to each chunk)
     const int b = static_cast<int>(j & 1);
+    Clock::time_point t0 = Clock::now();
     check_hip(hipEventSynchronize(pb.returned(b)), "hipEventSynchronize");
-    const uint32_t* h_sel = pb.h_sel[b];
-    uint64_t k = 0, start = 0;
-    for (size_t c = st[j].c_lo; c < st[j].c_hi; c++) {
-      const uint64_t end = start + chunks[c]->count;
-      SelectionVector& out = sels[c];
-      while (k < counts[b] && h_sel[k] < end) out.push_back(static_cast<uint32_t>(h_sel[k++] - start));
-      start = end;
-    }
+    ps.wait_sel_s += secs_since(t0);
+    t0 = Clock::now();
+    split_sel(ctx, chunks, st[j].c_lo, st[j].c_hi, pb.h_sel[b], counts[b], sels);
+    ps.split_s += secs_since(t0);
   };
   try {
     for (size_t i = 0; i < st.size(); i++) {
       const int b = static_cast<int>(i & 1);
-      if (i >= 2) check_hip(hipEventSynchronize(pb.staged(b)), "hipEventSynchronize");
+      Clock::time_point t0 = Clock::now();
+      if (i >= 2) check_hip(hipEventSynchronize(pb.copied(b)), "hipEventSynchronize");
+      ps.wait_copy_s += secs_since(t0);
+      t0 = Clock::now();
       const Flattened f = flatten_pinned(ctx, chunks.data() + st[i].c_lo, st[i].c_hi - st[i].c_lo, col, st[i].rows,
                                          PipelineBuffers::kHostKeys + 2 * b);
-      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b]);
-      check_hip(hipEventRecord(pb.staged(b), s), "hipEventRecord");
-      if (i >= 2) check_hip(hipStreamWaitEvent(s, pb.returned(b), 0), "hipStreamWaitEvent");
+      ps.flatten_s += secs_since(t0);
+      t0 = Clock::now();
+      if (i >= 2) check_hip(hipStreamWaitEvent(h, pb.probed(b), 0), "hipStreamWaitEvent");  // probe i-2 read it
+      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b], h);
+      check_hip(hipEventRecord(pb.copied(b), h), "hipEventRecord");
+      check_hip(hipStreamWaitEvent(s, pb.copied(b), 0), "hipStreamWaitEvent");
+      if (i >= 2) check_hip(hipStreamWaitEvent(s, pb.returned(b), 0), "hipStreamWaitEvent");  // d_sel[b] free
       check(rpt_bf_probe(bf_, &kc, nullptr, st[i].rows, pb.d_sel[b], pb.d_cnt[b], ws, ws_bytes, s));
       check_hip(hipMemcpyAsync(pb.h_cnt[b], pb.d_cnt[b], 8, hipMemcpyDeviceToHost, s), "copy count");
       check_hip(hipEventRecord(pb.probed(b), s), "hipEventRecord");
+      ps.enqueue_s += secs_since(t0);
       if (i >= 1) count_arrived(i - 1);
       if (i >= 2) split(i - 2);
     }
@@ -750,10 +944,12 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
     if (n >= 2) split(n - 2);
     split(n - 1);
   } catch (...) {
-    (void)hipStreamSynchronize(s);  // nothing may still read or write the staging buffers
-    (void)hipStreamSynchronize(d);
+    for (hipStream_t x : {h, s, d}) (void)hipStreamSynchronize(x);  // nothing may still use the staging buffers
     throw;
   }
+  ps.stages += st.size();
+  ps.rows += total;
+  ps.total_s += secs_since(t_begin);
 }
 
 void PTBloomFilter::ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const std::vector<DataChunk>& data,
@@ -1061,7 +1257,7 @@ uint64_t UseBF::Execute(DeviceContext& ctx, const DataChunk& input, SelectionVec
 
 uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& inputs,
                              std::vector<SelectionVector>& outs) const {
-  outs.assign(inputs.size(), SelectionVector());
+  reset_sels(outs, inputs.size());
   const uint64_t total = total_rows(inputs);
   auto all_rows = [&] {
     for (size_t i = 0; i < inputs.size(); i++) {
@@ -1077,6 +1273,27 @@ uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChu
     return all_rows();
   }
   if (total >= (1ULL << 32)) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "batch exceeds uint32 row ids");
+  {
+    // one applicable filter over a large batch: LookupSelBatch's pipeline (flatten, copy, probe and copy
+    // back of successive stages overlap) gives the same per-chunk sels
+    const PTBloomFilter* only = nullptr;
+    size_t only_i = 0, applicable = 0;
+    for (size_t i = 0; i < filters_.size(); i++) {
+      const auto& bf = filters_[i];
+      if (!bf || !bf->finalized_) continue;  // cpp:139-142
+      if (bf->IsEmpty()) return 0;           // cpp:145-155
+      applicable++;
+      only = bf.get();
+      only_i = i;
+    }
+    if (applicable == 1 && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
+      only->LookupSelBatch(ctx, inputs, outs, {cols_[only_i]});
+      uint64_t count = 0;
+      for (const SelectionVector& o : outs) count += o.size();
+      rows_out_ += count;
+      return count;
+    }
+  }
   auto s = static_cast<hipStream_t>(ctx.stream());
   uint32_t* d_rows = nullptr;  // surviving row ids (ascending, over the batch); nullptr = every row
   uint64_t count = total;
@@ -1106,12 +1323,7 @@ uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChu
   auto* h_rows = static_cast<uint32_t*>(ctx.host(3, count * 4));
   check_hip(hipMemcpyAsync(h_rows, d_rows, count * 4, hipMemcpyDeviceToHost, s), "copy sel");
   ctx.synchronize();
-  uint64_t k = 0, start = 0;
-  for (size_t i = 0; i < inputs.size(); i++) {
-    const uint64_t end = start + inputs[i]->count;
-    while (k < count && h_rows[k] < end) outs[i].push_back(static_cast<uint32_t>(h_rows[k++] - start));
-    start = end;
-  }
+  split_sel(ctx, inputs, 0, inputs.size(), h_rows, count, outs);
   return count;
 }
 

@@ -15,6 +15,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <stdexcept>
@@ -90,28 +91,54 @@ class DeviceContext {
   // the device address of host slot `slot`'s pinned buffer (kernels read / write it in place), cached
   // until the slot grows
   void* host_device_ptr(int slot);
-  // internal: the device-to-host stream of pipelined batches (created on first use) and its events
+  // internal: the device-to-host stream of pipelined batches, the host-to-device stream that feeds them
+  // (created on first use), and their events
   void* copy_stream();
+  void* h2d_stream();
+  static constexpr int kEvents = 16;
   void* event(int i);
+  // internal: run fn(0) .. fn(n - 1) on this context's worker threads (flatten_threads of them, the caller
+  // included; created on first use and kept, so a stage costs no thread start-up); rethrows the first
+  // exception a task threw, after every task has finished.
+  void parallel_for(size_t n, const std::function<void(size_t)>& fn);
 
   // Single-column batches of at least 2 * pipeline_rows rows are staged in stages of about this many
-  // rows (whole chunks): flattening stage i+1 on the host overlaps the copy and probe / insert of
-  // stage i and the copy back of stage i-1's selection vector.
+  // rows (whole chunks): flattening stage i+1 on the host overlaps the copy of stage i, the probe of
+  // stage i-1 and the copy back of stage i-2's selection vector.
   uint64_t pipeline_rows = 1ULL << 22;
-  // Host threads that flatten a batch (or stage) of >= 1 Mi rows into pinned memory.
+  // Host threads (the calling one included) that flatten a batch or stage of >= 1 Mi rows into pinned
+  // memory and split a stage's selection vector into per-chunk ones. DuckDB's operator threads each own a
+  // DeviceContext, so with many of them 1-2 per context is enough.
   unsigned flatten_threads = 8;
+
+  // Host-side time of the pipelined batch paths by phase (accumulated; reset by assigning {}): where a
+  // host-resident batch's time goes (tools/host_bench reports it).
+  struct PipelineStats {
+    uint64_t stages = 0, rows = 0;
+    double flatten_s = 0;     // chunks -> pinned staging (worker threads)
+    double enqueue_s = 0;     // copy / probe / insert launches
+    double wait_copy_s = 0;   // waiting for a pinned buffer's previous copy to finish before refilling it
+    double wait_count_s = 0;  // waiting for a stage's survivor count (probe done)
+    double wait_sel_s = 0;    // waiting for a stage's selection vector to arrive on the host
+    double split_s = 0;       // stage sel -> per-chunk sels (worker threads)
+    double total_s = 0;
+  };
+  PipelineStats stats;
 
  private:
   int device_;
   void* stream_ = nullptr;
   void* copy_stream_ = nullptr;
+  void* h2d_stream_ = nullptr;
   struct Buf {
     void* p = nullptr;
     size_t cap = 0;
     void* dp = nullptr;  // host slots: device address of p (0 until asked for)
   };
   Buf host_[kSlots], dev_[kSlots];
-  void* events_[8] = {};
+  void* events_[kEvents] = {};
+  struct Pool;
+  std::unique_ptr<Pool> pool_;
 };
 
 // One key column kept in HBM, one segment per staged batch: the device half of CREATE_BF's

@@ -401,9 +401,68 @@ static void typed_keys(int dev) {
   EXPECT(sel.size() >= 2 && sel[0] == 0 && sel[1] == 1, "DOUBLE: -0.0 / NaN equality transform");
 }
 
+// Pipelined batches big enough for the context's worker threads (stages of >= 1 Mi rows are flattened, and
+// stage sels of >= 64 Ki survivors split, on flatten_threads threads): FLAT / DICTIONARY chunks with NULLs,
+// both key columns, the selection vectors reused across calls (their capacity is kept), UseBF::ExecuteBatch's
+// single-filter route through the pipeline; every chunk against the oracle.
+static void pipelined_workers(int dev) {
+  const size_t nb = (2u << 20) + 777, np = (3u << 20) + 1234;  // both pipelined (>= 2 stages of 1 Mi rows)
+  Table bt = make_table(nb, 11, 53, 0), pt = make_table(np, 12, 41, 0);
+  ChunkStore bst, pst;
+  make_chunks(bt, nb, bst, false);
+  make_chunks(pt, np, pst, false);
+  std::vector<const rpt::DataChunk*> bptrs, pptrs;
+  for (const auto& ch : bst.chunks) bptrs.push_back(&ch);
+  for (const auto& ch : pst.chunks) pptrs.push_back(&ch);
+  for (int c = 0; c < 2; c++) {
+    rpt::DeviceContext ctx(dev);
+    ctx.pipeline_rows = 1u << 20;
+    ctx.flatten_threads = 4;
+    auto f = std::make_shared<rpt::PTBloomFilter>();
+    f->Initialize(dev, static_cast<uint32_t>(nb));
+    f->InsertBatch(ctx, bptrs, {static_cast<uint64_t>(c)});
+    const int lnb = f->LogNumBlocks();
+    std::vector<uint64_t> w(1ULL << lnb, 0);
+    const std::vector<uint64_t> vb = pack(c == 0 ? bt.v0 : bt.v1, 0, nb);
+    if (c == 0) rpt_oracle_insert_i64(w.data(), lnb, bt.c0.data(), nullptr, vb.data(), nb);
+    else rpt_oracle_insert_i32(w.data(), lnb, bt.c1.data(), nullptr, vb.data(), nb);
+    EXPECT(f->ExportWords() == w, "worker-thread pipelined insert (column %d) differs from the oracle", c);
+    f->finalized_ = true;
+    // expected sels per chunk (chunk k = rows [2048 k, ...))
+    std::vector<rpt::SelectionVector> want(pptrs.size());
+    size_t total = 0;
+    for (size_t k = 0; k < pptrs.size(); k++) {
+      const size_t lo = 2048 * k, cnt = pptrs[k]->count;
+      const std::vector<uint64_t> vp = pack(c == 0 ? pt.v0 : pt.v1, lo, cnt);
+      want[k].resize(cnt);
+      const uint64_t ne = c == 0 ? rpt_oracle_probe_i64(w.data(), lnb, pt.c0.data() + lo, nullptr, vp.data(), cnt, want[k].data())
+                                 : rpt_oracle_probe_i32(w.data(), lnb, pt.c1.data() + lo, nullptr, vp.data(), cnt, want[k].data());
+      want[k].resize(ne);
+      total += ne;
+    }
+    EXPECT(total > (1u << 17), "column %d: %zu survivors (the split must run on the workers)", c, total);
+    std::vector<rpt::SelectionVector> sels;
+    for (int rep = 0; rep < 2; rep++) {  // the second call reuses the vectors the first one filled
+      ctx.stats = {};
+      f->LookupSelBatch(ctx, pptrs, sels, {static_cast<uint64_t>(c)});
+      EXPECT(sels.size() == pptrs.size() && ctx.stats.stages >= 3 && ctx.stats.rows == np, "pipeline stats (column %d)", c);
+      size_t bad = 0;
+      for (size_t k = 0; k < pptrs.size(); k++) bad += sels[k] != want[k];
+      EXPECT(bad == 0, "worker-thread pipelined lookup (column %d, call %d): %zu chunks differ", c, rep, bad);
+    }
+    rpt::UseBF ub({f}, {static_cast<uint64_t>(c)});
+    std::vector<rpt::SelectionVector> outs(5, rpt::SelectionVector(7, 9));  // stale contents must not leak
+    const uint64_t got = ub.ExecuteBatch(ctx, pptrs, outs);
+    size_t bad = 0;
+    for (size_t k = 0; k < pptrs.size(); k++) bad += outs[k] != want[k];
+    EXPECT(got == total && outs.size() == pptrs.size() && bad == 0, "ExecuteBatch through the pipeline (column %d): %zu chunks differ", c, bad);
+  }
+}
+
 int main() {
   try {
     const int dev = 0;
+    pipelined_workers(dev);
     // ---------------- build -------------------------------------------------------------------
     const size_t nb = 50001;
     Table bt = make_table(nb, 1, 97, 2048);

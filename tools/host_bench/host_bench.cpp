@@ -18,8 +18,171 @@
 
 #include "rpt_host.hpp"
 
+namespace {
+using clk = std::chrono::steady_clock;
+double since(clk::time_point t0) { return std::chrono::duration<double>(clk::now() - t0).count(); }
+
+void print_stats(const char* what, const rpt::DeviceContext::PipelineStats& ps, double calls) {
+  printf("\"%s\": {\"stages_per_call\": %.1f, \"flatten_ms\": %.3f, \"enqueue_ms\": %.3f, \"wait_copy_ms\": %.3f, "
+         "\"wait_count_ms\": %.3f, \"wait_sel_ms\": %.3f, \"split_ms\": %.3f, \"total_ms\": %.3f}",
+         what, ps.stages / calls, ps.flatten_s / calls * 1e3, ps.enqueue_s / calls * 1e3, ps.wait_copy_s / calls * 1e3,
+         ps.wait_count_s / calls * 1e3, ps.wait_sel_s / calls * 1e3, ps.split_s / calls * 1e3, ps.total_s / calls * 1e3);
+}
+
+// The host -> device path of a DuckDB shim for JOB's INTEGER keys and for BIGINT keys:
+// FLAT int64, FLAT int32 and DICTIONARY int32 2048-row chunks through LookupSelBatch's pipeline (4 Mi-row
+// stages) with 1..16 worker threads per call, the host-side time of each phase per call (DeviceContext::
+// stats), then T operator threads each driving its own DeviceContext through UseBF::ExecuteBatch.
+int host_path(int dev) {
+  const size_t n_build = 10000000, n_probe = 1ULL << 25;  // C2's filter; 33.5M probe rows = 16384 chunks
+  std::mt19937_64 rng(7);
+  std::vector<int64_t> b64(n_build), p64(n_probe);
+  for (auto& k : b64) k = static_cast<int64_t>(rng() >> 1);
+  for (size_t i = 0; i < n_probe; i++) p64[i] = (rng() % 10 == 0) ? b64[rng() % n_build] : static_cast<int64_t>(rng() >> 1);
+  std::vector<int32_t> b32(n_build), p32(n_probe);
+  for (size_t i = 0; i < n_build; i++) b32[i] = static_cast<int32_t>(b64[i]);
+  for (size_t i = 0; i < n_probe; i++) p32[i] = static_cast<int32_t>(p64[i]);
+  // DICTIONARY int32 chunks: a 64 Ki-entry dictionary (a tenth of it build keys) and a random selection
+  const size_t n_dict = 1 << 16;
+  std::vector<int32_t> dict(n_dict);
+  for (size_t i = 0; i < n_dict; i++) dict[i] = (i % 10 == 0) ? b32[rng() % n_build] : static_cast<int32_t>(rng());
+  std::vector<uint32_t> dsel(n_probe);
+  for (auto& x : dsel) x = static_cast<uint32_t>(rng() % n_dict);
+  auto make = [&](const char* kind) {
+    std::vector<rpt::DataChunk> cs;
+    for (size_t lo = 0; lo < n_probe; lo += 2048) {
+      rpt::DataChunk c;
+      c.count = std::min<size_t>(2048, n_probe - lo);
+      rpt::Vector x;
+      if (std::strcmp(kind, "i64_flat") == 0) {
+        x.key_type = rpt::KeyType::I64;
+        x.data = p64.data() + lo;
+      } else if (std::strcmp(kind, "i32_flat") == 0) {
+        x.key_type = rpt::KeyType::I32;
+        x.data = p32.data() + lo;
+      } else {
+        x.type = rpt::VectorType::DICTIONARY;
+        x.key_type = rpt::KeyType::I32;
+        x.data = dict.data();
+        x.sel = dsel.data() + lo;
+        x.dict_size = n_dict;
+      }
+      c.data.push_back(x);
+      cs.push_back(c);
+    }
+    return cs;
+  };
+  auto build_chunks = [&](bool i32) {
+    std::vector<rpt::DataChunk> cs;
+    for (size_t lo = 0; lo < n_build; lo += 2048) {
+      rpt::DataChunk c;
+      c.count = std::min<size_t>(2048, n_build - lo);
+      rpt::Vector x;
+      x.key_type = i32 ? rpt::KeyType::I32 : rpt::KeyType::I64;
+      x.data = i32 ? static_cast<const void*>(b32.data() + lo) : static_cast<const void*>(b64.data() + lo);
+      c.data.push_back(x);
+      cs.push_back(c);
+    }
+    return cs;
+  };
+  for (const char* kind : {"i64_flat", "i32_flat", "i32_dict"}) {
+    const bool i32 = kind[1] == '3';
+    const size_t key_bytes = i32 ? 4 : 8;
+    auto pch = make(kind);
+    auto bch = build_chunks(i32);
+    rpt::DeviceContext ctx(dev);
+    auto bf = std::make_shared<rpt::PTBloomFilter>();
+    bf->Initialize(dev, static_cast<uint32_t>(n_build));
+    {
+      std::vector<const rpt::DataChunk*> all;
+      for (auto& c : bch) all.push_back(&c);
+      bf->InsertBatch(ctx, all, {0});  // warm-up
+      ctx.stats = {};
+      const auto t0 = clk::now();
+      bf->InsertBatch(ctx, all, {0});
+      const double sec = since(t0);
+      printf("{\"op\": \"host_path.InsertBatch\", \"keys\": \"%s\", \"rows\": %zu, \"rows_per_s\": %.4g, ", i32 ? "i32_flat" : "i64_flat",
+             n_build, n_build / sec);
+      print_stats("phases", ctx.stats, 1);
+      printf("}\n");
+    }
+    bf->finalized_ = true;
+    std::vector<const rpt::DataChunk*> all;
+    for (auto& c : pch) all.push_back(&c);
+    std::vector<rpt::SelectionVector> sels;
+    for (uint64_t stage : {uint64_t(1) << 21, uint64_t(1) << 22, uint64_t(1) << 23})
+      for (unsigned th : {1u, 2u, 4u, 8u, 16u}) {
+        if (stage != (uint64_t(1) << 22) && th != 8) continue;
+        ctx.pipeline_rows = stage;
+        ctx.flatten_threads = th;
+        bf->LookupSelBatch(ctx, all, sels, {0});  // warm-up (pool, staging)
+        ctx.stats = {};
+        const int calls = 4;
+        size_t surv = 0;
+        const auto t0 = clk::now();
+        for (int c = 0; c < calls; c++) {
+          bf->LookupSelBatch(ctx, all, sels, {0});
+          for (auto& sv : sels) surv += sv.size();
+        }
+        const double sec = since(t0);
+        const double rows = static_cast<double>(calls) * n_probe;
+        printf("{\"op\": \"host_path.LookupSelBatch\", \"keys\": \"%s\", \"chunks_per_call\": %zu, \"pipeline_rows\": %llu, "
+               "\"worker_threads\": %u, \"rows_per_s\": %.4g, \"h2d_GBps\": %.1f, \"pass_fraction\": %.4f, ",
+               kind, all.size(), static_cast<unsigned long long>(stage), th, rows / sec, rows * key_bytes / sec / 1e9,
+               surv / rows);
+        print_stats("phases_per_call", ctx.stats, calls);
+        printf("}\n");
+        fflush(stdout);
+      }
+    // T operator threads (DuckDB's parallel USE_BF), each with its own DeviceContext, each calling
+    // UseBF::ExecuteBatch on 4096-chunk (8 Mi-row) batches of the column
+    for (int T : {1, 2, 4, 8, 16}) {
+      const unsigned per_ctx = std::max(1, 16 / T);
+      std::vector<std::unique_ptr<rpt::DeviceContext>> ctxs;
+      std::vector<std::unique_ptr<rpt::UseBF>> ops;
+      for (int t = 0; t < T; t++) {
+        ctxs.push_back(std::make_unique<rpt::DeviceContext>(dev));
+        ctxs.back()->flatten_threads = per_ctx;
+        ops.push_back(std::make_unique<rpt::UseBF>(std::vector<std::shared_ptr<rpt::PTBloomFilter>>{bf}, std::vector<uint64_t>{0}));
+      }
+      const size_t per_batch = 4096, batches_per_thread = 4;
+      auto batch = [&](int t, size_t k) {
+        std::vector<const rpt::DataChunk*> b;
+        const size_t first = ((static_cast<size_t>(t) * batches_per_thread + k) * per_batch) % pch.size();
+        for (size_t j = 0; j < per_batch; j++) b.push_back(&pch[(first + j) % pch.size()]);
+        return b;
+      };
+      for (int t = 0; t < T; t++) {  // warm-up
+        std::vector<rpt::SelectionVector> outs;
+        ops[t]->ExecuteBatch(*ctxs[t], batch(t, 0), outs);
+      }
+      std::vector<size_t> surv(T, 0);
+      const auto t0 = clk::now();
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+          std::vector<rpt::SelectionVector> outs;
+          for (size_t k = 0; k < batches_per_thread; k++) surv[t] += ops[t]->ExecuteBatch(*ctxs[t], batch(t, k), outs);
+        });
+      for (auto& x : th) x.join();
+      const double sec = since(t0);
+      const double rows = static_cast<double>(T) * batches_per_thread * per_batch * 2048;
+      size_t s_all = 0;
+      for (size_t x : surv) s_all += x;
+      printf("{\"op\": \"host_path.ExecuteBatch\", \"keys\": \"%s\", \"operator_threads\": %d, \"worker_threads_per_context\": %u, "
+             "\"chunks_per_call\": %zu, \"rows_per_s\": %.4g, \"h2d_GBps\": %.1f, \"pass_fraction\": %.4f}\n",
+             kind, T, per_ctx, per_batch, rows / sec, rows * key_bytes / sec / 1e9, s_all / rows);
+      fflush(stdout);
+    }
+  }
+  return 0;
+}
+}  // namespace
+
 int main(int argc, char** argv) {
   const int dev = 0;
+  // --host-path: only the host -> device path section above (int64 / int32 / dictionary keys)
+  if (argc > 1 && std::strcmp(argv[1], "--host-path") == 0) return host_path(dev);
   // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
   // synchronize waits for the device (per-vector call latency experiment)
   if (argc > 1 && std::strcmp(argv[1], "--spin") == 0) {
@@ -48,7 +211,6 @@ int main(int argc, char** argv) {
   rpt::DeviceContext ctx(dev);
   rpt::PTBloomFilter bf;
   bf.Initialize(dev, static_cast<uint32_t>(n_build));
-  using clk = std::chrono::steady_clock;
   {
     std::vector<const rpt::DataChunk*> all;
     for (auto& c : bchunks) all.push_back(&c);
