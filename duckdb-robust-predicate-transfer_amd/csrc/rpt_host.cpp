@@ -3,6 +3,7 @@
 #include "rpt_host.hpp"
 
 #include <hip/hip_runtime_api.h>
+#include <emmintrin.h>  // SSE2 streaming stores (x86-64 baseline) for the pinned staging copies
 
 #include <algorithm>
 #include <chrono>
@@ -154,6 +155,35 @@ bool flatten_converted(const Vector& v, uint64_t count, uint8_t* keys, uint64_t*
   return any_null;
 }
 
+// A FLAT vector's bytes into pinned staging memory the device will read by DMA: streaming (non-temporal)
+// 16-B stores, which skip the read-for-ownership of every destination line a plain memcpy of a 16 KiB vector
+// does (the staging buffer is not read back by the host), then a store fence so the DMA sees the bytes.
+void copy_to_staging(uint8_t* dst, const void* src_v, size_t bytes) {
+  const uint8_t* src = static_cast<const uint8_t*>(src_v);
+  const size_t head = std::min(bytes, static_cast<size_t>((16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15));
+  if (bytes < 256) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  std::memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  bytes -= head;
+  size_t i = 0;
+  for (; i + 64 <= bytes; i += 64) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+    const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+    const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+    _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+  }
+  std::memcpy(dst + i, src + i, bytes - i);
+  _mm_sfence();
+}
+
 // A DICTIONARY vector's keys gathered through its selection (element type T: the column's own width), 64 rows
 // per step: the index bound is checked once per step (the largest index), NULLs only when the dictionary has a
 // validity mask.
@@ -195,7 +225,7 @@ bool flatten_column(const Vector& v, uint64_t count, uint8_t* keys, uint64_t* va
   bool any_null = false;
   switch (v.type) {
     case VectorType::FLAT:
-      std::memcpy(keys, v.data, count * es);
+      copy_to_staging(keys, v.data, count * es);
       if (v.validity) {
         for (uint64_t r = 0; r < count; r += 64) {
           const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - r));

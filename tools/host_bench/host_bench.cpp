@@ -33,7 +33,7 @@ void print_stats(const char* what, const rpt::DeviceContext::PipelineStats& ps, 
 // FLAT int64, FLAT int32 and DICTIONARY int32 2048-row chunks through LookupSelBatch's pipeline (4 Mi-row
 // stages) with 1..16 worker threads per call, the host-side time of each phase per call (DeviceContext::
 // stats), then T operator threads each driving its own DeviceContext through UseBF::ExecuteBatch.
-int host_path(int dev) {
+int host_path(int dev, bool trace) {
   const size_t n_build = 10000000, n_probe = 1ULL << 25;  // C2's filter; 33.5M probe rows = 16384 chunks
   std::mt19937_64 rng(7);
   std::vector<int64_t> b64(n_build), p64(n_probe);
@@ -85,7 +85,9 @@ int host_path(int dev) {
     }
     return cs;
   };
-  for (const char* kind : {"i64_flat", "i32_flat", "i32_dict"}) {
+  const std::vector<const char*> kinds = trace ? std::vector<const char*>{"i64_flat", "i32_flat"}
+                                               : std::vector<const char*>{"i64_flat", "i32_flat", "i32_dict"};
+  for (const char* kind : kinds) {
     const bool i32 = kind[1] == '3';
     const size_t key_bytes = i32 ? 4 : 8;
     auto pch = make(kind);
@@ -113,18 +115,22 @@ int host_path(int dev) {
     for (uint64_t stage : {uint64_t(1) << 21, uint64_t(1) << 22, uint64_t(1) << 23})
       for (unsigned th : {1u, 2u, 4u, 8u, 16u}) {
         if (stage != (uint64_t(1) << 22) && th != 8) continue;
+        if (trace && (stage != (uint64_t(1) << 22) || th != 8)) continue;
         ctx.pipeline_rows = stage;
         ctx.flatten_threads = th;
         bf->LookupSelBatch(ctx, all, sels, {0});  // warm-up (pool, staging)
         ctx.stats = {};
         const int calls = 4;
         size_t surv = 0;
-        const auto t0 = clk::now();
+        double sec = 0;
         for (int c = 0; c < calls; c++) {
+          // --host-path-trace: 20 ms of idle between calls, so a copy trace shows each call on its own
+          if (trace) std::this_thread::sleep_for(std::chrono::milliseconds(20));
+          const auto t0 = clk::now();
           bf->LookupSelBatch(ctx, all, sels, {0});
+          sec += since(t0);
           for (auto& sv : sels) surv += sv.size();
         }
-        const double sec = since(t0);
         const double rows = static_cast<double>(calls) * n_probe;
         printf("{\"op\": \"host_path.LookupSelBatch\", \"keys\": \"%s\", \"chunks_per_call\": %zu, \"pipeline_rows\": %llu, "
                "\"worker_threads\": %u, \"rows_per_s\": %.4g, \"h2d_GBps\": %.1f, \"pass_fraction\": %.4f, ",
@@ -137,6 +143,7 @@ int host_path(int dev) {
     // T operator threads (DuckDB's parallel USE_BF), each with its own DeviceContext, each calling
     // UseBF::ExecuteBatch on 4096-chunk (8 Mi-row) batches of the column
     for (int T : {1, 2, 4, 8, 16}) {
+      if (trace) break;
       const unsigned per_ctx = std::max(1, 16 / T);
       std::vector<std::unique_ptr<rpt::DeviceContext>> ctxs;
       std::vector<std::unique_ptr<rpt::UseBF>> ops;
@@ -182,7 +189,10 @@ int host_path(int dev) {
 int main(int argc, char** argv) {
   const int dev = 0;
   // --host-path: only the host -> device path section above (int64 / int32 / dictionary keys)
-  if (argc > 1 && std::strcmp(argv[1], "--host-path") == 0) return host_path(dev);
+  if (argc > 1 && std::strcmp(argv[1], "--host-path") == 0) return host_path(dev, false);
+  // --host-path-trace: int64 / int32 FLAT through the pipeline only (8 worker threads, 4 Mi-row stages), the
+  // calls 20 ms apart: the run to take under rocprofv3 --memory-copy-trace (copy-engine busy time per call)
+  if (argc > 1 && std::strcmp(argv[1], "--host-path-trace") == 0) return host_path(dev, true);
   // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
   // synchronize waits for the device (per-vector call latency experiment)
   if (argc > 1 && std::strcmp(argv[1], "--spin") == 0) {
