@@ -46,6 +46,16 @@ __global__ __launch_bounds__(1024) void group_scan_kernel(const uint32_t* __rest
 }
 
 // ---- P3: expand result bits into an ascending selection vector ----------------------------------
+// Entries of each wave's staging buffer. 8 * RPT_COMPACT_BALLOT_MIN (3072, 6 KiB per wave) rather than a whole
+// step's 4096 rows: 24 KiB of LDS per workgroup lets 6 workgroups share a CU instead of 4 (the kernel waits on
+// its stores and LDS, so more waves hide more): C5 compaction 0.153-0.154 -> 0.130 ms at p = 0.1, 0.468 ->
+// 0.426-0.430 ms at p = 0.5 (profiles/r05/ab_compact_stage.txt)
+#ifndef RPT_COMPACT_STAGE
+#define RPT_COMPACT_STAGE (RPT_SEL_BALLOT_EXPAND ? 8 * RPT_COMPACT_BALLOT_MIN : 8 * 512)
+#endif
+constexpr uint32_t kCompactStage = RPT_COMPACT_STAGE;
+static_assert(kCompactStage == 8 * kSegRows || (RPT_SEL_BALLOT_EXPAND && kCompactStage >= 8 * RPT_COMPACT_BALLOT_MIN),
+              "the LDS staging must hold every sparse step's survivors");
 __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* __restrict__ bits,
                                                                const uint32_t* __restrict__ seg_counts, uint64_t n_segs,
                                                                const uint32_t* __restrict__ group_offs,
@@ -53,7 +63,9 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
                                                                uint32_t* __restrict__ out_sel) {
   __shared__ uint32_t s_off[kGroupSegs];
   __shared__ uint32_t s_wave[kWavesPerBlock];
-  __shared__ uint16_t s_stage[kWavesPerBlock][8 * kSegRows];  // one 4096-row step per wave (row offsets)
+  // one 4096-row step's survivors per wave (row offsets); a step only stages when it has fewer than
+  // 8 * RPT_COMPACT_BALLOT_MIN survivors (denser steps expand word by word), so that many entries suffice
+  __shared__ uint16_t s_stage[kWavesPerBlock][kCompactStage];
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kGroupSegs;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t sidx = g0 + threadIdx.x;
