@@ -337,9 +337,6 @@ __global__ __launch_bounds__(kListsThreads) void bucket_lists_kernel(L1Lists L, 
 // B6: level-1 unpermute. Per level-1 tile: gather the pass bits of its bucket runs out of the level-2
 // result bits (bits2, level-2 array order) into LDS in the tile's bucket-sorted order, 64-bit pieces
 // per item (run, piece), then map every row through its position (pos1) -> result bits + counts.
-#ifndef RPT_BU_LATE_POS
-#define RPT_BU_LATE_POS 0  // A/B: load the row positions after the gather phase (value = unroll of that loop)
-#endif
 #ifndef RPT_BUCKET_UNPERMUTE_THREADS
 #define RPT_BUCKET_UNPERMUTE_THREADS 256
 #endif
@@ -363,14 +360,12 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
   const uint64_t n_segs = (n + kSegRows - 1) / kSegRows;
   constexpr uint32_t kSegsPerWave = (kL1TileRows / kSegRows) / kWaves;
   const uint64_t seg0 = tile * (kL1TileRows / kSegRows) + wave * kSegsPerWave;
-#if !RPT_BU_LATE_POS
   u32x4 pv[kSegsPerWave];  // row positions, in flight while the bits are staged
 #pragma unroll
   for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
     pv[sg] = u32x4{0, 0, 0, 0};
     if (seg0 + sg < n_segs) pv[sg] = *reinterpret_cast<const u32x4*>(pos1 + (seg0 + sg) * kSegRows + lane * 8);
   }
-#endif
   for (uint32_t i = threadIdx.x; i < kL1TileRows / 32; i += kBucketUnpermuteThreads) s_bits[i] = 0;
   // per bucket: run length, start in the tile's sorted order, start in bits2, 64-bit pieces (scans by
   // the whole workgroup, kMaxBuckets / 256 buckets per thread)
@@ -438,17 +433,6 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
   }
   __syncthreads();
   uint8_t* out_bytes = reinterpret_cast<uint8_t*>(out_bits);
-#if RPT_BU_LATE_POS
-  // the row positions loaded only now (fewer registers through the gather phase, more waves per SIMD)
-#pragma unroll RPT_BU_LATE_POS
-  for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
-    const uint64_t seg = seg0 + sg;
-    if (seg >= n_segs) break;
-    const u32x4 pvs = *reinterpret_cast<const u32x4*>(pos1 + seg * kSegRows + lane * 8);
-    uint32_t byte = 0;
-#pragma unroll
-    for (int c = 0; c < 4; c++) byte |= pass_bits2(s_bits, pvs[c]) << (2 * c);
-#else
 #pragma unroll
   for (uint32_t sg = 0; sg < kSegsPerWave; sg++) {
     const uint64_t seg = seg0 + sg;
@@ -456,7 +440,6 @@ __global__ __launch_bounds__(kBucketUnpermuteThreads) void bucket_unpermute_kern
     uint32_t byte = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) byte |= pass_bits2(s_bits, pv[sg][c]) << (2 * c);
-#endif
     if (err) byte = 0xFFu;
     const uint64_t row0 = seg * kSegRows + lane * 8;
     if (row0 + 8 > n) byte = row0 >= n ? 0u : byte & ((1u << (n - row0)) - 1u);

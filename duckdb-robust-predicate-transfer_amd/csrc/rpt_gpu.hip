@@ -257,6 +257,13 @@ int refuse_capture_write(rpt_bf* bf, hipStream_t s, const char* what) {
                 "call rpt_bf_settle()) before capturing", what);
   return RPT_OK;
 }
+#define RPT_REFUSE_IN_FLIGHT(order, what)                                                                     \
+  do {                                                                                                        \
+    if ((order).in_flight)                                                                                    \
+      return fail(RPT_ERR_INVALID_ARGUMENT,                                                                   \
+                  "%s inside stream capture while an earlier write to the filter is in flight: synchronize " \
+                  "it (or call rpt_bf_settle()) before capturing", what);                                      \
+  } while (0)
 #define RPT_REFUSE_CAPTURE_WRITE(bf, s, what)                  \
   do {                                                         \
     const int st_cap_ = refuse_capture_write(bf, s, what);     \
@@ -272,8 +279,13 @@ struct WriteOrder {
   hipStream_t s;
   std::unique_lock<std::mutex> lk;
   bool captured;
+  // captured, but a write another thread enqueued since refuse_capture_write looked is still in flight:
+  // the caller refuses (RPT_REFUSE_IN_FLIGHT) before enqueueing anything
+  bool in_flight = false;
   WriteOrder(rpt_bf* b, hipStream_t st) : bf(b), s(st), lk(b->order_mu), captured(stream_capturing(st)) {
-    if (bf->order_pending && !captured) (void)hipStreamWaitEvent(s, bf->order_ev, 0);
+    if (!bf->order_pending) return;
+    if (!captured) (void)hipStreamWaitEvent(s, bf->order_ev, 0);
+    else in_flight = hipEventQuery(bf->order_ev) != hipSuccess;
   }
   // pristine_after: every word is zero once this operation completes
   void done(bool pristine_after) {
@@ -1099,6 +1111,7 @@ int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream) {
   if (stream_capturing(as_stream(stream)))  // the deferred clear is a host-side flag a replay cannot redo
     return fail(RPT_ERR_INVALID_ARGUMENT, "rpt_bf_clear inside stream capture: clear outside the capture");
   WriteOrder order(bf, as_stream(stream));
+  RPT_REFUSE_IN_FLIGHT(order, "write");
   // the words are zeroed by the next operation on them (rpt_bf::clear_pending): a slice insert that
   // stores every slice whole needs no separate pass over the filter (8 GiB C5 filter: 1.35 ms)
   bf->clear_pending.store(true);
@@ -1159,6 +1172,7 @@ int rpt_bf_insert(rpt_bf* bf, const rpt_key_column* col, uint64_t n, rpt_stream_
   const unsigned grid = persistent_grid(bf->device, n_segs);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, nullptr};
   WriteOrder order(bf, as_stream(stream));
+  RPT_REFUSE_IN_FLIGHT(order, "write");
   const hipError_t ez = zero_pending_locked(bf, as_stream(stream));
   if (ez != hipSuccess) return fail(RPT_ERR_HIP, "hipMemsetAsync failed: %s", hipGetErrorString(ez));
   RPT_DISPATCH_KD(launch_insert_t, col->key_type, dense_ok(col, nullptr), grid, as_stream(stream), bf, a, n, n_segs);
@@ -1278,6 +1292,7 @@ int rpt_bf_insert_ws(rpt_bf* bf, const rpt_key_column* col, uint64_t n, void* wo
       std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, static_cast<uint64_t>(cus) / grid_slices)));
   // only the slice merge writes the words: it alone is ordered after the filter's previous writes
   WriteOrder order(bf, s);
+  RPT_REFUSE_IN_FLIGHT(order, "write");
   // one workgroup per slice: every slice stored whole (a deferred clear), plain stores of the non-zero
   // pieces (a pristine filter) or a per-slice choice of read-modify-write vs atomic ORs; several
   // workgroups per slice must merge with atomics (after the deferred clear's memset, if any)
@@ -1620,6 +1635,7 @@ int rpt_bf_merge_or(rpt_bf* dst, const rpt_bf* src, rpt_stream_t stream) {
   RPT_REFUSE_CAPTURE_WRITE(dst, as_stream(stream), "merge");
   if (src != dst) RPT_SETTLE(src, as_stream(stream));
   WriteOrder order(dst, as_stream(stream));
+  RPT_REFUSE_IN_FLIGHT(order, "write");
   const hipError_t ez = zero_pending_locked(dst, as_stream(stream));
   if (ez != hipSuccess) return fail(RPT_ERR_HIP, "hipMemsetAsync failed: %s", hipGetErrorString(ez));
   int st = rpt_words_or(dst->words, src->words, 1ULL << dst->log_num_blocks, stream);
@@ -1933,6 +1949,7 @@ int rpt_bf_allreduce_or_ws(rpt_bf* bf, void* nccl_comm, void* workspace, size_t 
     return fail(RPT_ERR_INVALID_ARGUMENT, "rpt_bf_allreduce_or inside stream capture");
   MergeHelper* h = nullptr;
   WriteOrder order(bf, s);
+  RPT_REFUSE_IN_FLIGHT(order, "write");
   if (zero_pending_locked(bf, s) != hipSuccess) {
     order.done(false);
     return fail(RPT_ERR_HIP, "hipMemsetAsync failed");
@@ -2304,6 +2321,7 @@ int rpt_bf_copy_words_from(rpt_bf* bf, const uint64_t* src_dev, uint64_t n_words
   RPT_ON_DEVICE(bf->device);
   RPT_REFUSE_CAPTURE_WRITE(bf, as_stream(stream), "copy into the filter");
   WriteOrder order(bf, as_stream(stream));
+  RPT_REFUSE_IN_FLIGHT(order, "write");
   const hipError_t e = hipMemcpyAsync(bf->words, src_dev, n_words * 8, hipMemcpyDeviceToDevice, as_stream(stream));
   if (e == hipSuccess) bf->clear_pending.store(false);  // every word is overwritten
   order.done(false);

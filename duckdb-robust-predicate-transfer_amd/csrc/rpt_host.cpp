@@ -295,7 +295,7 @@ Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, siz
     return nulls;
   };
   bool any_null = false;
-  if (total < (1u << 20) || n_chunks < 16 || ctx.flatten_threads <= 1) {
+  if (total < (1u << 17) || n_chunks < 16 || ctx.flatten_threads <= 1) {  // from 128 Ki rows (a ramp stage)
     any_null = flatten_range(0, n_chunks);
   } else {
     // several ranges per worker thread, so uneven chunks (dictionaries, conversions) still balance
@@ -367,7 +367,9 @@ rpt_key_column stage_key(DeviceContext& ctx, const std::vector<const DataChunk*>
 constexpr uint64_t kSingleCopyRows = RPT_SMALL_PROBE_ROWS;
 
 // Whole-chunk stages of about `target` rows for the pipelined batch paths (a short tail joins the
-// previous stage). Every chunk's key column must have the same key type.
+// previous stage). Every chunk's key column must have the same key type. (Stages ramping up from target / 8 at
+// the start of a batch and down at its end, to shorten the pipeline's fill and drain, were measured in r05 and
+// lost: more stages cost more in per-stage fixed costs than the shorter fill and drain saved)
 struct StageRange {
   size_t c_lo, c_hi;
   uint64_t rows;
@@ -472,7 +474,7 @@ void split_sel(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, 
       p = e;
     }
   };
-  if (cnt < (1u << 16) || n_chunks < 64 || ctx.flatten_threads <= 1) {
+  if (cnt < (1u << 13) || n_chunks < 64 || ctx.flatten_threads <= 1) {
     range(0, n_chunks);
     return;
   }

@@ -106,7 +106,7 @@ class DeviceContext {
   // rows (whole chunks): flattening stage i+1 on the host overlaps the copy of stage i, the probe of
   // stage i-1 and the copy back of stage i-2's selection vector.
   uint64_t pipeline_rows = 1ULL << 22;
-  // Host threads (the calling one included) that flatten a batch or stage of >= 1 Mi rows into pinned
+  // Host threads (the calling one included) that flatten a batch or stage of >= 128 Ki rows into pinned
   // memory and split a stage's selection vector into per-chunk ones. DuckDB's operator threads each own a
   // DeviceContext, so with many of them 1-2 per context is enough.
   unsigned flatten_threads = 8;
