@@ -269,16 +269,17 @@ struct Flattened {
   bool any_null;
 };
 
-// Column `col` of chunks[0 .. n_chunks) (total rows) into pinned slots `slot` (keys) and `slot + 1`
-// (validity words).
+// Column `col` of chunks[0 .. n_chunks) (total rows) into pinned slots `slot` (keys) and `valid_slot` (validity
+// words; default slot + 1).
 Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, size_t n_chunks, uint64_t col,
-                         uint64_t total, int slot) {
+                         uint64_t total, int slot, int valid_slot = -1) {
+  if (valid_slot < 0) valid_slot = slot + 1;
   if (n_chunks == 0) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "no chunks");
   const Vector& v0 = chunks[0]->data.at(col);
   const size_t es = key_size(device_type(v0.key_type));
   const uint64_t nwords = (total + 63) / 64;
   auto* hkeys = static_cast<uint8_t*>(ctx.host(slot, std::max<size_t>(total * es, 16)));
-  auto* hvalid = static_cast<uint64_t*>(ctx.host(slot + 1, std::max<size_t>(nwords * 8, 8)));
+  auto* hvalid = static_cast<uint64_t*>(ctx.host(valid_slot, std::max<size_t>(nwords * 8, 8)));
   std::memset(hvalid, 0xFF, nwords * 8);  // all valid; flatten_column clears the NULL rows
   std::vector<uint64_t> row0(n_chunks + 1, 0);
   for (size_t i = 0; i < n_chunks; i++) {
@@ -579,7 +580,7 @@ DeviceContext::DeviceContext(int device) : device_(device) {
 DeviceContext::~DeviceContext() {
   pool_.reset();
   DeviceScope ds(device_);
-  for (void* st : {stream_, copy_stream_, h2d_stream_})
+  for (void* st : {stream_, copy_stream_, h2d_stream_, aux_streams_[0], aux_streams_[1]})
     if (st) (void)hipStreamSynchronize(static_cast<hipStream_t>(st));
   for (auto& b : host_)
     if (b.p) (void)hipHostFree(b.p);
@@ -587,7 +588,7 @@ DeviceContext::~DeviceContext() {
     if (b.p) (void)hipFree(b.p);
   for (void* e : events_)
     if (e) (void)hipEventDestroy(static_cast<hipEvent_t>(e));
-  for (void* st : {h2d_stream_, copy_stream_, stream_})
+  for (void* st : {aux_streams_[1], aux_streams_[0], h2d_stream_, copy_stream_, stream_})
     if (st) (void)hipStreamDestroy(static_cast<hipStream_t>(st));
 }
 
@@ -596,6 +597,8 @@ void DeviceContext::synchronize() {
   check_hip(hipStreamSynchronize(static_cast<hipStream_t>(stream_)), "hipStreamSynchronize");
   if (copy_stream_) check_hip(hipStreamSynchronize(static_cast<hipStream_t>(copy_stream_)), "hipStreamSynchronize");
   if (h2d_stream_) check_hip(hipStreamSynchronize(static_cast<hipStream_t>(h2d_stream_)), "hipStreamSynchronize");
+  for (void* st : aux_streams_)
+    if (st) check_hip(hipStreamSynchronize(static_cast<hipStream_t>(st)), "hipStreamSynchronize");
 }
 
 void* DeviceContext::copy_stream() {
@@ -616,6 +619,17 @@ void* DeviceContext::h2d_stream() {
     h2d_stream_ = s;
   }
   return h2d_stream_;
+}
+
+void* DeviceContext::aux_stream(int i) {
+  if (i < 0 || i >= kAuxStreams) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "aux stream index out of range");
+  if (!aux_streams_[i]) {
+    DeviceScope ds(device_);
+    hipStream_t s;
+    check_hip(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+    aux_streams_[i] = s;
+  }
+  return aux_streams_[i];
 }
 
 void* DeviceContext::event(int i) {
@@ -1221,7 +1235,7 @@ uint64_t UseBF::Execute(DeviceContext& ctx, const DataChunk& input, SelectionVec
     std::vector<const rpt_bf*> bfs;
     std::vector<rpt_key_column> kcs;
     for (size_t k = 0; k < act.size(); k++) {
-      const int slot = DeviceContext::kSlots / 2 + 2 * static_cast<int>(k);
+      const int slot = 16 + 2 * static_cast<int>(k);
       const Flattened f = flatten_pinned(ctx, &in, 1, cols_[act[k]], n, slot);
       rpt_key_column kc;
       kc.key_type = static_cast<int32_t>(f.key_type);
@@ -1306,22 +1320,23 @@ uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChu
   }
   if (total >= (1ULL << 32)) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "batch exceeds uint32 row ids");
   {
-    // one applicable filter over a large batch: LookupSelBatch's pipeline (flatten, copy, probe and copy
-    // back of successive stages overlap) gives the same per-chunk sels
-    const PTBloomFilter* only = nullptr;
-    size_t only_i = 0, applicable = 0;
+    // large batches take the pipeline (flatten, copy, probe and copy back of successive stages overlap): one
+    // applicable filter through LookupSelBatch's, several through the chained one; same per-chunk sels
+    std::vector<size_t> act;
     for (size_t i = 0; i < filters_.size(); i++) {
       const auto& bf = filters_[i];
       if (!bf || !bf->finalized_) continue;  // cpp:139-142
       if (bf->IsEmpty()) return 0;           // cpp:145-155
-      applicable++;
-      only = bf.get();
-      only_i = i;
+      act.push_back(i);
     }
-    if (applicable == 1 && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
-      only->LookupSelBatch(ctx, inputs, outs, {cols_[only_i]});
+    if (!act.empty() && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
       uint64_t count = 0;
-      for (const SelectionVector& o : outs) count += o.size();
+      if (act.size() == 1) {
+        filters_[act[0]]->LookupSelBatch(ctx, inputs, outs, {cols_[act[0]]});
+        for (const SelectionVector& o : outs) count += o.size();
+      } else {
+        count = ExecuteChainPipelined(ctx, inputs, outs, act);
+      }
       rows_out_ += count;
       return count;
     }
@@ -1356,6 +1371,347 @@ uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChu
   check_hip(hipMemcpyAsync(h_rows, d_rows, count * 4, hipMemcpyDeviceToHost, s), "copy sel");
   ctx.synchronize();
   split_sel(ctx, inputs, 0, inputs.size(), h_rows, count, outs);
+  return count;
+}
+
+// A FLAT / DICTIONARY vector of I32 / I64 keys (element T) at rows rows[0 .. n) - base (ascending): the keys as
+// they are, NULLs cleared in `valid_words` from bit `out0` on, 64 rows per step.
+template <typename T, bool kDict>
+bool gather_typed(const Vector& v, const uint32_t* rows, uint64_t base, uint64_t n, uint8_t* keys, uint64_t* valid_words,
+                  uint64_t out0) {
+  const T* src = static_cast<const T*>(v.data);
+  T* dst = reinterpret_cast<T*>(keys);
+  bool any_null = false;
+  for (uint64_t j0 = 0; j0 < n; j0 += 64) {
+    const uint32_t m = static_cast<uint32_t>(std::min<uint64_t>(64, n - j0));
+    uint64_t nulls = 0;
+    if (kDict) {
+      uint32_t kmax = 0;
+      for (uint32_t e = 0; e < m; e++) kmax = std::max(kmax, v.sel[rows[j0 + e] - base]);
+      if (kmax >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
+    }
+    for (uint32_t e = 0; e < m; e++) {
+      if (!kDict && j0 + e + 32 < n) __builtin_prefetch(src + (rows[j0 + e + 32] - base));  // the survivors' lines
+      const uint64_t r = rows[j0 + e] - base;
+      const uint64_t idx = kDict ? v.sel[r] : r;
+      std::memcpy(dst + j0 + e, src + idx, sizeof(T));
+      if (v.validity) nulls |= static_cast<uint64_t>(!valid_bit(v.validity, idx)) << e;
+    }
+    any_null |= nulls != 0;
+    clear_bits(valid_words, out0 + j0, nulls, m);
+  }
+  return any_null;
+}
+
+// Rows rows[0 .. n) - base (ascending, chunk-local) of one vector gathered as device values into `keys`, their NULLs
+// cleared in `valid_words` (preset to all-valid) from bit `out0` on; the same conversions and NULL rules as
+// flatten_column. Returns true if any gathered row was NULL.
+bool gather_column(const Vector& v, const uint32_t* rows, uint64_t base, uint64_t n, uint8_t* keys,
+                   uint64_t* valid_words, uint64_t out0) {
+  const KeyType dt = device_type(v.key_type);
+  if (dt == v.key_type && (v.type == VectorType::FLAT || v.type == VectorType::DICTIONARY)) {
+    const bool dict = v.type == VectorType::DICTIONARY;
+    if (dt == KeyType::I32)
+      return dict ? gather_typed<uint32_t, true>(v, rows, base, n, keys, valid_words, out0)
+                  : gather_typed<uint32_t, false>(v, rows, base, n, keys, valid_words, out0);
+    return dict ? gather_typed<uint64_t, true>(v, rows, base, n, keys, valid_words, out0)
+                : gather_typed<uint64_t, false>(v, rows, base, n, keys, valid_words, out0);
+  }
+  const size_t ss = source_size(v.key_type), ds = key_size(dt);
+  const uint8_t* src = static_cast<const uint8_t*>(v.data);
+  bool any_null = false;
+  for (uint64_t j0 = 0; j0 < n; j0 += 64) {
+    const uint32_t m = static_cast<uint32_t>(std::min<uint64_t>(64, n - j0));
+    uint64_t nulls = 0;
+    for (uint32_t e = 0; e < m; e++) {
+      const uint64_t r = rows[j0 + e] - base;
+      uint8_t seq[8];
+      const uint8_t* p;
+      switch (v.type) {
+        case VectorType::SEQUENCE: {  // never NULL
+          const uint64_t x = static_cast<uint64_t>(v.seq_start) + static_cast<uint64_t>(v.seq_increment) * r;
+          std::memcpy(seq, &x, 8);
+          p = seq;
+          break;
+        }
+        case VectorType::CONSTANT:
+          p = src;
+          nulls |= static_cast<uint64_t>(!valid_bit(v.validity, 0)) << e;
+          break;
+        case VectorType::DICTIONARY: {
+          const uint32_t idx = v.sel[r];
+          if (idx >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
+          p = src + static_cast<uint64_t>(idx) * ss;
+          nulls |= static_cast<uint64_t>(!valid_bit(v.validity, idx)) << e;
+          break;
+        }
+        default:
+          p = src + r * ss;
+          nulls |= static_cast<uint64_t>(!valid_bit(v.validity, r)) << e;
+          break;
+      }
+      const uint64_t d = dt == v.key_type ? 0 : device_value(v.key_type, p);
+      std::memcpy(keys + (j0 + e) * ds, dt == v.key_type ? static_cast<const void*>(p) : &d, ds);
+    }
+    any_null |= nulls != 0;
+    clear_bits(valid_words, out0 + j0, nulls, m);
+  }
+  return any_null;
+}
+
+// The survivors of a filter as stage rows: out[x] = rows[idx[x]] for x in [0, n) (idx ascending), on the
+// context's workers for large n.
+void map_survivors(DeviceContext& ctx, const uint32_t* rows, const uint32_t* idx, uint64_t n, uint32_t* out) {
+  auto range = [&](uint64_t lo, uint64_t hi) {
+    for (uint64_t x = lo; x < hi; x++) out[x] = rows[idx[x]];
+  };
+  if (n < (1u << 16) || ctx.flatten_threads <= 1) {
+    range(0, n);
+  } else {
+    const size_t n_tasks = std::min<size_t>(n >> 14, 4 * static_cast<size_t>(ctx.flatten_threads));
+    ctx.parallel_for(n_tasks, [&](size_t t) { range(n * t / n_tasks, n * (t + 1) / n_tasks); });
+  }
+}
+
+// Column `col` of a stage's chunks (chunk i starting at stage row row0[i]) at stage rows into pinned slots `slot`
+// (keys) / `valid_slot` (validity), on the context's workers for large n. The rows are rows[0 .. n), or, with idx,
+// rows[idx[x]] (the previous filter's survivors mapped through its sel, idx ascending), written to mapped[x].
+Flattened gather_pinned(DeviceContext& ctx, const DataChunk* const* chunks, const std::vector<uint64_t>& row0,
+                        uint64_t col, const uint32_t* rows_in, const uint32_t* idx, uint32_t* mapped, uint64_t n,
+                        int slot, int valid_slot) {
+  const uint32_t* rows = idx ? mapped : rows_in;
+  const KeyType kt = chunks[0]->data.at(col).key_type;
+  const size_t es = key_size(device_type(kt));
+  const uint64_t nwords = (n + 63) / 64;
+  auto* hkeys = static_cast<uint8_t*>(ctx.host(slot, std::max<size_t>(n * es, 16)));
+  auto* hvalid = static_cast<uint64_t*>(ctx.host(valid_slot, std::max<size_t>(nwords * 8, 8)));
+  std::memset(hvalid, 0xFF, nwords * 8);
+  const size_t n_chunks = row0.size() - 1;
+  auto range = [&](uint64_t lo, uint64_t hi) {  // rows[lo .. hi): a run per chunk
+    if (idx)
+      for (uint64_t x = lo; x < hi; x++) mapped[x] = rows_in[idx[x]];
+    bool nulls = false;
+    size_t c = static_cast<size_t>(std::upper_bound(row0.begin(), row0.end(), static_cast<uint64_t>(rows[lo])) -
+                                   row0.begin()) - 1;
+    for (uint64_t j = lo; j < hi;) {
+      while (c < n_chunks && rows[j] >= row0[c + 1]) c++;
+      if (c >= n_chunks) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "survivor row beyond the stage");
+      // the chunk's end among the survivors: galloping from j (a chunk holds a few hundred of them)
+      const uint32_t bound = static_cast<uint32_t>(row0[c + 1]);
+      const uint32_t* p = rows + j;
+      const uint32_t* const end = rows + hi;
+      size_t step = 16;
+      while (static_cast<size_t>(end - p) > step && p[step] < bound) {
+        p += step;
+        step *= 2;
+      }
+      const uint32_t* e = std::lower_bound(p, static_cast<size_t>(end - p) > step ? p + step + 1 : end, bound);
+      const uint64_t m = static_cast<uint64_t>(e - rows) - j;
+      nulls |= gather_column(chunks[c]->data.at(col), rows + j, row0[c], m, hkeys + j * es, hvalid, j);
+      j += m;
+    }
+    return nulls;
+  };
+  bool any_null = false;
+  if (n < (1u << 16) || ctx.flatten_threads <= 1) {
+    if (n) any_null = range(0, n);
+  } else {
+    const size_t n_tasks = std::min<size_t>(n >> 14, 4 * static_cast<size_t>(ctx.flatten_threads));
+    std::vector<char> nulls(n_tasks, 0);
+    ctx.parallel_for(n_tasks, [&](size_t t) { nulls[t] = range(n * t / n_tasks, n * (t + 1) / n_tasks) ? 1 : 0; });
+    for (char c : nulls) any_null |= c != 0;
+  }
+  return Flattened{device_type(kt), hkeys, hvalid, any_null};
+}
+
+// The reference's filter loop (physical_use_bf.cpp:127-179) over a pipelined batch, with the survivors compacted
+// on the host between filters. Stage i's first applicable filter's column is flattened into pinned buffer
+// b = i % 3, copied on the host-to-device stream and probed over every row on compute stream b (the context's
+// stream or one of its aux streams). Each further filter gets only the previous one's survivors: their selection
+// vector comes back, the host gathers the next column's keys at those rows and sends them, and the probe's sel
+// (indices into the gathered keys) maps back through the survivor list. Against the filter-by-filter path this
+// sends a later column's keys for the survivors only (p x the bytes) instead of for every row. Three stages are in
+// flight: the chains of stages i-1 and i-2 advance on their own streams, between the host's other work, while the
+// copy engine moves stage i. A stage whose survivors run out stops its chain (cpp:166-173); the final survivor list
+// is split per chunk.
+uint64_t UseBF::ExecuteChainPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& inputs,
+                                      std::vector<SelectionVector>& outs, const std::vector<size_t>& act) const {
+  const Clock::time_point t_begin = Clock::now();
+  DeviceContext::PipelineStats& ps = ctx.stats;
+  const size_t k = act.size();
+  std::vector<StageRange> st = pipeline_stages(inputs, cols_[act[0]], ctx.pipeline_rows);
+  for (size_t f = 1; f < k; f++) (void)pipeline_stages(inputs, cols_[act[f]], ~0ULL);  // every column one key type
+  uint64_t max_rows = 0;
+  size_t ws_bytes = 16;
+  for (const StageRange& r : st) {
+    max_rows = std::max(max_rows, r.rows);
+    for (size_t f = 0; f < k; f++) ws_bytes = std::max(ws_bytes, rpt_bf_probe_workspace_bytes(filters_[act[f]]->native(), r.rows));
+  }
+  // kNB stages in flight, stage i in buffer b = i % kNB: private slots 32.. (DeviceContext::kSlots) per buffer:
+  // host / device 32 + b (the first column's keys), 35 + b (its validity), 38 + b / 41 + b (a later column's
+  // gathered keys / validity); host 44 + b / 47 + b (the survivor lists, ping-pong), 50 + b (a later probe's sel),
+  // 53 + b (the count); device 50 + b (the probe's sel), 53 (the counts), 54 + b (the probe workspaces)
+  constexpr int kNB = 3;
+  static_assert(kNB == DeviceContext::kAuxStreams + 1 && 57 <= DeviceContext::kSlots, "chain pipeline slots");
+  const size_t words = (max_rows + 63) / 64 * 8;
+  const size_t es0 = key_size(device_type(inputs[0]->data.at(cols_[act[0]]).key_type));
+  void* d_keys[2][kNB];
+  void* d_valid[2][kNB];
+  uint32_t* d_sel[kNB];
+  uint32_t* h_sel[kNB];
+  uint32_t* surv[kNB][2];
+  uint64_t* h_cnt[kNB];
+  void* ws[kNB];
+  hipStream_t cs[kNB];
+  auto* d_cnt = static_cast<uint64_t*>(ctx.dev(53, kNB * 8));
+  for (int b = 0; b < kNB; b++) {
+    for (int g = 0; g < 2; g++) {
+      (void)ctx.host(32 + 6 * g + b, std::max<size_t>(max_rows * (g ? 8 : es0), 16));
+      (void)ctx.host(35 + 6 * g + b, std::max<size_t>(words, 8));
+      d_keys[g][b] = ctx.dev(32 + 6 * g + b, std::max<size_t>(max_rows * (g ? 8 : es0), 16));
+      d_valid[g][b] = ctx.dev(35 + 6 * g + b, std::max<size_t>(words, 8));
+    }
+    for (int v = 0; v < 2; v++) surv[b][v] = static_cast<uint32_t*>(ctx.host(44 + 3 * v + b, std::max<size_t>(max_rows * 4, 4)));
+    h_sel[b] = static_cast<uint32_t*>(ctx.host(50 + b, std::max<size_t>(max_rows * 4, 4)));
+    h_cnt[b] = static_cast<uint64_t*>(ctx.host(53 + b, 8));
+    d_sel[b] = static_cast<uint32_t*>(ctx.dev(50 + b, std::max<size_t>(max_rows * 4, 4)));
+    ws[b] = ctx.dev(54 + b, ws_bytes);
+    cs[b] = static_cast<hipStream_t>(b == 0 ? ctx.stream() : ctx.aux_stream(b - 1));
+  }
+  auto h = static_cast<hipStream_t>(ctx.h2d_stream());
+  auto copied = [&](int b) { return static_cast<hipEvent_t>(ctx.event(b)); };
+  auto arrived = [&](int b) { return static_cast<hipEvent_t>(ctx.event(kNB + b)); };  // a count (+ sel) on the host
+  auto probed = [&](int b) { return static_cast<hipEvent_t>(ctx.event(2 * kNB + b)); };  // the first probe read its keys
+  rpt_key_column kc0[kNB];
+  uint64_t count = 0;
+  // A stage's chain as a state machine, so its round trips overlap the next stage's flatten: phase 0 = the first
+  // probe's count and the head of its sel are on their way (the head sized from the previous stage's survivors,
+  // so one round trip usually brings the whole sel), 1 = the rest of that sel, 2 = filter `lev`'s count and sel
+  // (indices into its input list surv[b][sv]); advance() takes every step whose event has fired (all of them,
+  // waiting, when `block`).
+  struct Chain {
+    size_t j = 0;
+    int phase = 0;
+    size_t lev = 0;
+    int sv = 0;
+    uint64_t n = 0, head = 0;
+    bool live = false;
+    std::vector<uint64_t> row0;
+  } ch[kNB];
+  double head_frac = 0.25;  // the first probe's pass fraction expected (the last stage's)
+  // probe filter `lev` over n keys, its count and `sel_rows` sel entries back to the host (a later filter's count
+  // is <= n, so one copy of n brings its whole sel)
+  auto probe = [&](int b, size_t lev, const rpt_key_column* kc, uint64_t n, uint32_t* sel_to, uint64_t sel_rows) {
+    check(rpt_bf_probe(filters_[act[lev]]->native(), kc, nullptr, n, d_sel[b], d_cnt + b, ws[b], ws_bytes, cs[b]));
+    check_hip(hipMemcpyAsync(h_cnt[b], d_cnt + b, 8, hipMemcpyDeviceToHost, cs[b]), "copy count");
+    if (sel_rows) check_hip(hipMemcpyAsync(sel_to, d_sel[b], sel_rows * 4, hipMemcpyDeviceToHost, cs[b]), "copy sel");
+    check_hip(hipEventRecord(arrived(b), cs[b]), "hipEventRecord");
+  };
+  // gather filter c.lev's column at the survivors (mapped through the previous filter's sel when `idx`) and probe it
+  auto next_filter = [&](Chain& c, int b, const uint32_t* idx) {
+    Clock::time_point t0 = Clock::now();
+    const Flattened g = gather_pinned(ctx, inputs.data() + st[c.j].c_lo, c.row0, cols_[act[c.lev]], surv[b][c.sv], idx,
+                                      surv[b][c.sv ^ 1], c.n, 38 + b, 41 + b);
+    if (idx) c.sv ^= 1;
+    ps.flatten_s += secs_since(t0);
+    t0 = Clock::now();
+    const rpt_key_column kc = copy_flattened(ctx, g, c.n, d_keys[1][b], d_valid[1][b], cs[b]);
+    probe(b, c.lev, &kc, c.n, h_sel[b], c.n);
+    ps.enqueue_s += secs_since(t0);
+    c.phase = 2;
+  };
+  auto advance = [&](Chain& c, bool block) {
+    const int b = static_cast<int>(c.j % kNB);
+    while (c.live) {
+      if (block) {
+        const Clock::time_point t0 = Clock::now();
+        check_hip(hipEventSynchronize(arrived(b)), "hipEventSynchronize");
+        ps.wait_count_s += secs_since(t0);
+      } else {
+        const hipError_t q = hipEventQuery(arrived(b));
+        if (q == hipErrorNotReady) return;
+        check_hip(q, "hipEventQuery");
+      }
+      bool done = false;
+      if (c.phase == 0) {
+        c.n = *h_cnt[b];
+        head_frac = static_cast<double>(c.n) / static_cast<double>(st[c.j].rows);
+        if (c.n == 0) {
+          done = true;
+        } else if (c.n > c.head) {  // the rest of the first filter's sel (stage row ids)
+          check_hip(hipMemcpyAsync(surv[b][0] + c.head, d_sel[b] + c.head, (c.n - c.head) * 4, hipMemcpyDeviceToHost, cs[b]),
+                    "copy sel");
+          check_hip(hipEventRecord(arrived(b), cs[b]), "hipEventRecord");
+          c.phase = 1;
+        } else {
+          c.lev = 1;
+          next_filter(c, b, nullptr);
+        }
+      } else if (c.phase == 1) {
+        c.lev = 1;
+        next_filter(c, b, nullptr);
+      } else {
+        const uint64_t m = *h_cnt[b];
+        c.n = m;
+        if (m == 0) {
+          done = true;
+        } else if (++c.lev == k) {  // the last filter's survivors as stage rows
+          const Clock::time_point t0 = Clock::now();
+          map_survivors(ctx, surv[b][c.sv], h_sel[b], m, surv[b][c.sv ^ 1]);
+          c.sv ^= 1;
+          ps.split_s += secs_since(t0);
+          done = true;
+        } else {
+          next_filter(c, b, h_sel[b]);
+        }
+      }
+      if (done) {
+        const Clock::time_point t0 = Clock::now();
+        split_sel(ctx, inputs, st[c.j].c_lo, st[c.j].c_hi, surv[b][c.sv], c.n, outs);
+        count += c.n;
+        ps.split_s += secs_since(t0);
+        c.live = false;
+      }
+    }
+  };
+  try {
+    for (size_t i = 0; i < st.size(); i++) {
+      const int b = static_cast<int>(i % kNB);
+      advance(ch[b], true);  // stage i - kNB: its buffers are about to be reused
+      for (int o = 1; o < kNB; o++) advance(ch[(b + o) % kNB], false);
+      Clock::time_point t0 = Clock::now();
+      if (i >= kNB) check_hip(hipEventSynchronize(copied(b)), "hipEventSynchronize");
+      ps.wait_copy_s += secs_since(t0);
+      t0 = Clock::now();
+      const Flattened f = flatten_pinned(ctx, inputs.data() + st[i].c_lo, st[i].c_hi - st[i].c_lo, cols_[act[0]],
+                                         st[i].rows, 32 + b, 35 + b);
+      ps.flatten_s += secs_since(t0);
+      t0 = Clock::now();
+      if (i >= kNB) check_hip(hipStreamWaitEvent(h, probed(b), 0), "hipStreamWaitEvent");  // stage i - kNB read them
+      kc0[b] = copy_flattened(ctx, f, st[i].rows, d_keys[0][b], d_valid[0][b], h);
+      check_hip(hipEventRecord(copied(b), h), "hipEventRecord");
+      check_hip(hipStreamWaitEvent(cs[b], copied(b), 0), "hipStreamWaitEvent");
+      Chain& c = ch[b];
+      c.head = std::min<uint64_t>(st[i].rows, static_cast<uint64_t>(head_frac * 1.25 * static_cast<double>(st[i].rows)) + 4096);
+      probe(b, 0, &kc0[b], st[i].rows, surv[b][0], c.head);
+      check_hip(hipEventRecord(probed(b), cs[b]), "hipEventRecord");
+      ps.enqueue_s += secs_since(t0);
+      c.j = i;
+      c.phase = 0;
+      c.sv = 0;
+      c.live = true;
+      c.row0.assign(st[i].c_hi - st[i].c_lo + 1, 0);
+      for (size_t x = st[i].c_lo; x < st[i].c_hi; x++) c.row0[x - st[i].c_lo + 1] = c.row0[x - st[i].c_lo] + inputs[x]->count;
+      for (int o = 1; o < kNB; o++) advance(ch[(b + o) % kNB], false);
+    }
+    for (size_t i = st.size() > kNB ? st.size() - kNB : 0; i < st.size(); i++) advance(ch[i % kNB], true);
+  } catch (...) {
+    for (hipStream_t x : {h, cs[0], cs[1]}) (void)hipStreamSynchronize(x);  // nothing may still use the staging buffers
+    throw;
+  }
+  ps.stages += st.size();
+  ps.rows += total_rows(inputs);
+  ps.total_s += secs_since(t_begin);
   return count;
 }
 

@@ -82,10 +82,11 @@ class DeviceContext {
   DeviceContext& operator=(const DeviceContext&) = delete;
   int device() const { return device_; }
   void* stream() const { return stream_; }
-  void synchronize();  // both streams
+  void synchronize();  // every stream
 
-  // internal: grow-on-demand buffers (host slots 16..31: UseBF's chained key columns)
-  static constexpr int kSlots = 32;
+  // internal: grow-on-demand buffers (host slots 16..31: UseBF::Execute's chained key columns; 32..63: the
+  // pipelined filter chain of UseBF::ExecuteBatch)
+  static constexpr int kSlots = 64;
   void* host(int slot, size_t bytes);
   void* dev(int slot, size_t bytes);
   // the device address of host slot `slot`'s pinned buffer (kernels read / write it in place), cached
@@ -95,6 +96,10 @@ class DeviceContext {
   // (created on first use), and their events
   void* copy_stream();
   void* h2d_stream();
+  // internal: further compute streams (created on first use): the pipelined filter chain runs successive
+  // stages' chains on stream() and these, so one stage's next filter never queues behind a later stage's copy
+  static constexpr int kAuxStreams = 2;
+  void* aux_stream(int i);
   static constexpr int kEvents = 16;
   void* event(int i);
   // internal: run fn(0) .. fn(n - 1) on this context's worker threads (flatten_threads of them, the caller
@@ -130,6 +135,7 @@ class DeviceContext {
   void* stream_ = nullptr;
   void* copy_stream_ = nullptr;
   void* h2d_stream_ = nullptr;
+  void* aux_streams_[kAuxStreams] = {};
   struct Buf {
     void* p = nullptr;
     size_t cap = 0;
@@ -329,6 +335,11 @@ class UseBF {
   uint64_t rows_out() const { return rows_out_; }
 
  private:
+  // ExecuteBatch for 2+ applicable filters over a large batch: the first filter's column goes through
+  // LookupSelBatch's pipeline; each further filter gets only the previous one's survivors (their keys gathered on
+  // the host), and successive stages overlap.
+  uint64_t ExecuteChainPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& inputs,
+                                 std::vector<SelectionVector>& outs, const std::vector<size_t>& act) const;
   std::vector<std::shared_ptr<PTBloomFilter>> filters_;
   std::vector<uint64_t> cols_;
   bool passthrough_;

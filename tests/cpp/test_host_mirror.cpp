@@ -456,13 +456,147 @@ static void pipelined_workers(int dev) {
     size_t bad = 0;
     for (size_t k = 0; k < pptrs.size(); k++) bad += outs[k] != want[k];
     EXPECT(got == total && outs.size() == pptrs.size() && bad == 0, "ExecuteBatch through the pipeline (column %d): %zu chunks differ", c, bad);
+    // a dictionary index out of range in a chunk of the third stage: the worker thread that flattens it throws,
+    // the pipeline drains its streams and LookupSelBatch raises INVALID_ARGUMENT; the context stays usable
+    if (c == 0) {
+      std::vector<uint32_t> bad_sel(2048, 0);
+      bad_sel[777] = 1u << 30;
+      std::vector<int64_t> dict(16, 5);
+      rpt::DataChunk broken;
+      broken.count = 2048;
+      broken.data.resize(1);
+      broken.data[0].type = rpt::VectorType::DICTIONARY;
+      broken.data[0].key_type = rpt::KeyType::I64;
+      broken.data[0].data = dict.data();
+      broken.data[0].sel = bad_sel.data();
+      broken.data[0].dict_size = dict.size();
+      std::vector<const rpt::DataChunk*> with_bad = pptrs;
+      with_bad[with_bad.size() / 2 + 10] = &broken;
+      bool threw = false;
+      try {
+        f->LookupSelBatch(ctx, with_bad, sels, {0});
+      } catch (const rpt::GpuError& e) {
+        threw = e.status() == RPT_ERR_INVALID_ARGUMENT;
+      }
+      EXPECT(threw, "an out-of-range dictionary index inside a worker's flatten raises INVALID_ARGUMENT");
+      f->LookupSelBatch(ctx, pptrs, sels, {0});
+      size_t bad2 = 0;
+      for (size_t k = 0; k < pptrs.size(); k++) bad2 += sels[k] != want[k];
+      EXPECT(bad2 == 0, "the context after a failed pipelined batch: %zu chunks differ", bad2);
+    }
   }
+}
+
+// UseBF::ExecuteBatch with 2..5 applicable filters over a pipelined batch (ExecuteChainPipelined): per stage the
+// first filter probes every row, each further one the previous one's survivors, their keys gathered on the host
+// from FLAT / DICTIONARY / CONSTANT chunks with NULLs; BIGINT and INTEGER columns mixed, a non-finalized filter
+// skipped, a stage whose column-1 keys all miss f1 (its chain stops there); every chunk against the oracle's
+// intersection of per-row hits, pipelined and filter by filter (pipeline_rows beyond the batch).
+static void pipelined_chain(int dev) {
+  const size_t nb = 96 * 2048, np = (3u << 20) + 1234;
+  Table bt = make_table(nb, 21, 53, 0), pt = make_table(np, 22, 41, 2048);  // chunk 3's column 0: CONSTANT
+  ChunkStore bst, pst;
+  make_chunks(bt, nb, bst, false);
+  std::vector<const rpt::DataChunk*> pptrs;
+  rpt::DeviceContext ctx(dev);
+  ctx.pipeline_rows = 1u << 20;
+  ctx.flatten_threads = 4;
+  // f0: column 0 of build chunks [0, 48); f1: column 1 of [0, 80); f2: column 0 of [48, 96)
+  struct Spec { int col; size_t c_lo, c_hi; };
+  const Spec specs[3] = {{0, 0, 48}, {1, 0, 80}, {0, 48, 96}};
+  std::vector<std::shared_ptr<rpt::PTBloomFilter>> fs;
+  std::vector<std::vector<uint64_t>> words;
+  for (const Spec& sp : specs) {
+    std::vector<const rpt::DataChunk*> part;
+    for (size_t k = sp.c_lo; k < sp.c_hi; k++) part.push_back(&bst.chunks[k]);
+    const size_t lo = sp.c_lo * 2048, n = (sp.c_hi - sp.c_lo) * 2048;
+    auto f = std::make_shared<rpt::PTBloomFilter>();
+    f->Initialize(dev, static_cast<uint32_t>(n));
+    f->InsertBatch(ctx, part, {static_cast<uint64_t>(sp.col)});
+    f->finalized_ = true;
+    const int lnb = f->LogNumBlocks();
+    std::vector<uint64_t> w(1ULL << lnb, 0);
+    const std::vector<uint64_t> vb = pack(sp.col == 0 ? bt.v0 : bt.v1, lo, n);
+    if (sp.col == 0) rpt_oracle_insert_i64(w.data(), lnb, bt.c0.data() + lo, nullptr, vb.data(), n);
+    else rpt_oracle_insert_i32(w.data(), lnb, bt.c1.data() + lo, nullptr, vb.data(), n);
+    EXPECT(f->ExportWords() == w, "chain filter on column %d differs from the oracle", sp.col);
+    words.push_back(std::move(w));
+    fs.push_back(f);
+  }
+  // stage 1 (rows [1 Mi, 2 Mi)): every column-1 key one value f1 rejects (NULLs would not do: their hash is a
+  // value like any other, and the build's NULLs put it in f1)
+  int32_t miss = -1000000;
+  for (;; miss--) {
+    uint64_t one = 1;
+    uint32_t sel1;
+    if (rpt_oracle_probe_i32(words[1].data(), fs[1]->LogNumBlocks(), &miss, nullptr, &one, 1, &sel1) == 0) break;
+  }
+  for (size_t i = 1u << 20; i < (2u << 20); i++) {
+    pt.c1[i] = miss;
+    pt.v1[i] = true;
+  }
+  make_chunks(pt, np, pst, true);
+  for (const auto& ch : pst.chunks) pptrs.push_back(&ch);
+  EXPECT(pptrs[3]->data[0].type == rpt::VectorType::CONSTANT, "chunk 3 column 0 CONSTANT");
+  std::vector<std::vector<uint8_t>> hit;  // per filter: does probe row i pass it
+  for (size_t i = 0; i < 3; i++) {
+    const Spec& sp = specs[i];
+    const std::vector<uint64_t> vp = pack(sp.col == 0 ? pt.v0 : pt.v1, 0, np);
+    std::vector<uint32_t> sel(np);
+    const int lnb = fs[i]->LogNumBlocks();
+    const uint64_t ne = sp.col == 0 ? rpt_oracle_probe_i64(words[i].data(), lnb, pt.c0.data(), nullptr, vp.data(), np, sel.data())
+                                    : rpt_oracle_probe_i32(words[i].data(), lnb, pt.c1.data(), nullptr, vp.data(), np, sel.data());
+    std::vector<uint8_t> h(np, 0);
+    for (uint64_t j = 0; j < ne; j++) h[sel[j]] = 1;
+    hit.push_back(std::move(h));
+  }
+  auto unfinished = std::make_shared<rpt::PTBloomFilter>();  // never finalized: UseBF skips it (cpp:139-142)
+  unfinished->Initialize(dev, 1000);
+  struct Case { std::vector<int> order; };
+  const Case cases[] = {{{0, 1}}, {{0, 1, 2}}, {{1, 0, 2, 1}}, {{2, -1, 0}}, {{0, 1, 2, 0, 1}}};
+  for (const Case& cs : cases) {
+    std::vector<std::shared_ptr<rpt::PTBloomFilter>> use;
+    std::vector<uint64_t> cols;
+    for (int i : cs.order) {
+      use.push_back(i < 0 ? unfinished : fs[i]);
+      cols.push_back(i < 0 ? 0 : static_cast<uint64_t>(specs[i].col));
+    }
+    std::vector<rpt::SelectionVector> want(pptrs.size());
+    size_t total = 0, stage1 = 0;
+    for (size_t k = 0; k < pptrs.size(); k++) {
+      for (size_t r = 0; r < pptrs[k]->count; r++) {
+        bool pass = true;
+        for (int i : cs.order) pass = pass && (i < 0 || hit[i][2048 * k + r]);
+        if (pass) want[k].push_back(static_cast<uint32_t>(r));
+      }
+      total += want[k].size();
+      if (2048 * k >= (1u << 20) && 2048 * k < (2u << 20)) stage1 += want[k].size();
+    }
+    const bool with_f1 = std::find(cs.order.begin(), cs.order.end(), 1) != cs.order.end();
+    EXPECT(total > 10000 && (stage1 == 0) == with_f1, "chain of %zu: %zu survivors, %zu in stage 1", cs.order.size(), total, stage1);
+    rpt::UseBF ub(use, cols);
+    std::vector<rpt::SelectionVector> outs(3, rpt::SelectionVector(5, 1));  // stale contents must not leak
+    for (int rep = 0; rep < 3; rep++) {  // pipelined twice (outs reused), then filter by filter
+      ctx.stats = {};
+      ctx.pipeline_rows = rep < 2 ? (1u << 20) : ~0ULL / 4;
+      const uint64_t got = ub.ExecuteBatch(ctx, pptrs, outs);
+      size_t bad = 0;
+      for (size_t k = 0; k < pptrs.size(); k++) bad += outs[k] != want[k];
+      EXPECT(got == total && outs.size() == pptrs.size() && bad == 0, "chain of %zu filters (call %d): %zu chunks differ, %llu vs %zu rows",
+             cs.order.size(), rep, bad, (unsigned long long)got, total);
+      if (rep < 2)
+        EXPECT(ctx.stats.stages >= 3 && ctx.stats.rows == np, "chain of %zu: %llu pipeline stages", cs.order.size(),
+               (unsigned long long)ctx.stats.stages);
+    }
+  }
+  ctx.pipeline_rows = 1u << 20;
 }
 
 int main() {
   try {
     const int dev = 0;
     pipelined_workers(dev);
+    pipelined_chain(dev);
     // ---------------- build -------------------------------------------------------------------
     const size_t nb = 50001;
     Table bt = make_table(nb, 1, 97, 2048);

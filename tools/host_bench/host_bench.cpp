@@ -184,6 +184,97 @@ int host_path(int dev, bool trace) {
   }
   return 0;
 }
+// USE_BF's filter chain over large batches (UseBF::ExecuteBatch with 1..3 applicable filters on three key
+// columns: BIGINT 10% hits, INTEGER 50% hits, BIGINT 50% hits): the pipelined chain (4 Mi-row stages, 8 worker
+// threads) beside the filter-by-filter path (the whole batch per filter, pipeline_rows beyond the batch), both
+// checked equal.
+int host_chain(int dev) {
+  const size_t n_build = 10000000, n_probe = 1ULL << 25;
+  std::mt19937_64 rng(11);
+  std::vector<int64_t> b0(n_build), b2(n_build), p0(n_probe), p2(n_probe);
+  std::vector<int32_t> b1(n_build), p1(n_probe);
+  for (size_t i = 0; i < n_build; i++) {
+    b0[i] = static_cast<int64_t>(rng() >> 1);
+    b1[i] = static_cast<int32_t>(rng());
+    b2[i] = static_cast<int64_t>(rng() >> 1);
+  }
+  for (size_t i = 0; i < n_probe; i++) {
+    p0[i] = (rng() % 10 == 0) ? b0[rng() % n_build] : static_cast<int64_t>(rng() >> 1);
+    p1[i] = (rng() % 2 == 0) ? b1[rng() % n_build] : static_cast<int32_t>(rng());
+    p2[i] = (rng() % 2 == 0) ? b2[rng() % n_build] : static_cast<int64_t>(rng() >> 1);
+  }
+  auto chunks = [](size_t n, const int64_t* c0, const int32_t* c1, const int64_t* c2) {
+    std::vector<rpt::DataChunk> cs;
+    for (size_t lo = 0; lo < n; lo += 2048) {
+      rpt::DataChunk c;
+      c.count = std::min<size_t>(2048, n - lo);
+      c.data.resize(3);
+      c.data[0].key_type = rpt::KeyType::I64;
+      c.data[0].data = c0 + lo;
+      c.data[1].key_type = rpt::KeyType::I32;
+      c.data[1].data = c1 + lo;
+      c.data[2].key_type = rpt::KeyType::I64;
+      c.data[2].data = c2 + lo;
+      cs.push_back(c);
+    }
+    return cs;
+  };
+  auto bch = chunks(n_build, b0.data(), b1.data(), b2.data());
+  auto pch = chunks(n_probe, p0.data(), p1.data(), p2.data());
+  std::vector<const rpt::DataChunk*> ball, pall;
+  for (auto& c : bch) ball.push_back(&c);
+  for (auto& c : pch) pall.push_back(&c);
+  rpt::DeviceContext ctx(dev);
+  ctx.flatten_threads = 8;
+  std::vector<std::shared_ptr<rpt::PTBloomFilter>> fs;
+  for (uint64_t col = 0; col < 3; col++) {
+    auto f = std::make_shared<rpt::PTBloomFilter>();
+    f->Initialize(dev, static_cast<uint32_t>(n_build));
+    f->InsertBatch(ctx, ball, {col});
+    f->finalized_ = true;
+    fs.push_back(f);
+  }
+  const double rows = static_cast<double>(n_probe);
+  for (size_t k = 1; k <= 3; k++) {
+    rpt::UseBF ub(std::vector<std::shared_ptr<rpt::PTBloomFilter>>(fs.begin(), fs.begin() + k),
+                  k == 1 ? std::vector<uint64_t>{0} : k == 2 ? std::vector<uint64_t>{0, 1} : std::vector<uint64_t>{0, 1, 2});
+    std::vector<rpt::SelectionVector> ref, outs;
+    const int calls = 4;
+    uint64_t surv = 0;
+    double sec_ref = 0;
+    ctx.pipeline_rows = ~0ULL / 4;  // filter by filter: the whole batch per filter
+    ub.ExecuteBatch(ctx, pall, ref);  // warm-up
+    for (int c = 0; c < calls; c++) {
+      const auto t0 = clk::now();
+      surv = ub.ExecuteBatch(ctx, pall, ref);
+      sec_ref += since(t0);
+    }
+    for (uint64_t stage : {uint64_t(1) << 21, uint64_t(1) << 22}) {
+      ctx.pipeline_rows = stage;
+      ub.ExecuteBatch(ctx, pall, outs);  // warm-up
+      ctx.stats = {};
+      double sec = 0;
+      for (int c = 0; c < calls; c++) {
+        const auto t0 = clk::now();
+        ub.ExecuteBatch(ctx, pall, outs);
+        sec += since(t0);
+      }
+      size_t bad = 0;
+      for (size_t i = 0; i < pall.size(); i++) bad += outs[i] != ref[i];
+      if (bad) {
+        fprintf(stderr, "chain of %zu: pipelined and filter-by-filter sels differ in %zu chunks\n", k, bad);
+        return 1;
+      }
+      printf("{\"op\": \"host_path.ExecuteBatch.chain\", \"filters\": %zu, \"chunks_per_call\": %zu, \"worker_threads\": 8, "
+             "\"pass_fraction\": %.4f, \"filter_by_filter_rows_per_s\": %.4g, \"pipelined_rows_per_s\": %.4g, \"pipeline_rows\": %llu, ",
+             k, pall.size(), surv / rows, calls * rows / sec_ref, calls * rows / sec, static_cast<unsigned long long>(stage));
+      print_stats("phases_per_call", ctx.stats, calls);
+      printf("}\n");
+      fflush(stdout);
+    }
+  }
+  return 0;
+}
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -193,6 +284,8 @@ int main(int argc, char** argv) {
   // --host-path-trace: int64 / int32 FLAT through the pipeline only (8 worker threads, 4 Mi-row stages), the
   // calls 20 ms apart: the run to take under rocprofv3 --memory-copy-trace (copy-engine busy time per call)
   if (argc > 1 && std::strcmp(argv[1], "--host-path-trace") == 0) return host_path(dev, true);
+  // --chain: UseBF::ExecuteBatch with 1..3 filters, pipelined chain vs filter by filter
+  if (argc > 1 && std::strcmp(argv[1], "--chain") == 0) return host_chain(dev);
   // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
   // synchronize waits for the device (per-vector call latency experiment)
   if (argc > 1 && std::strcmp(argv[1], "--spin") == 0) {
