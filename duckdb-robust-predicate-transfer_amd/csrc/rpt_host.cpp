@@ -11,6 +11,7 @@
 #include <cstring>
 #include <exception>
 #include <limits>
+#include <map>
 #include <thread>
 #include <utility>
 
@@ -570,6 +571,90 @@ void DeviceContext::parallel_for(size_t n, const std::function<void(size_t)>& fn
 }
 
 // ---- DeviceContext -----------------------------------------------------------------------------
+// ---- pinned host buffer cache ----------------------------------------------------------------------
+// Pinned buffers of contexts that grow a slot or die, kept for the next context that asks for that size
+// (powers of two from 64 KiB): hipHostMalloc pins every page, which per-query operator states would otherwise
+// pay on every query. Never freed at exit (the HIP runtime may be
+// gone by then); ReleasePinnedCache frees what is cached.
+namespace {
+struct PinnedCache {
+  std::mutex mu;
+  std::map<size_t, std::vector<void*>> free;  // by capacity
+  size_t cached = 0, limit = size_t(4) << 30;
+};
+PinnedCache& pinned_cache() {
+  static PinnedCache* c = new PinnedCache;  // intentionally leaked (see above)
+  return *c;
+}
+size_t pinned_class(size_t bytes) {
+  size_t c = size_t(1) << 16;
+  while (c < bytes) c <<= 1;
+  return c;
+}
+void* pinned_take(size_t cap) {
+  PinnedCache& c = pinned_cache();
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.free.find(cap);
+    if (it != c.free.end() && !it->second.empty()) {
+      void* p = it->second.back();
+      it->second.pop_back();
+      c.cached -= cap;
+      return p;
+    }
+  }
+  void* p = nullptr;
+  check_hip(hipHostMalloc(&p, cap, hipHostMallocDefault), "hipHostMalloc");
+  return p;
+}
+void pinned_give(void* p, size_t cap) {  // p is no longer used by any stream
+  PinnedCache& c = pinned_cache();
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    if (c.cached + cap <= c.limit) {
+      c.free[cap].push_back(p);
+      c.cached += cap;
+      return;
+    }
+  }
+  (void)hipHostFree(p);
+}
+}  // namespace
+
+void SetPinnedCacheLimit(size_t bytes) {
+  PinnedCache& c = pinned_cache();
+  std::vector<std::pair<void*, size_t>> drop;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    c.limit = bytes;
+    for (auto it = c.free.rbegin(); it != c.free.rend() && c.cached > c.limit; ++it)
+      while (!it->second.empty() && c.cached > c.limit) {
+        drop.emplace_back(it->second.back(), it->first);
+        it->second.pop_back();
+        c.cached -= it->first;
+      }
+  }
+  for (auto& d : drop) (void)hipHostFree(d.first);
+}
+
+size_t PinnedCacheBytes() {
+  PinnedCache& c = pinned_cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  return c.cached;
+}
+
+void ReleasePinnedCache() {
+  PinnedCache& c = pinned_cache();
+  std::map<size_t, std::vector<void*>> all;
+  {
+    std::lock_guard<std::mutex> lk(c.mu);
+    all.swap(c.free);
+    c.cached = 0;
+  }
+  for (auto& kv : all)
+    for (void* p : kv.second) (void)hipHostFree(p);
+}
+
 DeviceContext::DeviceContext(int device) : device_(device) {
   DeviceScope ds(device_);
   hipStream_t s;
@@ -583,7 +668,7 @@ DeviceContext::~DeviceContext() {
   for (void* st : {stream_, copy_stream_, h2d_stream_, aux_streams_[0], aux_streams_[1]})
     if (st) (void)hipStreamSynchronize(static_cast<hipStream_t>(st));
   for (auto& b : host_)
-    if (b.p) (void)hipHostFree(b.p);
+    if (b.p) pinned_give(b.p, b.cap);  // the streams are drained above
   for (auto& b : dev_)
     if (b.p) (void)hipFree(b.p);
   for (void* e : events_)
@@ -648,11 +733,11 @@ void* DeviceContext::host(int slot, size_t bytes) {
   Buf& b = host_[slot];
   if (b.cap < bytes) {
     synchronize();
-    if (b.p) check_hip(hipHostFree(b.p), "hipHostFree");
+    if (b.p) pinned_give(b.p, b.cap);
     b.p = nullptr;
     b.dp = nullptr;
-    const size_t cap = std::max(bytes, 2 * b.cap);
-    check_hip(hipHostMalloc(&b.p, cap, hipHostMallocDefault), "hipHostMalloc");
+    const size_t cap = pinned_class(std::max(bytes, 2 * b.cap));
+    b.p = pinned_take(cap);
     b.cap = cap;
   }
   return b.p;
@@ -707,10 +792,10 @@ void DeviceKeyColumn::release() {
 }
 
 const DeviceKeyColumn::Segment& DeviceKeyColumn::Append(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
-                                                        uint64_t col) {
+                                                        uint64_t col, int slot) {
   const uint64_t total = total_rows(chunks);
   if (total == 0) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "empty batch");
-  const Flattened f = flatten_pinned(ctx, chunks.data(), chunks.size(), col, total, 0);
+  const Flattened f = flatten_pinned(ctx, chunks.data(), chunks.size(), col, total, slot);
   DeviceScope ds(device_);
   void* dkeys = nullptr;
   void* dvalid = nullptr;
@@ -830,13 +915,13 @@ void PTBloomFilter::InsertPipelined(DeviceContext& ctx, const std::vector<const 
   ps.total_s += secs_since(t_begin);
 }
 
-void PTBloomFilter::InsertDevice(DeviceContext& ctx, const rpt_key_column& col, uint64_t n) {
+void PTBloomFilter::InsertDevice(DeviceContext& ctx, const rpt_key_column& col, uint64_t n, bool synchronize) {
   if (n == 0) return;
   // large batches take the partitioned / bucketed insert (same filter bits)
   const size_t ws_bytes = rpt_bf_insert_workspace_bytes(bf_, n);
   if (ws_bytes) check(rpt_bf_insert_ws(bf_, &col, n, ctx.dev(6, ws_bytes), ws_bytes, ctx.stream()));
   else check(rpt_bf_insert(bf_, &col, n, ctx.stream()));
-  ctx.synchronize();  // the staging buffers are reused by the next call
+  if (synchronize) ctx.synchronize();  // the staging buffers are reused by the next call
 }
 
 uint64_t PTBloomFilter::LookupSel(DeviceContext& ctx, const DataChunk& chunk, SelectionVector& sel,
@@ -1087,7 +1172,21 @@ CreateBF::CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint6
 
 void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
   // materialize the chunk (every column, flattened, owned): the source re-emits it
-  // (physical_create_bf.cpp:211-218)
+  // (physical_create_bf.cpp:211-218). The copies are bump-allocated from 1 MiB blocks the state owns (one
+  // allocation per ~64 chunks, nothing zero-filled first).
+  const Clock::time_point t0 = Clock::now();
+  auto alloc = [&local](size_t words) {
+    if (words > local.arena_left) {
+      const size_t blk = std::max<size_t>(words, size_t(1) << 17);
+      local.storage.emplace_back(new uint64_t[blk]);
+      local.arena = local.storage.back().get();
+      local.arena_left = blk;
+    }
+    uint64_t* p = local.arena;
+    local.arena += words;
+    local.arena_left -= words;
+    return p;
+  };
   DataChunk m;
   m.count = chunk.count;
   m.data.resize(chunk.data.size());
@@ -1095,21 +1194,21 @@ void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
     const Vector& v = chunk.data[c];
     if (v.data == nullptr && v.type != VectorType::SEQUENCE) continue;  // a column this mirror does not carry
     const size_t es = source_size(v.key_type);
-    std::vector<uint64_t> keys((chunk.count * es + 7) / 8 + 1, 0);
-    std::vector<uint64_t> valid((chunk.count + 63) / 64 + 1, ~0ULL);  // all valid; NULL rows cleared
-    const bool any_null =
-        flatten_column(v, chunk.count, reinterpret_cast<uint8_t*>(keys.data()), valid.data(), 0, /*to_device=*/false);
+    const size_t nvalid = (chunk.count + 63) / 64 + 1;
+    uint64_t* keys = alloc((chunk.count * es + 7) / 8 + 1);
+    uint64_t* valid = alloc(nvalid);
+    std::fill(valid, valid + nvalid, ~0ULL);  // all valid; NULL rows cleared
+    const bool any_null = flatten_column(v, chunk.count, reinterpret_cast<uint8_t*>(keys), valid, 0, /*to_device=*/false);
     Vector f;
     f.type = VectorType::FLAT;
     f.key_type = v.key_type;
-    f.data = keys.data();  // heap buffers keep their address when the vectors are moved
-    f.validity = any_null ? valid.data() : nullptr;
-    local.storage.push_back(std::move(keys));
-    local.storage.push_back(std::move(valid));
+    f.data = keys;
+    f.validity = any_null ? valid : nullptr;
     m.data[c] = f;
   }
   local.chunks.push_back(std::move(m));
   local.pending_rows += chunk.count;
+  local.materialize_s += secs_since(t0);
   // insert into one filter per build column (physical_create_bf.cpp:221-227), a batch at a time
   if (local.pending_rows >= sink_flush_rows_) Flush(local);
 }
@@ -1119,20 +1218,32 @@ void CreateBF::Flush(LocalState& local) const {
     local.pending_from = local.chunks.size();
     return;
   }
+  const Clock::time_point t0 = Clock::now();
   std::vector<const DataChunk*> batch;
   for (size_t k = local.pending_from; k < local.chunks.size(); k++)
     if (local.chunks[k].count) batch.push_back(&local.chunks[k]);
+  // async: flush k stages through pinned buffer k % 2 (host slots 8 + 4 i + 2 b / + 1 for build column i) and
+  // leaves its copies and inserts running; flush k + 2 first waits for them (event b)
+  const bool async = local.async_flush && cols_.size() <= kAsyncFlushColumns;
+  const int b = async ? static_cast<int>(local.flushes & 1) : 0;
+  auto done = static_cast<hipEvent_t>(local.ctx.event(b));
+  if (async && local.flushes >= 2) check_hip(hipEventSynchronize(done), "hipEventSynchronize");
   for (size_t i = 0; i < cols_.size(); i++) {
-    const DeviceKeyColumn::Segment& g = local.keys[i].Append(local.ctx, batch, cols_[i]);
+    const int slot = async ? 8 + 4 * static_cast<int>(i) + 2 * b : 0;
+    const DeviceKeyColumn::Segment& g = local.keys[i].Append(local.ctx, batch, cols_[i], slot);
     filters_[i]->NoteKeyType(batch[0]->data.at(cols_[i]).key_type);
-    filters_[i]->InsertDevice(local.ctx, g.col, g.rows);
+    filters_[i]->InsertDevice(local.ctx, g.col, g.rows, /*synchronize=*/!async);
   }
+  if (async) check_hip(hipEventRecord(done, static_cast<hipStream_t>(local.ctx.stream())), "hipEventRecord");
+  local.flushes++;
   local.pending_from = local.chunks.size();
   local.pending_rows = 0;
+  local.flush_s += secs_since(t0);
 }
 
 void CreateBF::Combine(LocalState& local) {
   Flush(local);
+  local.ctx.synchronize();  // the state's inserts are done (Finalize and the source read what they wrote)
   std::lock_guard<std::mutex> lk(lock_);
   for (auto& c : local.chunks) {
     total_rows_ += c.count;
@@ -1142,6 +1253,8 @@ void CreateBF::Combine(LocalState& local) {
   for (size_t i = 0; i < cols_.size(); i++) all_keys_[i].Splice(std::move(local.keys[i]));
   local.chunks.clear();
   local.storage.clear();
+  local.arena = nullptr;
+  local.arena_left = 0;
   local.pending_from = 0;
 }
 

@@ -73,6 +73,13 @@ struct DataChunk {
 
 using SelectionVector = std::vector<uint32_t>;  // sel_t
 
+// Pinned host staging of DeviceContexts that grow a slot or are destroyed goes to a process-wide cache (up to
+// `bytes`, default 4 GiB) and is handed to the next context that needs that size, so per-query operator states
+// do not pin fresh pages (hipHostMalloc) every query. ReleasePinnedCache frees what is cached now.
+void SetPinnedCacheLimit(size_t bytes);
+size_t PinnedCacheBytes();
+void ReleasePinnedCache();
+
 // Device stream + pinned/device staging owned by one host thread (DuckDB thread-local state).
 class DeviceContext {
  public:
@@ -164,8 +171,10 @@ class DeviceKeyColumn {
   DeviceKeyColumn(const DeviceKeyColumn&) = delete;
   DeviceKeyColumn& operator=(const DeviceKeyColumn&) = delete;
 
-  // Flatten column `col` of `chunks` (FLAT / CONSTANT / DICTIONARY) into a new device segment.
-  const Segment& Append(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col);
+  // Flatten column `col` of `chunks` (FLAT / CONSTANT / DICTIONARY) into a new device segment, through the
+  // context's pinned slots `slot` / `slot + 1`; the copy is enqueued on the context's stream (it has not
+  // necessarily finished when Append returns: synchronize before reusing those slots).
+  const Segment& Append(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col, int slot = 0);
   // Take over `other`'s segments (CREATE_BF Combine).
   void Splice(DeviceKeyColumn&& other);
   const std::vector<Segment>& segments() const { return segs_; }
@@ -198,8 +207,10 @@ class PTBloomFilter {
   // DeviceContext::pipeline_rows); sels[i] holds chunk i's survivors (ids relative to chunk i)
   void LookupSelBatch(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks,
                       std::vector<SelectionVector>& sels, const std::vector<uint64_t>& cols) const;
-  // Insert a device-resident key column (large batches take the routed inserts; same bits).
-  void InsertDevice(DeviceContext& ctx, const rpt_key_column& col, uint64_t n);
+  // Insert a device-resident key column (large batches take the routed inserts; same bits). synchronize =
+  // false: the insert is only enqueued on the context's stream (col and the context's workspace slot 6 stay in
+  // use until the caller synchronizes).
+  void InsertDevice(DeviceContext& ctx, const rpt_key_column& col, uint64_t n, bool synchronize = true);
   // bloom_filter.cpp:34-58: reallocate for actual_rows and re-insert the materialized chunks
   void ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const std::vector<DataChunk>& data,
                              const std::vector<uint64_t>& cols);
@@ -255,12 +266,20 @@ class CreateBF {
       for (size_t i = 0; i < n_cols; i++) keys.emplace_back(device);
     }
     DeviceContext ctx;
-    std::vector<DataChunk> chunks;               // materialized chunks (views of owned storage)
-    std::vector<std::vector<uint64_t>> storage;  // owned copies backing `chunks`
-    std::vector<DeviceKeyColumn> keys;           // build columns already staged to HBM
-    size_t pending_from = 0;                     // chunks[pending_from..] not yet inserted
+    std::vector<DataChunk> chunks;                      // materialized chunks (views of owned storage)
+    std::vector<std::unique_ptr<uint64_t[]>> storage;   // owned blocks backing `chunks` (bump-allocated)
+    uint64_t* arena = nullptr;                          // the current block's free words
+    size_t arena_left = 0;
+    std::vector<DeviceKeyColumn> keys;                  // build columns already staged to HBM
+    size_t pending_from = 0;                            // chunks[pending_from..] not yet inserted
     uint64_t pending_rows = 0;
+    uint64_t flushes = 0;
+    // A flush's copy and insert overlap the next chunks' materialization (two pinned buffers per build column,
+    // up to kAsyncFlushColumns columns); false: every flush waits for its insert.
+    bool async_flush = true;
+    double materialize_s = 0, flush_s = 0;  // host time in Sink's materialization / in the flushes
   };
+  static constexpr size_t kAsyncFlushColumns = 12;
   // CreateBFGlobalSourceState (physical_create_bf.cpp:441-485): chunk ranges, one per source thread
   struct GlobalSourceState {
     std::vector<std::pair<size_t, size_t>> chunks_todo;
@@ -311,7 +330,7 @@ class CreateBF {
   std::vector<bool> resized_;
   std::mutex lock_;
   std::vector<DataChunk> all_chunks_;
-  std::vector<std::vector<uint64_t>> all_storage_;
+  std::vector<std::unique_ptr<uint64_t[]>> all_storage_;
   std::vector<DeviceKeyColumn> all_keys_;
   uint64_t total_rows_ = 0;
 };

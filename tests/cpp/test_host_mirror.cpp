@@ -590,11 +590,73 @@ static void pipelined_chain(int dev) {
     }
   }
   ctx.pipeline_rows = 1u << 20;
+  // a chunk whose column-1 dictionary indices are out of range: the gather for f1 (on a worker thread, mid
+  // chain) throws, the pipeline drains its streams and ExecuteBatch raises INVALID_ARGUMENT; the context stays
+  // usable
+  {
+    const size_t victim = pptrs.size() / 2 + 7;
+    rpt::DataChunk broken = *pptrs[victim];
+    std::vector<uint32_t> bad_sel(broken.count, 1u << 30);
+    std::vector<int32_t> dict(4, 1);
+    broken.data[1].type = rpt::VectorType::DICTIONARY;
+    broken.data[1].data = dict.data();
+    broken.data[1].sel = bad_sel.data();
+    broken.data[1].dict_size = dict.size();
+    broken.data[1].validity = nullptr;
+    std::vector<const rpt::DataChunk*> with_bad = pptrs;
+    with_bad[victim] = &broken;
+    rpt::UseBF ub({fs[0], fs[1]}, {0, 1});
+    std::vector<rpt::SelectionVector> outs;
+    bool threw = false;
+    try {
+      ub.ExecuteBatch(ctx, with_bad, outs);
+    } catch (const rpt::GpuError& e) {
+      threw = e.status() == RPT_ERR_INVALID_ARGUMENT;
+    }
+    EXPECT(threw, "an out-of-range dictionary index in a gathered column raises INVALID_ARGUMENT");
+    const uint64_t got = ub.ExecuteBatch(ctx, pptrs, outs);
+    size_t bad = 0, total = 0;
+    for (size_t k = 0; k < pptrs.size(); k++) {
+      rpt::SelectionVector w;
+      for (size_t r = 0; r < pptrs[k]->count; r++)
+        if (hit[0][2048 * k + r] && hit[1][2048 * k + r]) w.push_back(static_cast<uint32_t>(r));
+      total += w.size();
+      bad += outs[k] != w;
+    }
+    EXPECT(bad == 0 && got == total, "the context after a failed chain: %zu chunks differ", bad);
+  }
+}
+
+// The process-wide pinned staging cache: a destroyed context's buffers are cached and handed to the next
+// context of that size class (the same address), the limit bounds what is kept, ReleasePinnedCache empties it.
+static void pinned_cache(int dev) {
+  rpt::ReleasePinnedCache();
+  EXPECT(rpt::PinnedCacheBytes() == 0, "cache empty after release");
+  void* first = nullptr;
+  {
+    rpt::DeviceContext a(dev);
+    first = a.host(3, 3u << 20);  // a 4 MiB class
+  }
+  EXPECT(rpt::PinnedCacheBytes() == (4u << 20), "destroyed context's buffer cached: %zu", rpt::PinnedCacheBytes());
+  {
+    rpt::DeviceContext b(dev);
+    void* again = b.host(7, 4u << 20);
+    EXPECT(again == first && rpt::PinnedCacheBytes() == 0, "the cached buffer is reused");
+    void* bigger = b.host(7, 5u << 20);  // grows: the 4 MiB buffer goes back, an 8 MiB one is pinned
+    EXPECT(bigger != nullptr && rpt::PinnedCacheBytes() == (4u << 20), "growth returns the old buffer");
+    std::memset(bigger, 1, 5u << 20);
+  }
+  rpt::SetPinnedCacheLimit(6u << 20);  // keeps 4 MiB, not 4 + 8
+  EXPECT(rpt::PinnedCacheBytes() <= (6u << 20), "limit applied: %zu", rpt::PinnedCacheBytes());
+  rpt::SetPinnedCacheLimit(size_t(4) << 30);
+  rpt::ReleasePinnedCache();
+  EXPECT(rpt::PinnedCacheBytes() == 0, "released");
 }
 
 int main() {
   try {
     const int dev = 0;
+    pinned_cache(dev);
     pipelined_workers(dev);
     pipelined_chain(dev);
     // ---------------- build -------------------------------------------------------------------
@@ -629,6 +691,25 @@ int main() {
     EXPECT(f0->ExportWords() == w0, "filter 0 words differ from the oracle");
     EXPECT(f1->ExportWords() == w1, "filter 1 words differ from the oracle");
     EXPECT(f0->finalized_ && f1->finalized_ && !f0->IsEmpty(), "finalized / has data");
+    {  // the same build with synchronous sink flushes (LocalState::async_flush = false): the same words
+      rpt::CreateBF sync_create(dev, 1000, {0, 1}, 5000);
+      std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> ls;
+      for (int t = 0; t < 3; t++) {
+        ls.push_back(sync_create.MakeLocalState());
+        ls.back()->async_flush = false;
+      }
+      std::vector<std::thread> st;
+      for (int t = 0; t < 3; t++)
+        st.emplace_back([&, t] {
+          for (size_t k = t; k < bst.chunks.size(); k += 3) sync_create.Sink(*ls[t], bst.chunks[k]);
+          sync_create.Combine(*ls[t]);
+        });
+      for (auto& th : st) th.join();
+      sync_create.Finalize();
+      EXPECT(sync_create.GetBloomFilter(0)->ExportWords() == w0 && sync_create.GetBloomFilter(1)->ExportWords() == w1,
+             "synchronous sink flushes: words differ from the oracle");
+      EXPECT(ls[0]->flushes >= 3 && ls[0]->materialize_s > 0 && ls[0]->flush_s > 0, "sink stats");
+    }
     // min/max dynamic filter per build column (physical_create_bf.cpp:229-272), NULLs skipped
     {
       std::vector<uint64_t> va = pack(bt.v0, 0, nb), vb = pack(bt.v1, 0, nb);

@@ -275,6 +275,121 @@ int host_chain(int dev) {
   }
   return 0;
 }
+// CREATE_BF end to end on a 1e8-row build: 8 sink threads over 2048-row chunks (sink batches staged
+// to HBM), Combine, then Finalize with an under-estimated cardinality so the filter is resized and
+// rehashed -- from the HBM key segments -- versus the same rehash re-staging the materialized host
+// chunks over PCIe (each with a fresh DeviceContext, as Finalize has); every flush size with the sink's
+// flushes synchronous and asynchronous (LocalState::async_flush).
+int create_bf(int dev) {
+  std::mt19937_64 rng(43);
+  auto chunks_of = [](std::vector<int64_t>& v) {
+    std::vector<rpt::DataChunk> cs;
+    for (size_t lo = 0; lo < v.size(); lo += 2048) {
+      rpt::DataChunk c;
+      c.count = std::min<size_t>(2048, v.size() - lo);
+      rpt::Vector x;
+      x.key_type = rpt::KeyType::I64;
+      x.data = v.data() + lo;
+      c.data.push_back(x);
+      cs.push_back(c);
+    }
+    return cs;
+  };
+  {
+    const size_t n_cb = 100000000;
+    std::vector<int64_t> cb(n_cb);
+    for (auto& k : cb) k = static_cast<int64_t>(rng() >> 1);
+    auto cchunks = chunks_of(cb);
+    {  // what pinning costs: hipHostMalloc + hipHostFree of a 32 MiB staging buffer
+      const int reps = 8;
+      double ms = 0, free_ms = 0;
+      for (int r = 0; r < reps; r++) {
+        void* p = nullptr;
+        auto t0 = clk::now();
+        if (hipHostMalloc(&p, size_t(32) << 20, hipHostMallocDefault) != hipSuccess) return 3;
+        ms += since(t0) * 1e3;
+        t0 = clk::now();
+        (void)hipHostFree(p);
+        free_ms += since(t0) * 1e3;
+      }
+      double dms = 0;
+      for (int r = 0; r < reps; r++) {
+        void* p = nullptr;
+        auto t0 = clk::now();
+        if (hipMalloc(&p, size_t(32) << 20) != hipSuccess) return 3;
+        dms += since(t0) * 1e3;
+        (void)hipFree(p);
+      }
+      printf("{\"op\": \"hipHostMalloc\", \"bytes\": %zu, \"malloc_ms\": %.3f, \"free_ms\": %.3f, \"hipMalloc_ms\": %.3f}\n",
+             size_t(32) << 20, ms / reps, free_ms / reps, dms / reps);
+    }
+    for (uint64_t flush : {uint64_t(1) << 20, rpt::CreateBF::kDefaultSinkFlushRows, uint64_t(1) << 24})
+    for (bool async : {false, true})
+    for (bool warm : {false, true})
+    for (unsigned workers : {8u, 2u}) {
+      if (flush != rpt::CreateBF::kDefaultSinkFlushRows && (!warm || workers != 2)) continue;
+      if (!warm) rpt::ReleasePinnedCache();  // cold: every sink state pins its staging afresh
+      rpt::CreateBF create(dev, /*estimated_cardinality=*/1000, {0}, flush);
+      const int T = 8;
+      std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> locals;
+      for (int t = 0; t < T; t++) {
+        locals.push_back(create.MakeLocalState());
+        locals.back()->async_flush = async;
+        locals.back()->ctx.flatten_threads = workers;
+      }
+      auto t0 = clk::now();
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {  // each thread sinks its chunks, then combines (as DuckDB's pipeline does)
+          for (size_t k = t; k < cchunks.size(); k += T) create.Sink(*locals[t], cchunks[k]);
+          create.Combine(*locals[t]);
+        });
+      for (auto& x : th) x.join();
+      const double sink_s = std::chrono::duration<double>(clk::now() - t0).count();
+      t0 = clk::now();
+      create.Finalize();
+      const double fin_s = std::chrono::duration<double>(clk::now() - t0).count();
+      auto bfh = create.GetBloomFilter(0);
+      const auto words = bfh->ExportWords();
+      double hbm_s, host_s;
+      {
+        t0 = clk::now();
+        rpt::DeviceContext c2(dev);
+        bfh->ReinitializeAndRehash(c2, n_cb, create.DeviceKeys(0));
+        hbm_s = std::chrono::duration<double>(clk::now() - t0).count();
+      }
+      std::vector<rpt::DataChunk> host_chunks;
+      {
+        auto gs = create.GetGlobalSourceState(1);
+        rpt::CreateBF::LocalSourceState ls;
+        rpt::DataChunk c;
+        while (create.GetData(*gs, ls, c)) host_chunks.push_back(c);
+      }
+      {
+        t0 = clk::now();
+        rpt::DeviceContext c3(dev);
+        bfh->ReinitializeAndRehash(c3, n_cb, host_chunks, {0});
+        host_s = std::chrono::duration<double>(clk::now() - t0).count();
+      }
+      double mat_s = 0, fl_s = 0;
+      for (auto& l : locals) {
+        mat_s += l->materialize_s;
+        fl_s += l->flush_s;
+      }
+      printf("{\"op\": \"CreateBF\", \"rows\": %zu, \"sink_threads\": %d, \"sink_flush_rows\": %llu, \"async_flush\": %s, \"pinned_cache\": \"%s\", \"workers_per_state\": %u, "
+             "\"segments\": %zu, \"sink_combine_rows_per_s\": %.4g, \"materialize_ms_per_thread\": %.2f, "
+             "\"flush_ms_per_thread\": %.2f, \"finalize_ms\": %.2f, "
+             "\"rehash_hbm_ms\": %.2f, \"rehash_from_host_ms\": %.2f, \"resized\": %s, \"same_words\": %s}\n",
+             n_cb, T, static_cast<unsigned long long>(flush), async ? "true" : "false", warm ? "warm" : "cold", workers,
+             create.DeviceKeys(0).segments().size(),
+             n_cb / sink_s, mat_s / T * 1e3, fl_s / T * 1e3, fin_s * 1e3, hbm_s * 1e3, host_s * 1e3,
+             create.Resized(0) ? "true" : "false", bfh->ExportWords() == words ? "true" : "false");
+      fflush(stdout);
+    }
+  }
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -286,6 +401,8 @@ int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "--host-path-trace") == 0) return host_path(dev, true);
   // --chain: UseBF::ExecuteBatch with 1..3 filters, pipelined chain vs filter by filter
   if (argc > 1 && std::strcmp(argv[1], "--chain") == 0) return host_chain(dev);
+  // --create: only the CREATE_BF section
+  if (argc > 1 && std::strcmp(argv[1], "--create") == 0) return create_bf(dev);
   // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
   // synchronize waits for the device (per-vector call latency experiment)
   if (argc > 1 && std::strcmp(argv[1], "--spin") == 0) {
@@ -446,61 +563,5 @@ int main(int argc, char** argv) {
              per_call, calls, s / calls * 1e6, static_cast<double>(calls) * per_call * 2048 / s);
     }
   }
-  // CREATE_BF end to end on a 1e8-row build: 8 sink threads over 2048-row chunks (sink batches staged
-  // to HBM), Combine, then Finalize with an under-estimated cardinality so the filter is resized and
-  // rehashed -- from the HBM key segments -- versus the same rehash re-staging the materialized host
-  // chunks over PCIe (each with a fresh DeviceContext, as Finalize has).
-  {
-    const size_t n_cb = 100000000;
-    std::vector<int64_t> cb(n_cb);
-    for (auto& k : cb) k = static_cast<int64_t>(rng() >> 1);
-    auto cchunks = chunks_of(cb);
-    for (uint64_t flush : {uint64_t(1) << 20, rpt::CreateBF::kDefaultSinkFlushRows, uint64_t(1) << 24}) {
-      rpt::CreateBF create(dev, /*estimated_cardinality=*/1000, {0}, flush);
-      const int T = 8;
-      std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> locals;
-      for (int t = 0; t < T; t++) locals.push_back(create.MakeLocalState());
-      auto t0 = clk::now();
-      std::vector<std::thread> th;
-      for (int t = 0; t < T; t++)
-        th.emplace_back([&, t] {  // each thread sinks its chunks, then combines (as DuckDB's pipeline does)
-          for (size_t k = t; k < cchunks.size(); k += T) create.Sink(*locals[t], cchunks[k]);
-          create.Combine(*locals[t]);
-        });
-      for (auto& x : th) x.join();
-      const double sink_s = std::chrono::duration<double>(clk::now() - t0).count();
-      t0 = clk::now();
-      create.Finalize();
-      const double fin_s = std::chrono::duration<double>(clk::now() - t0).count();
-      auto bfh = create.GetBloomFilter(0);
-      const auto words = bfh->ExportWords();
-      double hbm_s, host_s;
-      {
-        t0 = clk::now();
-        rpt::DeviceContext c2(dev);
-        bfh->ReinitializeAndRehash(c2, n_cb, create.DeviceKeys(0));
-        hbm_s = std::chrono::duration<double>(clk::now() - t0).count();
-      }
-      std::vector<rpt::DataChunk> host_chunks;
-      {
-        auto gs = create.GetGlobalSourceState(1);
-        rpt::CreateBF::LocalSourceState ls;
-        rpt::DataChunk c;
-        while (create.GetData(*gs, ls, c)) host_chunks.push_back(c);
-      }
-      {
-        t0 = clk::now();
-        rpt::DeviceContext c3(dev);
-        bfh->ReinitializeAndRehash(c3, n_cb, host_chunks, {0});
-        host_s = std::chrono::duration<double>(clk::now() - t0).count();
-      }
-      printf("{\"op\": \"CreateBF\", \"rows\": %zu, \"sink_threads\": %d, \"sink_flush_rows\": %llu, "
-             "\"segments\": %zu, \"sink_combine_rows_per_s\": %.4g, \"finalize_ms\": %.2f, "
-             "\"rehash_hbm_ms\": %.2f, \"rehash_from_host_ms\": %.2f, \"resized\": %s, \"same_words\": %s}\n",
-             n_cb, T, static_cast<unsigned long long>(flush), create.DeviceKeys(0).segments().size(), n_cb / sink_s,
-             fin_s * 1e3, hbm_s * 1e3, host_s * 1e3, create.Resized(0) ? "true" : "false",
-             bfh->ExportWords() == words ? "true" : "false");
-    }
-  }
-  return 0;
+  return create_bf(dev);
 }
