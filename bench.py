@@ -97,6 +97,10 @@ def parse():
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="print only the cpu_baseline object for this config (no GPU; e.g. to put the CPU "
                          "restatement at T threads beside the host-resident GPU path of tools/host_bench)")
+    ap.add_argument("--cpu-chain", type=int, default=0,
+                    help="with --cpu-baseline-only: USE_BF's loop over this many filters instead (column 0 BIGINT "
+                         "10%% hits, column 1 INTEGER 50%%, column 2 BIGINT 50%%, ...: the shape of tools/host_bench "
+                         "--chain)")
     ap.add_argument("--merge", default="native", choices=["native", "torch"],
                     help="N > 1: the product merge rpt_bf_allreduce_or_ws over RCCL (default; a failing "
                          "communicator exits non-zero), or the torch.distributed composition (reported as "
@@ -359,6 +363,39 @@ def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, thre
     }
 
 
+def cpu_chain_baseline(k: int, n_build: int, n_filter: int, sample: int, threads: int) -> dict:
+    """USE_BF's filter loop (physical_use_bf.cpp:137-183) as the C++ restatement runs it: k filters, each sized for
+    n_filter rows with n_build keys (separate copies, so each has its own cache footprint), probe column f hitting
+    with 10 % (f = 0) or 50 % (f > 0), INTEGER for odd f (zero-extended: same hashes); per 2048-row vector, filter f
+    over the survivors of filters 0..f-1."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import numpy as np
+    import rpt_oracle as orc
+
+    lnb = orc.log_num_blocks(n_filter)
+    as_i32 = lambda x: x.astype(np.int32).view(np.uint32).astype(np.int64)  # noqa: E731
+    bases = []
+    for i32 in (False, True):  # the INTEGER columns' filter holds the build keys as INTEGERs
+        w = orc.new_words(lnb)
+        bk = orc.synth_build_keys(n_build)
+        orc.build_mt(w, lnb, as_i32(bk) if i32 else bk, threads)
+        bases.append(w)
+    words = [bases[f % 2].copy() for f in range(k)]
+    keys = []
+    for f in range(k):
+        kf = orc.synth_probe_keys(sample, n_build, 100 if f == 0 else 500, start=f << 40)
+        keys.append(as_i32(kf) if f % 2 else kf)
+    orc.probe_chain_mt(words, [lnb] * k, keys, threads)  # warm-up
+    runs = [orc.probe_chain_mt(words, [lnb] * k, keys, threads) for _ in range(5)]
+    med = statistics.median(r[0] for r in runs)
+    return {"value": sample / med, "unit": "rows/s", "cores": threads, "kind": "port", "filters": k,
+            "pass_fraction": runs[0][1] / sample,
+            "sample": (f"{sample:.0e} rows, {k} filters of 2^{lnb} blocks ({n_build:.0e} keys each), {threads} "
+                       "std::threads, 2048-row vectors, filter f over filter f-1's survivors, hash included; "
+                       "median of 5 after 1 warm-up"),
+            "cpu_model": _cpu_model()}
+
+
 def _cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -392,6 +429,10 @@ def main():
         n_filter = int(args.filter_rows) if args.filter_rows else (CONFIGS[cfg][1](1) if not args.build_rows else n_build)
         sample = int(args.cpu_sample) if args.cpu_sample else int(args.probe_rows)
         threads = args.cpu_threads or cpu_share()
+        if args.cpu_chain:
+            cb = cpu_chain_baseline(args.cpu_chain, n_build, n_filter, sample, threads)
+            print(json.dumps({"cpu_baseline": cb, "config": cfg}), flush=True)
+            return
         cb = cpu_baseline(n_build, n_filter, int(round(args.p * 1000)), sample, threads,
                           "--cpu-threads" if args.cpu_threads else "this process's CPU share", args.key_type)
         print(json.dumps({"cpu_baseline": cb, "config": cfg, "key_type": args.key_type}), flush=True)

@@ -445,4 +445,54 @@ double rpt_oracle_probe_mt(const uint64_t* words, int log_nb, const int64_t* key
   return s;
 }
 
+// USE_BF's filter loop per vector (physical_use_bf.cpp:137-183): filter 0 over every row of the vector, each
+// further filter over the previous one's survivors (its own key column, same rows), stopping when none are left;
+// per 2048-row vector on `threads` threads, hash included. The final survivors are counted (*out_count).
+double rpt_oracle_probe_chain_mt(const uint64_t* const* words, const int* log_nb, const int64_t* const* keys, int k,
+                                 uint64_t n, int threads, uint64_t* out_count) {
+  std::atomic<uint64_t> next{0};
+  std::atomic<uint64_t> total{0};
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> ts;
+  for (int t = 0; t < std::max(1, threads); t++) {
+    ts.emplace_back([&] {
+      uint64_t hashes[kVectorSize];
+      uint32_t sel[kVectorSize];
+      uint64_t local = 0;
+      for (;;) {
+        const uint64_t base = next.fetch_add(kVectorSize, std::memory_order_relaxed);
+        if (base >= n) break;
+        uint64_t cnt = std::min<uint64_t>(kVectorSize, n - base);
+        for (uint32_t i = 0; i < cnt; i++) sel[i] = i;
+        for (int f = 0; f < k && cnt > 0; f++) {
+          const uint64_t nb = 1ULL << log_nb[f];
+          const uint64_t* w = words[f];
+          const int64_t* kf = keys[f] + base;
+          uint64_t c = 0;
+          auto test = [&](uint64_t j) {  // j: index into the current survivors
+            const uint64_t h = hashes[j], m = mask_of(h);
+            sel[c] = sel[j];
+            c += (w[block_of(h, nb)] & m) == m;
+          };
+          constexpr uint64_t kLag = 24;
+          for (uint64_t j = 0; j < cnt; j++) {
+            hashes[j] = murmur64(static_cast<uint64_t>(kf[sel[j]]));
+            __builtin_prefetch(&w[block_of(hashes[j], nb)]);
+            if (j >= kLag) test(j - kLag);
+          }
+          for (uint64_t j = cnt > kLag ? cnt - kLag : 0; j < cnt; j++) test(j);
+          cnt = c;
+        }
+        local += cnt;
+        asm volatile("" ::"r"(sel) : "memory");
+      }
+      total.fetch_add(local);
+    });
+  }
+  for (auto& t : ts) t.join();
+  double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (out_count) *out_count = total.load();
+  return s;
+}
+
 }  // extern "C"

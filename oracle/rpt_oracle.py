@@ -45,6 +45,7 @@ _SIG = {
     "rpt_oracle_synth_probe_keys": (None, [c_uint64, c_uint32, c_uint64, c_uint64, c_void_p]),
     "rpt_oracle_build_mt": (c_double, [c_void_p, c_int, c_void_p, c_uint64, c_int]),
     "rpt_oracle_probe_mt": (c_double, [c_void_p, c_int, c_void_p, c_uint64, c_int, POINTER(c_uint64)]),
+    "rpt_oracle_probe_chain_mt": (c_double, [c_void_p, c_void_p, c_void_p, c_int, c_uint64, c_int, POINTER(c_uint64)]),
 }
 
 _lib = None
@@ -202,4 +203,19 @@ def probe_mt(words: np.ndarray, log_nb: int, keys: np.ndarray, threads: int) -> 
     keys = np.ascontiguousarray(keys, dtype=np.int64)
     cnt = c_uint64()
     s = lib().rpt_oracle_probe_mt(_p(words), log_nb, _p(keys), keys.size, threads, ctypes.byref(cnt))
+    return float(s), int(cnt.value)
+
+
+def probe_chain_mt(words: list, log_nbs: list, keys: list, threads: int) -> tuple[float, int]:
+    """USE_BF's filter loop per 2048-row vector (rpt_oracle_probe_chain_mt): filter f over column f of the rows
+    that passed filters 0..f-1. Returns (seconds, survivors)."""
+    k = len(words)
+    keys = [np.ascontiguousarray(x, dtype=np.int64) for x in keys]
+    n = keys[0].size
+    assert len(log_nbs) == k == len(keys) and all(x.size == n for x in keys)
+    wp = (ctypes.c_void_p * k)(*[w.ctypes.data for w in words])
+    kp = (ctypes.c_void_p * k)(*[x.ctypes.data for x in keys])
+    lp = (ctypes.c_int * k)(*log_nbs)
+    cnt = c_uint64()
+    s = lib().rpt_oracle_probe_chain_mt(wp, lp, kp, k, n, threads, ctypes.byref(cnt))
     return float(s), int(cnt.value)

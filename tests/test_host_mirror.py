@@ -1,8 +1,9 @@
 """C++ host mirror (include/rpt_host.hpp) of PTBloomFilter / CREATE_BF / USE_BF, end to end.
 
 The GPU test runs tests/cpp/build/test_host_mirror (4 sink threads, FLAT/CONSTANT/DICTIONARY vectors
-with NULLs, sink batches kept in HBM, resize + rehash from HBM in Finalize, the parallel source,
-a two-filter USE_BF chain, early exits) against the oracle.
+with NULLs, sink batches kept in HBM with asynchronous and synchronous flushes, resize + rehash from HBM in
+Finalize, the parallel source, a two-filter USE_BF chain, early exits, the pipelined batch paths on worker
+threads, 2- to 5-filter pipelined chains, the pinned staging cache) against the oracle.
 """
 import os
 import subprocess
@@ -29,7 +30,8 @@ def test_host_mirror_links():
     for name in ["rpt::PTBloomFilter::Insert", "rpt::PTBloomFilter::LookupSel", "rpt::CreateBF::Finalize",
                  "rpt::UseBF::Execute", "rpt::PTBloomFilter::ReinitializeAndRehash",
                  "rpt::CreateBF::GetData", "rpt::CreateBF::GetGlobalSourceState", "rpt::DeviceKeyColumn::Append",
-                 "rpt::PTBloomFilter::InsertDevice"]:
+                 "rpt::PTBloomFilter::InsertDevice", "rpt::UseBF::ExecuteBatch", "rpt::UseBF::ExecuteChainPipelined",
+                 "rpt::ReleasePinnedCache", "rpt::SetPinnedCacheLimit", "rpt::PinnedCacheBytes"]:
         assert name in syms, name
 
 
