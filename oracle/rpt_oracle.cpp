@@ -398,51 +398,14 @@ double rpt_oracle_build_mt(uint64_t* words, int log_nb, const int64_t* keys, uin
 }
 
 // Probe: per 2048-row vector hash -> LookupHashes into a per-thread SelectionVector
-// (physical_use_bf.hpp:16,23). The survivors are counted (sum returned in *out_count).
+// (physical_use_bf.hpp:16,23): the filter loop below with one filter. (Until r05 it had a loop of its own that
+// ran at half this rate at 16 threads on the GPU box's EPYC 9575F, same filter, keys and survivors, cause not
+// isolated: profiles/r05/cpu_baseline_check*.jsonl.) The survivors are counted (*out_count).
+double rpt_oracle_probe_chain_mt(const uint64_t* const* words, const int* log_nb, const int64_t* const* keys, int k,
+                                 uint64_t n, int threads, uint64_t* out_count);
 double rpt_oracle_probe_mt(const uint64_t* words, int log_nb, const int64_t* keys, uint64_t n, int threads,
                            uint64_t* out_count) {
-  const uint64_t nb = 1ULL << log_nb;
-  std::atomic<uint64_t> next{0};
-  std::atomic<uint64_t> total{0};
-  auto t0 = std::chrono::steady_clock::now();
-  std::vector<std::thread> ts;
-  for (int t = 0; t < std::max(1, threads); t++) {
-    ts.emplace_back([&] {
-      uint64_t hashes[kVectorSize];
-      uint32_t sel[kVectorSize];
-      uint64_t local = 0;
-      for (;;) {
-        uint64_t base = next.fetch_add(kVectorSize, std::memory_order_relaxed);
-        if (base >= n) break;
-        uint64_t cnt = std::min<uint64_t>(kVectorSize, n - base);
-        uint64_t c = 0;
-        auto test = [&](uint64_t i) {
-          const uint64_t h = hashes[i], m = mask_of(h);
-          sel[c] = static_cast<uint32_t>(i);
-          c += (words[block_of(h, nb)] & m) == m;
-        };
-        if (nb > kPrefetchMinWords) {  // software pipeline: row i is tested kLag rows after its prefetch
-          constexpr uint64_t kLag = 24;
-          for (uint64_t i = 0; i < cnt; i++) {
-            hashes[i] = murmur64(static_cast<uint64_t>(keys[base + i]));
-            __builtin_prefetch(&words[block_of(hashes[i], nb)]);
-            if (i >= kLag) test(i - kLag);
-          }
-          for (uint64_t i = cnt > kLag ? cnt - kLag : 0; i < cnt; i++) test(i);
-        } else {
-          for (uint64_t i = 0; i < cnt; i++) hashes[i] = murmur64(static_cast<uint64_t>(keys[base + i]));
-          for (uint64_t i = 0; i < cnt; i++) test(i);
-        }
-        local += c;
-        asm volatile("" ::"r"(sel) : "memory");
-      }
-      total.fetch_add(local);
-    });
-  }
-  for (auto& t : ts) t.join();
-  double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (out_count) *out_count = total.load();
-  return s;
+  return rpt_oracle_probe_chain_mt(&words, &log_nb, &keys, 1, n, threads, out_count);
 }
 
 // USE_BF's filter loop per vector (physical_use_bf.cpp:137-183): filter 0 over every row of the vector, each
