@@ -572,14 +572,14 @@ void DeviceContext::parallel_for(size_t n, const std::function<void(size_t)>& fn
 
 // ---- DeviceContext -----------------------------------------------------------------------------
 // ---- pinned host buffer cache ----------------------------------------------------------------------
-// Pinned buffers of contexts that grow a slot or die, kept for the next context that asks for that size
-// (powers of two from 64 KiB): hipHostMalloc pins every page, which per-query operator states would otherwise
-// pay on every query. Never freed at exit (the HIP runtime may be
-// gone by then); ReleasePinnedCache frees what is cached.
+// Pinned buffers of contexts that grow a slot or die, kept for the next context of that device that asks for that
+// size (powers of two from 64 KiB): hipHostMalloc pins every page (12.7 ms per 32 MiB on the GPU box), which
+// per-query operator states would otherwise pay on every query. Never freed at exit (the HIP runtime may be gone
+// by then); ReleasePinnedCache frees what is cached.
 namespace {
 struct PinnedCache {
   std::mutex mu;
-  std::map<size_t, std::vector<void*>> free;  // by capacity
+  std::map<std::pair<int, size_t>, std::vector<void*>> free;  // by (device, capacity)
   size_t cached = 0, limit = size_t(4) << 30;
 };
 PinnedCache& pinned_cache() {
@@ -591,11 +591,11 @@ size_t pinned_class(size_t bytes) {
   while (c < bytes) c <<= 1;
   return c;
 }
-void* pinned_take(size_t cap) {
+void* pinned_take(int device, size_t cap) {
   PinnedCache& c = pinned_cache();
   {
     std::lock_guard<std::mutex> lk(c.mu);
-    auto it = c.free.find(cap);
+    auto it = c.free.find({device, cap});
     if (it != c.free.end() && !it->second.empty()) {
       void* p = it->second.back();
       it->second.pop_back();
@@ -604,15 +604,16 @@ void* pinned_take(size_t cap) {
     }
   }
   void* p = nullptr;
+  DeviceScope ds(device);
   check_hip(hipHostMalloc(&p, cap, hipHostMallocDefault), "hipHostMalloc");
   return p;
 }
-void pinned_give(void* p, size_t cap) {  // p is no longer used by any stream
+void pinned_give(int device, void* p, size_t cap) {  // p is no longer used by any stream
   PinnedCache& c = pinned_cache();
   {
     std::lock_guard<std::mutex> lk(c.mu);
     if (c.cached + cap <= c.limit) {
-      c.free[cap].push_back(p);
+      c.free[{device, cap}].push_back(p);
       c.cached += cap;
       return;
     }
@@ -629,9 +630,9 @@ void SetPinnedCacheLimit(size_t bytes) {
     c.limit = bytes;
     for (auto it = c.free.rbegin(); it != c.free.rend() && c.cached > c.limit; ++it)
       while (!it->second.empty() && c.cached > c.limit) {
-        drop.emplace_back(it->second.back(), it->first);
+        drop.emplace_back(it->second.back(), it->first.second);
         it->second.pop_back();
-        c.cached -= it->first;
+        c.cached -= it->first.second;
       }
   }
   for (auto& d : drop) (void)hipHostFree(d.first);
@@ -645,7 +646,7 @@ size_t PinnedCacheBytes() {
 
 void ReleasePinnedCache() {
   PinnedCache& c = pinned_cache();
-  std::map<size_t, std::vector<void*>> all;
+  std::map<std::pair<int, size_t>, std::vector<void*>> all;
   {
     std::lock_guard<std::mutex> lk(c.mu);
     all.swap(c.free);
@@ -668,7 +669,7 @@ DeviceContext::~DeviceContext() {
   for (void* st : {stream_, copy_stream_, h2d_stream_, aux_streams_[0], aux_streams_[1]})
     if (st) (void)hipStreamSynchronize(static_cast<hipStream_t>(st));
   for (auto& b : host_)
-    if (b.p) pinned_give(b.p, b.cap);  // the streams are drained above
+    if (b.p) pinned_give(device_, b.p, b.cap);  // the streams are drained above
   for (auto& b : dev_)
     if (b.p) (void)hipFree(b.p);
   for (void* e : events_)
@@ -733,11 +734,11 @@ void* DeviceContext::host(int slot, size_t bytes) {
   Buf& b = host_[slot];
   if (b.cap < bytes) {
     synchronize();
-    if (b.p) pinned_give(b.p, b.cap);
+    if (b.p) pinned_give(device_, b.p, b.cap);
     b.p = nullptr;
     b.dp = nullptr;
     const size_t cap = pinned_class(std::max(bytes, 2 * b.cap));
-    b.p = pinned_take(cap);
+    b.p = pinned_take(device_, cap);
     b.cap = cap;
   }
   return b.p;
