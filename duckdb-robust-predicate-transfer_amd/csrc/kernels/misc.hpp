@@ -70,6 +70,21 @@ __global__ __launch_bounds__(kBlockThreads) void or_slices_kernel(uint64_t* __re
   }
 }
 
+// ---- narrow BIGINT keys: 4-B low words + one high word per chunk -> int64 keys --------------------
+// One workgroup per chunk c (rows [row0[c], row0[c + 1])): out[r] = hi[c] << 32 | lo[r]. The host-to-device copy of
+// a host-resident batch is the bound of the DuckDB shim; BIGINT keys whose chunk shares its high 32 bits
+// cross PCIe as 4 B and are widened here (HBM: 12 B per key, microseconds per stage).
+constexpr int kWidenThreads = 256;
+__global__ __launch_bounds__(kWidenThreads) void widen_keys_kernel(const uint32_t* __restrict__ lo,
+                                                                  const uint32_t* __restrict__ hi,
+                                                                  const uint32_t* __restrict__ row0,
+                                                                  uint64_t* __restrict__ out) {
+  const uint32_t c = blockIdx.x;
+  const uint32_t a = row0[c], e = row0[c + 1];
+  const uint64_t h = static_cast<uint64_t>(hi[c]) << 32;
+  for (uint32_t r = a + threadIdx.x; r < e; r += kWidenThreads) out[r] = h | lo[r];
+}
+
 // ---- popcount ------------------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlockThreads) void popcount_kernel(const uint64_t* __restrict__ w, uint64_t n_words,
                                                                 unsigned long long* __restrict__ out) {

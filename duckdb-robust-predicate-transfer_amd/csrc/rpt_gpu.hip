@@ -1602,6 +1602,19 @@ int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, r
   return launch_hash<false>(col, n, out_hashes, stream);
 }
 
+int rpt_keys_widen(const uint32_t* lo, const uint32_t* chunk_hi, const uint32_t* chunk_row0, uint64_t n_chunks,
+                   uint64_t* out, rpt_stream_t stream) {
+  if (n_chunks == 0) return RPT_OK;
+  if (!lo || !chunk_hi || !chunk_row0 || !out) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  if (n_chunks > 0x7FFFFFFFu) return fail(RPT_ERR_INVALID_ARGUMENT, "too many chunks");
+  ProfScope prof_w("widen_keys_kernel", as_stream(stream));
+  hipLaunchKernelGGL(rpt::widen_keys_kernel, dim3(static_cast<unsigned>(n_chunks)), dim3(rpt::kWidenThreads), 0,
+                     as_stream(stream), lo, chunk_hi, chunk_row0, out);
+  prof_w.end();
+  RPT_LAUNCHED("widen_keys_kernel");
+  return RPT_OK;
+}
+
 int rpt_words_or_slices(uint64_t* dst, const uint64_t* srcs, uint32_t k, uint64_t n_words, rpt_stream_t stream) {
   if (!dst || (!srcs && k > 0)) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
   if (n_words == 0) return RPT_OK;

@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <emmintrin.h>  // SSE2 streaming stores (x86-64 baseline) for the pinned staging copies
+#include <immintrin.h>  // AVX2 (runtime-dispatched) for the narrow-key packing
 
 #include <algorithm>
 #include <chrono>
@@ -268,12 +269,140 @@ struct Flattened {
   const uint8_t* keys;
   const uint64_t* valid;
   bool any_null;
+  // narrow: BIGINT keys as 4-B low words, meta = each chunk's high word [n_chunks] then the chunks' first rows
+  // [n_chunks + 1] (uint32), widened on the device (rpt_keys_widen)
+  bool narrow = false;
+  const uint32_t* meta = nullptr;
+  uint64_t n_chunks = 0;
 };
+
+// FLAT BIGINT keys src[0 .. count) -> their low words at lo; returns the OR of (key ^ v0) >> 32 (0: they all
+// share v0's high word). AVX2 where the host has it (runtime dispatch; the GPU box's EPYC does), SSE2 otherwise.
+__attribute__((target("avx2"))) uint64_t narrow_flat_avx2(const int64_t* src, uint64_t count, uint32_t* lo, uint64_t v0) {
+  const __m256i x = _mm256_set1_epi64x(static_cast<long long>(v0));
+  const __m256i even = _mm256_setr_epi32(0, 2, 4, 6, 1, 3, 5, 7);
+  __m256i acc = _mm256_setzero_si256();
+  const bool aligned = (reinterpret_cast<uintptr_t>(lo) & 31) == 0;
+  uint64_t r = 0;
+  for (; r + 8 <= count; r += 8) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + r));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + r + 4));
+    acc = _mm256_or_si256(acc, _mm256_or_si256(_mm256_srli_epi64(_mm256_xor_si256(a, x), 32),
+                                               _mm256_srli_epi64(_mm256_xor_si256(b, x), 32)));
+    // low dwords of a into the low 128 bits, of b into the high 128 bits
+    const __m256i pa = _mm256_permutevar8x32_epi32(a, even), pb = _mm256_permutevar8x32_epi32(b, even);
+    const __m256i packed = _mm256_permute2x128_si256(pa, pb, 0x20);
+    if (aligned) _mm256_stream_si256(reinterpret_cast<__m256i*>(lo + r), packed);
+    else _mm256_storeu_si256(reinterpret_cast<__m256i*>(lo + r), packed);
+  }
+  uint64_t tail = 0;
+  for (; r < count; r++) {
+    const uint64_t k = static_cast<uint64_t>(src[r]);
+    tail |= (k ^ v0) >> 32;
+    lo[r] = static_cast<uint32_t>(k);
+  }
+  if (aligned) _mm_sfence();
+  alignas(32) uint64_t a4[4];
+  _mm256_store_si256(reinterpret_cast<__m256i*>(a4), acc);
+  return a4[0] | a4[1] | a4[2] | a4[3] | tail;
+}
+
+uint64_t narrow_flat_sse2(const int64_t* src, uint64_t count, uint32_t* lo, uint64_t v0) {
+  const __m128i x = _mm_set1_epi64x(static_cast<long long>(v0));
+  __m128i acc = _mm_setzero_si128();
+  const bool aligned = (reinterpret_cast<uintptr_t>(lo) & 15) == 0;
+  uint64_t r = 0;
+  for (; r + 4 <= count; r += 4) {
+    const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + r));
+    const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + r + 2));
+    acc = _mm_or_si128(acc, _mm_or_si128(_mm_srli_epi64(_mm_xor_si128(a, x), 32), _mm_srli_epi64(_mm_xor_si128(b, x), 32)));
+    // the low dwords of a and b -> one 16-B store
+    const __m128i packed = _mm_unpacklo_epi64(_mm_shuffle_epi32(a, _MM_SHUFFLE(2, 0, 2, 0)),
+                                              _mm_shuffle_epi32(b, _MM_SHUFFLE(2, 0, 2, 0)));
+    if (aligned) _mm_stream_si128(reinterpret_cast<__m128i*>(lo + r), packed);
+    else _mm_storeu_si128(reinterpret_cast<__m128i*>(lo + r), packed);
+  }
+  uint64_t tail = 0;
+  for (; r < count; r++) {
+    const uint64_t k = static_cast<uint64_t>(src[r]);
+    tail |= (k ^ v0) >> 32;
+    lo[r] = static_cast<uint32_t>(k);
+  }
+  if (aligned) _mm_sfence();
+  alignas(16) uint64_t a2[2];
+  _mm_store_si128(reinterpret_cast<__m128i*>(a2), acc);
+  return a2[0] | a2[1] | tail;
+}
+
+const bool g_has_avx2 = __builtin_cpu_supports("avx2");
+
+// One chunk's BIGINT keys as their low 32-bit words at `lo` and the high word they all share in *hi, NULL rows
+// cleared in `valid_words` from bit row0 on (as flatten_column). False when the keys do not share their high word
+// (or for SEQUENCE vectors); `lo` and the validity bits are then partly written and the caller re-flattens.
+bool narrow_column(const Vector& v, uint64_t count, uint32_t* lo, uint32_t* hi, uint64_t* valid_words, uint64_t row0,
+                   bool& any_null) {
+  if (v.key_type != KeyType::I64 || count == 0) return count == 0 && v.key_type == KeyType::I64;
+  const int64_t* src = static_cast<const int64_t*>(v.data);
+  switch (v.type) {
+    case VectorType::FLAT: {
+      const uint64_t v0 = static_cast<uint64_t>(src[0]);
+      if ((g_has_avx2 ? narrow_flat_avx2(src, count, lo, v0) : narrow_flat_sse2(src, count, lo, v0)) != 0) return false;
+      *hi = static_cast<uint32_t>(v0 >> 32);
+      if (v.validity) {
+        for (uint64_t q = 0; q < count; q += 64) {
+          const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - q));
+          const uint64_t nulls = ~mask_bits(v.validity, q, n) & (n == 64 ? ~0ULL : (1ULL << n) - 1);
+          any_null |= nulls != 0;
+          clear_bits(valid_words, row0 + q, nulls, n);
+        }
+      }
+      return true;
+    }
+    case VectorType::CONSTANT: {
+      const uint64_t k = static_cast<uint64_t>(src[0]);
+      std::fill(lo, lo + count, static_cast<uint32_t>(k));
+      *hi = static_cast<uint32_t>(k >> 32);
+      if (!valid_bit(v.validity, 0)) {
+        any_null = true;
+        for (uint64_t q = 0; q < count; q += 64) clear_bits(valid_words, row0 + q, ~0ULL, static_cast<uint32_t>(std::min<uint64_t>(64, count - q)));
+      }
+      return true;
+    }
+    case VectorType::DICTIONARY: {
+      if (v.dict_size == 0) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
+      const uint64_t v0 = static_cast<uint64_t>(src[v.sel[0] < v.dict_size ? v.sel[0] : 0]);
+      uint64_t acc = 0;
+      for (uint64_t q = 0; q < count; q += 64) {
+        const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - q));
+        const uint32_t* sel = v.sel + q;
+        uint32_t kmax = 0;
+        for (uint32_t e = 0; e < n; e++) kmax = std::max(kmax, sel[e]);
+        if (kmax >= v.dict_size) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "dictionary index out of range");
+        for (uint32_t e = 0; e < n; e++) {
+          const uint64_t k = static_cast<uint64_t>(src[sel[e]]);
+          acc |= (k ^ v0) >> 32;
+          lo[q + e] = static_cast<uint32_t>(k);
+        }
+        if (v.validity) {
+          uint64_t nulls = 0;
+          for (uint32_t e = 0; e < n; e++) nulls |= static_cast<uint64_t>(!valid_bit(v.validity, sel[e])) << e;
+          any_null |= nulls != 0;
+          clear_bits(valid_words, row0 + q, nulls, n);
+        }
+      }
+      if (acc != 0) return false;
+      *hi = static_cast<uint32_t>(v0 >> 32);
+      return true;
+    }
+    default:
+      return false;
+  }
+}
 
 // Column `col` of chunks[0 .. n_chunks) (total rows) into pinned slots `slot` (keys) and `valid_slot` (validity
 // words; default slot + 1).
 Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, size_t n_chunks, uint64_t col,
-                         uint64_t total, int slot, int valid_slot = -1) {
+                         uint64_t total, int slot, int valid_slot = -1, int narrow_slot = -1) {
   if (valid_slot < 0) valid_slot = slot + 1;
   if (n_chunks == 0) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "no chunks");
   const Vector& v0 = chunks[0]->data.at(col);
@@ -281,13 +410,42 @@ Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, siz
   const uint64_t nwords = (total + 63) / 64;
   auto* hkeys = static_cast<uint8_t*>(ctx.host(slot, std::max<size_t>(total * es, 16)));
   auto* hvalid = static_cast<uint64_t*>(ctx.host(valid_slot, std::max<size_t>(nwords * 8, 8)));
-  std::memset(hvalid, 0xFF, nwords * 8);  // all valid; flatten_column clears the NULL rows
   std::vector<uint64_t> row0(n_chunks + 1, 0);
   for (size_t i = 0; i < n_chunks; i++) {
     if (chunks[i]->data.at(col).key_type != v0.key_type)
       throw GpuError(RPT_ERR_INVALID_ARGUMENT, "mixed key types in one column");
     row0[i + 1] = row0[i] + chunks[i]->count;
   }
+  const bool big = total >= (1u << 17) && n_chunks >= 16 && ctx.flatten_threads > 1;  // from 128 Ki rows (a ramp stage)
+  const size_t n_tasks = big ? std::min<size_t>(n_chunks / 4, 4 * static_cast<size_t>(ctx.flatten_threads)) : 1;
+  // narrow BIGINT keys: every chunk's keys share their high word -> 4 B per key over PCIe (else the plain flatten
+  // below, after this attempt's partial writes)
+  if (narrow_slot >= 0 && v0.key_type == KeyType::I64 && total < (1ULL << 32)) {
+    std::memset(hvalid, 0xFF, nwords * 8);
+    auto* lo = reinterpret_cast<uint32_t*>(hkeys);
+    auto* meta = static_cast<uint32_t*>(ctx.host(narrow_slot, (2 * n_chunks + 1) * 4));
+    for (size_t i = 0; i <= n_chunks; i++) meta[n_chunks + i] = static_cast<uint32_t>(row0[i]);
+    std::atomic<bool> ok{true};
+    std::vector<char> nulls(n_tasks, 0);
+    auto range = [&](size_t t) {
+      bool nl = false;
+      for (size_t i = n_chunks * t / n_tasks; i < n_chunks * (t + 1) / n_tasks && ok.load(std::memory_order_relaxed); i++)
+        if (!narrow_column(chunks[i]->data.at(col), chunks[i]->count, lo + row0[i], meta + i, hvalid, row0[i], nl))
+          ok.store(false, std::memory_order_relaxed);
+      nulls[t] = nl ? 1 : 0;
+    };
+    if (n_tasks == 1) range(0);
+    else ctx.parallel_for(n_tasks, range);
+    if (ok.load()) {
+      Flattened f{KeyType::I64, hkeys, hvalid, false};
+      for (char c : nulls) f.any_null |= c != 0;
+      f.narrow = true;
+      f.meta = meta;
+      f.n_chunks = n_chunks;
+      return f;
+    }
+  }
+  std::memset(hvalid, 0xFF, nwords * 8);  // all valid; flatten_column clears the NULL rows
   // Flattening into the pinned staging buffer is the host side's bottleneck for large batches; big
   // batches are split over ctx.flatten_threads threads by chunk.
   auto flatten_range = [&](size_t lo, size_t hi) {
@@ -297,11 +455,10 @@ Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, siz
     return nulls;
   };
   bool any_null = false;
-  if (total < (1u << 17) || n_chunks < 16 || ctx.flatten_threads <= 1) {  // from 128 Ki rows (a ramp stage)
+  if (!big) {
     any_null = flatten_range(0, n_chunks);
   } else {
     // several ranges per worker thread, so uneven chunks (dictionaries, conversions) still balance
-    const size_t n_tasks = std::min<size_t>(n_chunks / 4, 4 * static_cast<size_t>(ctx.flatten_threads));
     std::vector<char> nulls(n_tasks, 0);
     ctx.parallel_for(n_tasks, [&](size_t t) {
       nulls[t] = flatten_range(n_chunks * t / n_tasks, n_chunks * (t + 1) / n_tasks) ? 1 : 0;
@@ -314,9 +471,17 @@ Flattened flatten_pinned(DeviceContext& ctx, const DataChunk* const* chunks, siz
 // Copy a flattened column to device buffers (dvalid is only written when the batch had NULLs), on `stream`
 // (default: the context's).
 rpt_key_column copy_flattened(DeviceContext& ctx, const Flattened& f, uint64_t total, void* dkeys, void* dvalid,
-                              void* stream = nullptr) {
+                              void* stream = nullptr, void* d_lo = nullptr, void* d_meta = nullptr) {
   auto s = static_cast<hipStream_t>(stream ? stream : ctx.stream());
-  check_hip(hipMemcpyAsync(dkeys, f.keys, total * key_size(f.key_type), hipMemcpyHostToDevice, s), "stage keys");
+  if (f.narrow) {  // 4-B low words + the chunks' high words and first rows, widened into dkeys
+    if (!d_lo || !d_meta) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "narrow keys without device staging");
+    check_hip(hipMemcpyAsync(d_lo, f.keys, total * 4, hipMemcpyHostToDevice, s), "stage keys");
+    check_hip(hipMemcpyAsync(d_meta, f.meta, (2 * f.n_chunks + 1) * 4, hipMemcpyHostToDevice, s), "stage chunk words");
+    const auto* m = static_cast<const uint32_t*>(d_meta);
+    check(rpt_keys_widen(static_cast<const uint32_t*>(d_lo), m, m + f.n_chunks, f.n_chunks, static_cast<uint64_t*>(dkeys), s));
+  } else {
+    check_hip(hipMemcpyAsync(dkeys, f.keys, total * key_size(f.key_type), hipMemcpyHostToDevice, s), "stage keys");
+  }
   if (f.any_null)
     check_hip(hipMemcpyAsync(dvalid, f.valid, (total + 63) / 64 * 8, hipMemcpyHostToDevice, s), "stage validity");
   rpt_key_column kc;
@@ -412,9 +577,19 @@ struct PTBloomFilter::PipelineBuffers {
   uint64_t* d_cnt[2];
   uint32_t* h_sel[2];
   uint64_t* h_cnt[2];
+  // narrow BIGINT stages (max_chunks > 0): device slots 56 + b (4-B low words), 58 + b and host slot 56 + b (the
+  // chunks' high words and first rows)
+  void* d_lo[2] = {nullptr, nullptr};
+  void* d_meta[2] = {nullptr, nullptr};
+  static constexpr int kNarrowMeta = 56;
   DeviceContext& ctx;
-  PipelineBuffers(DeviceContext& c, uint64_t max_rows, size_t key_bytes) : ctx(c) {
+  PipelineBuffers(DeviceContext& c, uint64_t max_rows, size_t key_bytes, size_t max_chunks = 0) : ctx(c) {
     const size_t words = (max_rows + 63) / 64 * 8;
+    for (int b = 0; max_chunks && b < 2; b++) {
+      d_lo[b] = ctx.dev(56 + b, std::max<size_t>(max_rows * 4, 16));
+      d_meta[b] = ctx.dev(58 + b, (2 * max_chunks + 1) * 4);
+      (void)ctx.host(kNarrowMeta + b, (2 * max_chunks + 1) * 4);
+    }
     for (int b = 0; b < 2; b++) {
       (void)ctx.host(kHostKeys + 2 * b, std::max<size_t>(max_rows * key_bytes, 16));
       (void)ctx.host(kHostKeys + 2 * b + 1, std::max<size_t>(words, 8));
@@ -880,8 +1055,12 @@ void PTBloomFilter::InsertPipelined(DeviceContext& ctx, const std::vector<const 
     total += r.rows;
     ws_bytes = std::max(ws_bytes, rpt_bf_insert_workspace_bytes(bf_, r.rows));
   }
-  const size_t es = key_size(device_type(chunks[st[0].c_lo]->data.at(col).key_type));
-  PipelineBuffers pb(ctx, max_rows, es);
+  const KeyType kt = chunks[st[0].c_lo]->data.at(col).key_type;
+  const size_t es = key_size(device_type(kt));
+  bool narrow = ctx.narrow_keys && kt == KeyType::I64;  // until a stage's keys are not narrow
+  size_t max_chunks = 0;
+  for (const StageRange& r : st) max_chunks = std::max(max_chunks, r.c_hi - r.c_lo);
+  PipelineBuffers pb(ctx, max_rows, es, narrow ? max_chunks : 0);
   void* ws = ws_bytes ? ctx.dev(6, ws_bytes) : nullptr;
   auto s = static_cast<hipStream_t>(ctx.stream());
   auto h = static_cast<hipStream_t>(ctx.h2d_stream());
@@ -893,11 +1072,14 @@ void PTBloomFilter::InsertPipelined(DeviceContext& ctx, const std::vector<const 
       ps.wait_copy_s += secs_since(t0);
       t0 = Clock::now();
       const Flattened f = flatten_pinned(ctx, chunks.data() + st[i].c_lo, st[i].c_hi - st[i].c_lo, col, st[i].rows,
-                                         PipelineBuffers::kHostKeys + 2 * b);
+                                         PipelineBuffers::kHostKeys + 2 * b, -1,
+                                         narrow ? PipelineBuffers::kNarrowMeta + b : -1);
+      narrow = f.narrow;
+      ps.narrow_stages += f.narrow;
       ps.flatten_s += secs_since(t0);
       t0 = Clock::now();
       if (i >= 2) check_hip(hipStreamWaitEvent(h, pb.probed(b), 0), "hipStreamWaitEvent");  // insert i-2 read it
-      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b], h);
+      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b], h, pb.d_lo[b], pb.d_meta[b]);
       check_hip(hipEventRecord(pb.copied(b), h), "hipEventRecord");
       check_hip(hipStreamWaitEvent(s, pb.copied(b), 0), "hipStreamWaitEvent");
       if (rpt_bf_insert_workspace_bytes(bf_, st[i].rows)) check(rpt_bf_insert_ws(bf_, &kc, st[i].rows, ws, ws_bytes, s));
@@ -1020,8 +1202,12 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
     total += r.rows;
     ws_bytes = std::max(ws_bytes, rpt_bf_probe_workspace_bytes(bf_, r.rows));
   }
-  const size_t es = key_size(device_type(chunks[st[0].c_lo]->data.at(col).key_type));
-  PipelineBuffers pb(ctx, max_rows, es);
+  const KeyType kt = chunks[st[0].c_lo]->data.at(col).key_type;
+  const size_t es = key_size(device_type(kt));
+  bool narrow = ctx.narrow_keys && kt == KeyType::I64;  // until a stage's keys are not narrow
+  size_t max_chunks = 0;
+  for (const StageRange& r : st) max_chunks = std::max(max_chunks, r.c_hi - r.c_lo);
+  PipelineBuffers pb(ctx, max_rows, es, narrow ? max_chunks : 0);
   void* ws = ctx.dev(2, ws_bytes);
   auto s = static_cast<hipStream_t>(ctx.stream());
   auto d = static_cast<hipStream_t>(ctx.copy_stream());
@@ -1056,11 +1242,14 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
       ps.wait_copy_s += secs_since(t0);
       t0 = Clock::now();
       const Flattened f = flatten_pinned(ctx, chunks.data() + st[i].c_lo, st[i].c_hi - st[i].c_lo, col, st[i].rows,
-                                         PipelineBuffers::kHostKeys + 2 * b);
+                                         PipelineBuffers::kHostKeys + 2 * b, -1,
+                                         narrow ? PipelineBuffers::kNarrowMeta + b : -1);
+      narrow = f.narrow;
+      ps.narrow_stages += f.narrow;
       ps.flatten_s += secs_since(t0);
       t0 = Clock::now();
       if (i >= 2) check_hip(hipStreamWaitEvent(h, pb.probed(b), 0), "hipStreamWaitEvent");  // probe i-2 read it
-      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b], h);
+      const rpt_key_column kc = copy_flattened(ctx, f, st[i].rows, pb.d_keys[b], pb.d_valid[b], h, pb.d_lo[b], pb.d_meta[b]);
       check_hip(hipEventRecord(pb.copied(b), h), "hipEventRecord");
       check_hip(hipStreamWaitEvent(s, pb.copied(b), 0), "hipStreamWaitEvent");
       if (i >= 2) check_hip(hipStreamWaitEvent(s, pb.returned(b), 0), "hipStreamWaitEvent");  // d_sel[b] free

@@ -250,6 +250,13 @@ int rpt_hash_keys(const rpt_key_column* col, uint64_t n, uint64_t* out_hashes, r
  * rpt_hash_combine(col_j) for j = 1, 2, ... is the composite-key hash; insert / probe it as an
  * RPT_KEY_HASH column. */
 int rpt_hash_combine(const rpt_key_column* col, uint64_t n, uint64_t* inout_hashes, rpt_stream_t stream);
+/* Narrow BIGINT keys (device memory): out[r] = (uint64_t)chunk_hi[c] << 32 | lo[r] for the rows r of chunk c,
+ * [chunk_row0[c], chunk_row0[c + 1]), c < n_chunks (chunk_row0 ascending; out and lo hold chunk_row0[n_chunks]
+ * entries). A host-resident batch whose chunks each share their keys' high 32 bits crosses PCIe as 4-B low words
+ * plus one high word per chunk and is widened here before the insert / probe (the C++ host mirror does this by
+ * itself). Stream-ordered; n_chunks == 0 is a no-op. */
+int rpt_keys_widen(const uint32_t* lo, const uint32_t* chunk_hi, const uint32_t* chunk_row0, uint64_t n_chunks,
+                   uint64_t* out, rpt_stream_t stream);
 
 /* ---- merge / fold / export ----------------------------------------------------------------- */
 /* dst |= src (same log_num_blocks, same device): merging per-thread or per-GPU partial filters

@@ -122,6 +122,10 @@ class DeviceContext {
   // memory and split a stage's selection vector into per-chunk ones. DuckDB's operator threads each own a
   // DeviceContext, so with many of them 1-2 per context is enough.
   unsigned flatten_threads = 8;
+  // Pipelined BIGINT batches whose chunks each share their keys' high 32 bits (ids below 2^32, or any 2^32-aligned
+  // window) cross PCIe as 4-B low words and are widened on the device (rpt_keys_widen): half the bytes of the
+  // shim's bound. A stage that does not qualify is flattened as 8-B keys and the rest of the batch stays plain.
+  bool narrow_keys = true;
 
   // Host-side time of the pipelined batch paths by phase (accumulated; reset by assigning {}): where a
   // host-resident batch's time goes (tools/host_bench reports it).
@@ -133,6 +137,7 @@ class DeviceContext {
     double wait_count_s = 0;  // waiting for a stage's survivor count (probe done)
     double wait_sel_s = 0;    // waiting for a stage's selection vector to arrive on the host
     double split_s = 0;       // stage sel -> per-chunk sels (worker threads)
+    uint64_t narrow_stages = 0;  // stages sent as narrow BIGINT keys
     double total_s = 0;
   };
   PipelineStats stats;

@@ -653,9 +653,96 @@ static void pinned_cache(int dev) {
   EXPECT(rpt::PinnedCacheBytes() == 0, "released");
 }
 
+// Narrow BIGINT keys (DeviceContext::narrow_keys): chunks whose keys share their high 32 bits (0, 5 and 0xFFFFFFFF,
+// i.e. negative keys, by chunk) cross PCIe as 4-B low words and are widened on the device; FLAT / DICTIONARY /
+// CONSTANT chunks with NULLs, pipelined insert and lookup against the oracle, the same with narrow_keys off, and
+// a batch whose chunks mix high words (stays plain after its first stage's attempt).
+static void narrow_keys(int dev) {
+  const size_t nb = (2u << 20) + 333, np = (3u << 20) + 555;
+  Table bt = make_table(nb, 31, 47, 0), pt = make_table(np, 32, 43, 2048);
+  const uint32_t his[3] = {0u, 5u, 0xFFFFFFFFu};
+  auto narrowed = [&](Table& t, size_t n) {
+    for (size_t i = 0; i < n; i++)
+      t.c0[i] = static_cast<int64_t>((static_cast<uint64_t>(his[(i / 2048) % 3]) << 32) |
+                                     static_cast<uint32_t>(t.c0[i] & 0x3FFFF));
+  };
+  narrowed(bt, nb);
+  narrowed(pt, np);
+  ChunkStore bst, pst;
+  make_chunks(bt, nb, bst, false);
+  make_chunks(pt, np, pst, true);
+  std::vector<const rpt::DataChunk*> bptrs, pptrs;
+  for (const auto& ch : bst.chunks) bptrs.push_back(&ch);
+  for (const auto& ch : pst.chunks) pptrs.push_back(&ch);
+  EXPECT(pptrs[3]->data[0].type == rpt::VectorType::CONSTANT, "chunk 3 column 0 CONSTANT");
+  const int lnb = rpt_oracle_log_num_blocks(nb);
+  std::vector<uint64_t> w(1ULL << lnb, 0);
+  {
+    const std::vector<uint64_t> vb = pack(bt.v0, 0, nb);
+    rpt_oracle_insert_i64(w.data(), lnb, bt.c0.data(), nullptr, vb.data(), nb);
+  }
+  std::vector<rpt::SelectionVector> want(pptrs.size());
+  for (size_t k = 0; k < pptrs.size(); k++) {
+    const size_t lo = 2048 * k, cnt = pptrs[k]->count;
+    const std::vector<uint64_t> vp = pack(pt.v0, lo, cnt);
+    want[k].resize(cnt);
+    want[k].resize(rpt_oracle_probe_i64(w.data(), lnb, pt.c0.data() + lo, nullptr, vp.data(), cnt, want[k].data()));
+  }
+  for (int on = 1; on >= 0; on--) {
+    rpt::DeviceContext ctx(dev);
+    ctx.pipeline_rows = 1u << 20;
+    ctx.flatten_threads = 4;
+    ctx.narrow_keys = on != 0;
+    auto f = std::make_shared<rpt::PTBloomFilter>();
+    f->Initialize(dev, static_cast<uint32_t>(nb));
+    f->InsertBatch(ctx, bptrs, {0});
+    EXPECT(f->ExportWords() == w, "pipelined insert of narrow keys (narrow_keys %d) differs from the oracle", on);
+    EXPECT(on ? ctx.stats.narrow_stages >= 2 : ctx.stats.narrow_stages == 0, "insert: %llu narrow stages (narrow_keys %d)",
+           (unsigned long long)ctx.stats.narrow_stages, on);
+    f->finalized_ = true;
+    ctx.stats = {};
+    std::vector<rpt::SelectionVector> sels;
+    f->LookupSelBatch(ctx, pptrs, sels, {0});
+    size_t bad = 0;
+    for (size_t k = 0; k < pptrs.size(); k++) bad += sels[k] != want[k];
+    EXPECT(bad == 0, "pipelined lookup of narrow keys (narrow_keys %d): %zu chunks differ", on, bad);
+    EXPECT(on ? ctx.stats.narrow_stages == ctx.stats.stages : ctx.stats.narrow_stages == 0,
+           "lookup: %llu of %llu stages narrow (narrow_keys %d)", (unsigned long long)ctx.stats.narrow_stages,
+           (unsigned long long)ctx.stats.stages, on);
+  }
+  // a batch whose chunks' keys straddle high words (BIGINT keys around 0: both signs in one chunk)
+  {
+    Table mt = make_table(np, 33, 0, 0);
+    ChunkStore mst;
+    make_chunks(mt, np, mst, false);
+    std::vector<const rpt::DataChunk*> mptrs;
+    for (const auto& ch : mst.chunks) mptrs.push_back(&ch);
+    rpt::DeviceContext ctx(dev);
+    ctx.pipeline_rows = 1u << 20;
+    auto f = std::make_shared<rpt::PTBloomFilter>();
+    f->Initialize(dev, static_cast<uint32_t>(nb));
+    f->InsertBatch(ctx, bptrs, {0});
+    f->finalized_ = true;
+    ctx.stats = {};
+    std::vector<rpt::SelectionVector> sels;
+    f->LookupSelBatch(ctx, mptrs, sels, {0});
+    size_t bad = 0;
+    for (size_t k = 0; k < mptrs.size(); k++) {
+      const size_t lo = 2048 * k, cnt = mptrs[k]->count;
+      const std::vector<uint64_t> vp = pack(mt.v0, lo, cnt);
+      rpt::SelectionVector e(cnt);
+      e.resize(rpt_oracle_probe_i64(w.data(), lnb, mt.c0.data() + lo, nullptr, vp.data(), cnt, e.data()));
+      bad += sels[k] != e;
+    }
+    EXPECT(bad == 0 && ctx.stats.narrow_stages == 0 && ctx.stats.stages >= 3, "mixed high words: %zu chunks differ, %llu narrow stages",
+           bad, (unsigned long long)ctx.stats.narrow_stages);
+  }
+}
+
 int main() {
   try {
     const int dev = 0;
+    narrow_keys(dev);
     pinned_cache(dev);
     pipelined_workers(dev);
     pipelined_chain(dev);

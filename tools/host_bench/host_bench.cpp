@@ -23,10 +23,89 @@ using clk = std::chrono::steady_clock;
 double since(clk::time_point t0) { return std::chrono::duration<double>(clk::now() - t0).count(); }
 
 void print_stats(const char* what, const rpt::DeviceContext::PipelineStats& ps, double calls) {
-  printf("\"%s\": {\"stages_per_call\": %.1f, \"flatten_ms\": %.3f, \"enqueue_ms\": %.3f, \"wait_copy_ms\": %.3f, "
-         "\"wait_count_ms\": %.3f, \"wait_sel_ms\": %.3f, \"split_ms\": %.3f, \"total_ms\": %.3f}",
-         what, ps.stages / calls, ps.flatten_s / calls * 1e3, ps.enqueue_s / calls * 1e3, ps.wait_copy_s / calls * 1e3,
-         ps.wait_count_s / calls * 1e3, ps.wait_sel_s / calls * 1e3, ps.split_s / calls * 1e3, ps.total_s / calls * 1e3);
+  printf("\"%s\": {\"stages_per_call\": %.1f, \"narrow_stages_per_call\": %.1f, \"flatten_ms\": %.3f, \"enqueue_ms\": %.3f, "
+         "\"wait_copy_ms\": %.3f, \"wait_count_ms\": %.3f, \"wait_sel_ms\": %.3f, \"split_ms\": %.3f, \"total_ms\": %.3f}",
+         what, ps.stages / calls, ps.narrow_stages / calls, ps.flatten_s / calls * 1e3, ps.enqueue_s / calls * 1e3,
+         ps.wait_copy_s / calls * 1e3, ps.wait_count_s / calls * 1e3, ps.wait_sel_s / calls * 1e3, ps.split_s / calls * 1e3,
+         ps.total_s / calls * 1e3);
+}
+
+// Narrow BIGINT keys (DeviceContext::narrow_keys): C2's shape (1e7 build keys, 2^25 probe rows in 2048-row FLAT
+// chunks, p = 0.1) with keys below 2^32 (4-B low words over PCIe) and with random 63-bit keys (the narrow attempt
+// fails on the first stage), InsertBatch and LookupSelBatch (4 Mi-row stages, 8 workers) with narrow_keys on / off.
+int host_narrow(int dev) {
+  const size_t n_build = 10000000, n_probe = 1ULL << 25;
+  for (int ids : {1, 0}) {
+    std::mt19937_64 rng(17);
+    const uint64_t mask = ids ? 0xFFFFFFFFULL : (~0ULL >> 1);
+    std::vector<int64_t> b(n_build), q(n_probe);
+    for (auto& k : b) k = static_cast<int64_t>(rng() & mask);
+    for (size_t i = 0; i < n_probe; i++) q[i] = (rng() % 10 == 0) ? b[rng() % n_build] : static_cast<int64_t>(rng() & mask);
+    auto chunks = [](const std::vector<int64_t>& v) {
+      std::vector<rpt::DataChunk> cs;
+      for (size_t lo = 0; lo < v.size(); lo += 2048) {
+        rpt::DataChunk c;
+        c.count = std::min<size_t>(2048, v.size() - lo);
+        rpt::Vector x;
+        x.key_type = rpt::KeyType::I64;
+        x.data = v.data() + lo;
+        c.data.push_back(x);
+        cs.push_back(c);
+      }
+      return cs;
+    };
+    auto bch = chunks(b), pch = chunks(q);
+    std::vector<const rpt::DataChunk*> ball, pall;
+    for (auto& c : bch) ball.push_back(&c);
+    for (auto& c : pch) pall.push_back(&c);
+    std::vector<uint64_t> words[2];
+    std::vector<rpt::SelectionVector> sels[2];
+    for (int cfg = 0; cfg < 3; cfg++) {
+      const int on = cfg > 0 ? 1 : 0;
+      const unsigned workers = cfg == 2 ? 16 : 8;
+      rpt::DeviceContext ctx(dev);
+      ctx.narrow_keys = on != 0;
+      ctx.flatten_threads = workers;
+      rpt::PTBloomFilter bf;
+      bf.Initialize(dev, static_cast<uint32_t>(n_build));
+      bf.InsertBatch(ctx, ball, {0});  // warm-up
+      const int calls = 4;
+      ctx.stats = {};
+      double ins = 0;
+      for (int c = 0; c < calls; c++) {
+        const auto t0 = clk::now();
+        bf.InsertBatch(ctx, ball, {0});
+        ins += since(t0);
+      }
+      const auto ins_stats = ctx.stats;
+      words[on] = bf.ExportWords();
+      bf.finalized_ = true;
+      bf.LookupSelBatch(ctx, pall, sels[on], {0});  // warm-up
+      ctx.stats = {};
+      double sec = 0;
+      for (int c = 0; c < calls; c++) {
+        const auto t0 = clk::now();
+        bf.LookupSelBatch(ctx, pall, sels[on], {0});
+        sec += since(t0);
+      }
+      size_t surv = 0;
+      for (auto& sv : sels[on]) surv += sv.size();
+      printf("{\"op\": \"host_path.narrow\", \"keys\": \"%s\", \"narrow_keys\": %s, \"workers\": %u, \"insert_rows_per_s\": %.4g, "
+             "\"lookup_rows_per_s\": %.4g, \"pass_fraction\": %.4f, ",
+             ids ? "int64 below 2^32" : "int64 random 63-bit", on ? "true" : "false", workers, calls * double(n_build) / ins,
+             calls * double(n_probe) / sec, surv / double(n_probe));
+      print_stats("insert_phases_per_call", ins_stats, calls);
+      printf(", ");
+      print_stats("lookup_phases_per_call", ctx.stats, calls);
+      printf("}\n");
+      fflush(stdout);
+    }
+    if (words[0] != words[1] || sels[0] != sels[1]) {
+      fprintf(stderr, "narrow and plain results differ (%s)\n", ids ? "ids" : "random");
+      return 1;
+    }
+  }
+  return 0;
 }
 
 // The host -> device path of a DuckDB shim for JOB's INTEGER keys and for BIGINT keys:
@@ -401,6 +480,8 @@ int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "--host-path-trace") == 0) return host_path(dev, true);
   // --chain: UseBF::ExecuteBatch with 1..3 filters, pipelined chain vs filter by filter
   if (argc > 1 && std::strcmp(argv[1], "--chain") == 0) return host_chain(dev);
+  // --narrow: narrow BIGINT keys on / off
+  if (argc > 1 && std::strcmp(argv[1], "--narrow") == 0) return host_narrow(dev);
   // --create: only the CREATE_BF section
   if (argc > 1 && std::strcmp(argv[1], "--create") == 0) return create_bf(dev);
   // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
