@@ -276,65 +276,103 @@ struct Flattened {
   uint64_t n_chunks = 0;
 };
 
-// FLAT BIGINT keys src[0 .. count) -> their low words at lo; returns the OR of (key ^ v0) >> 32 (0: they all
-// share v0's high word). AVX2 where the host has it (runtime dispatch; the GPU box's EPYC does), SSE2 otherwise.
-__attribute__((target("avx2"))) uint64_t narrow_flat_avx2(const int64_t* src, uint64_t count, uint32_t* lo, uint64_t v0) {
-  const __m256i x = _mm256_set1_epi64x(static_cast<long long>(v0));
+// FLAT BIGINT keys src[0 .. count) -> their low words at lo; returns true when they all share one high word
+// (every bit of the high words equal: their OR equals their AND), which *hi then holds. One pass: the check
+// accumulates while the low words are stored. AVX-512 (vpmovqd) or AVX2 where the host has them (runtime
+// dispatch; the GPU box's EPYC 9575F has both), SSE2 otherwise.
+__attribute__((target("avx512f"))) bool narrow_flat_avx512(const int64_t* src, uint64_t count, uint32_t* lo, uint32_t* hi) {
+  __m512i o = _mm512_setzero_si512(), n = _mm512_set1_epi64(-1);
+  const bool aligned = (reinterpret_cast<uintptr_t>(lo) & 31) == 0;
+  uint64_t r = 0;
+  for (; r + 8 <= count; r += 8) {
+    const __m512i v = _mm512_loadu_si512(src + r);
+    o = _mm512_or_si512(o, v);
+    n = _mm512_and_si512(n, v);
+    const __m256i packed = _mm512_cvtepi64_epi32(v);  // the low dwords
+    if (aligned) _mm256_stream_si256(reinterpret_cast<__m256i*>(lo + r), packed);
+    else _mm256_storeu_si256(reinterpret_cast<__m256i*>(lo + r), packed);
+  }
+  uint64_t so = static_cast<uint64_t>(_mm512_reduce_or_epi64(o)), sn = static_cast<uint64_t>(_mm512_reduce_and_epi64(n));
+  for (; r < count; r++) {
+    const uint64_t k = static_cast<uint64_t>(src[r]);
+    so |= k;
+    sn &= k;
+    lo[r] = static_cast<uint32_t>(k);
+  }
+  if (aligned) _mm_sfence();
+  *hi = static_cast<uint32_t>(so >> 32);
+  return (so >> 32) == (sn >> 32);
+}
+
+__attribute__((target("avx2"))) bool narrow_flat_avx2(const int64_t* src, uint64_t count, uint32_t* lo, uint32_t* hi) {
   const __m256i even = _mm256_setr_epi32(0, 2, 4, 6, 1, 3, 5, 7);
-  __m256i acc = _mm256_setzero_si256();
+  __m256i o = _mm256_setzero_si256(), n = _mm256_set1_epi64x(-1);
   const bool aligned = (reinterpret_cast<uintptr_t>(lo) & 31) == 0;
   uint64_t r = 0;
   for (; r + 8 <= count; r += 8) {
     const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + r));
     const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + r + 4));
-    acc = _mm256_or_si256(acc, _mm256_or_si256(_mm256_srli_epi64(_mm256_xor_si256(a, x), 32),
-                                               _mm256_srli_epi64(_mm256_xor_si256(b, x), 32)));
+    o = _mm256_or_si256(o, _mm256_or_si256(a, b));
+    n = _mm256_and_si256(n, _mm256_and_si256(a, b));
     // low dwords of a into the low 128 bits, of b into the high 128 bits
-    const __m256i pa = _mm256_permutevar8x32_epi32(a, even), pb = _mm256_permutevar8x32_epi32(b, even);
-    const __m256i packed = _mm256_permute2x128_si256(pa, pb, 0x20);
+    const __m256i packed = _mm256_permute2x128_si256(_mm256_permutevar8x32_epi32(a, even),
+                                                     _mm256_permutevar8x32_epi32(b, even), 0x20);
     if (aligned) _mm256_stream_si256(reinterpret_cast<__m256i*>(lo + r), packed);
     else _mm256_storeu_si256(reinterpret_cast<__m256i*>(lo + r), packed);
   }
-  uint64_t tail = 0;
+  alignas(32) uint64_t ov[4], nv[4];
+  _mm256_store_si256(reinterpret_cast<__m256i*>(ov), o);
+  _mm256_store_si256(reinterpret_cast<__m256i*>(nv), n);
+  uint64_t so = ov[0] | ov[1] | ov[2] | ov[3], sn = nv[0] & nv[1] & nv[2] & nv[3];
   for (; r < count; r++) {
     const uint64_t k = static_cast<uint64_t>(src[r]);
-    tail |= (k ^ v0) >> 32;
+    so |= k;
+    sn &= k;
     lo[r] = static_cast<uint32_t>(k);
   }
   if (aligned) _mm_sfence();
-  alignas(32) uint64_t a4[4];
-  _mm256_store_si256(reinterpret_cast<__m256i*>(a4), acc);
-  return a4[0] | a4[1] | a4[2] | a4[3] | tail;
+  *hi = static_cast<uint32_t>(so >> 32);
+  return (so >> 32) == (sn >> 32);
 }
 
-uint64_t narrow_flat_sse2(const int64_t* src, uint64_t count, uint32_t* lo, uint64_t v0) {
-  const __m128i x = _mm_set1_epi64x(static_cast<long long>(v0));
-  __m128i acc = _mm_setzero_si128();
+bool narrow_flat_sse2(const int64_t* src, uint64_t count, uint32_t* lo, uint32_t* hi) {
+  __m128i o = _mm_setzero_si128(), n = _mm_set1_epi64x(-1);
   const bool aligned = (reinterpret_cast<uintptr_t>(lo) & 15) == 0;
   uint64_t r = 0;
   for (; r + 4 <= count; r += 4) {
     const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + r));
     const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + r + 2));
-    acc = _mm_or_si128(acc, _mm_or_si128(_mm_srli_epi64(_mm_xor_si128(a, x), 32), _mm_srli_epi64(_mm_xor_si128(b, x), 32)));
+    o = _mm_or_si128(o, _mm_or_si128(a, b));
+    n = _mm_and_si128(n, _mm_and_si128(a, b));
     // the low dwords of a and b -> one 16-B store
     const __m128i packed = _mm_unpacklo_epi64(_mm_shuffle_epi32(a, _MM_SHUFFLE(2, 0, 2, 0)),
                                               _mm_shuffle_epi32(b, _MM_SHUFFLE(2, 0, 2, 0)));
     if (aligned) _mm_stream_si128(reinterpret_cast<__m128i*>(lo + r), packed);
     else _mm_storeu_si128(reinterpret_cast<__m128i*>(lo + r), packed);
   }
-  uint64_t tail = 0;
+  alignas(16) uint64_t ov[2], nv[2];
+  _mm_store_si128(reinterpret_cast<__m128i*>(ov), o);
+  _mm_store_si128(reinterpret_cast<__m128i*>(nv), n);
+  uint64_t so = ov[0] | ov[1], sn = nv[0] & nv[1];
   for (; r < count; r++) {
     const uint64_t k = static_cast<uint64_t>(src[r]);
-    tail |= (k ^ v0) >> 32;
+    so |= k;
+    sn &= k;
     lo[r] = static_cast<uint32_t>(k);
   }
   if (aligned) _mm_sfence();
-  alignas(16) uint64_t a2[2];
-  _mm_store_si128(reinterpret_cast<__m128i*>(a2), acc);
-  return a2[0] | a2[1] | tail;
+  *hi = static_cast<uint32_t>(so >> 32);
+  return (so >> 32) == (sn >> 32);
 }
 
-const bool g_has_avx2 = __builtin_cpu_supports("avx2");
+// 2: AVX-512F, 1: AVX2, 0: SSE2 (cpu_init first: a static initializer may run before the runtime's)
+int simd_level() {
+  static const int level = [] {
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx512f") ? 2 : __builtin_cpu_supports("avx2") ? 1 : 0;
+  }();
+  return level;
+}
 
 // One chunk's BIGINT keys as their low 32-bit words at `lo` and the high word they all share in *hi, NULL rows
 // cleared in `valid_words` from bit row0 on (as flatten_column). False when the keys do not share their high word
@@ -345,9 +383,10 @@ bool narrow_column(const Vector& v, uint64_t count, uint32_t* lo, uint32_t* hi, 
   const int64_t* src = static_cast<const int64_t*>(v.data);
   switch (v.type) {
     case VectorType::FLAT: {
-      const uint64_t v0 = static_cast<uint64_t>(src[0]);
-      if ((g_has_avx2 ? narrow_flat_avx2(src, count, lo, v0) : narrow_flat_sse2(src, count, lo, v0)) != 0) return false;
-      *hi = static_cast<uint32_t>(v0 >> 32);
+      const int lvl = simd_level();
+      if (!(lvl == 2 ? narrow_flat_avx512(src, count, lo, hi)
+                     : lvl == 1 ? narrow_flat_avx2(src, count, lo, hi) : narrow_flat_sse2(src, count, lo, hi)))
+        return false;
       if (v.validity) {
         for (uint64_t q = 0; q < count; q += 64) {
           const uint32_t n = static_cast<uint32_t>(std::min<uint64_t>(64, count - q));
@@ -1853,9 +1892,10 @@ uint64_t UseBF::ExecuteChainPipelined(DeviceContext& ctx, const std::vector<cons
   // kNB stages in flight, stage i in buffer b = i % kNB: private slots 32.. (DeviceContext::kSlots) per buffer:
   // host / device 32 + b (the first column's keys), 35 + b (its validity), 38 + b / 41 + b (a later column's
   // gathered keys / validity); host 44 + b / 47 + b (the survivor lists, ping-pong), 50 + b (a later probe's sel),
-  // 53 + b (the count); device 50 + b (the probe's sel), 53 (the counts), 54 + b (the probe workspaces)
+  // 53 + b (the count); device 50 + b (the probe's sel), 53 (the counts), 54 + b (the probe workspaces); narrow
+  // BIGINT first columns: device 64 + b (low words), 67 + b and host 70 + b (the chunks' high words and first rows)
   constexpr int kNB = 3;
-  static_assert(kNB == DeviceContext::kAuxStreams + 1 && 57 <= DeviceContext::kSlots, "chain pipeline slots");
+  static_assert(kNB == DeviceContext::kAuxStreams + 1 && 73 <= DeviceContext::kSlots, "chain pipeline slots");
   const size_t words = (max_rows + 63) / 64 * 8;
   const size_t es0 = key_size(device_type(inputs[0]->data.at(cols_[act[0]]).key_type));
   void* d_keys[2][kNB];
@@ -1880,6 +1920,18 @@ uint64_t UseBF::ExecuteChainPipelined(DeviceContext& ctx, const std::vector<cons
     d_sel[b] = static_cast<uint32_t*>(ctx.dev(50 + b, std::max<size_t>(max_rows * 4, 4)));
     ws[b] = ctx.dev(54 + b, ws_bytes);
     cs[b] = static_cast<hipStream_t>(b == 0 ? ctx.stream() : ctx.aux_stream(b - 1));
+  }
+  bool narrow = ctx.narrow_keys && inputs[0]->data.at(cols_[act[0]]).key_type == KeyType::I64;  // until a stage is not
+  void* d_lo[kNB] = {};
+  void* d_meta[kNB] = {};
+  if (narrow) {
+    size_t max_chunks = 0;
+    for (const StageRange& r : st) max_chunks = std::max(max_chunks, r.c_hi - r.c_lo);
+    for (int b = 0; b < kNB; b++) {
+      d_lo[b] = ctx.dev(64 + b, std::max<size_t>(max_rows * 4, 16));
+      d_meta[b] = ctx.dev(67 + b, (2 * max_chunks + 1) * 4);
+      (void)ctx.host(70 + b, (2 * max_chunks + 1) * 4);
+    }
   }
   auto h = static_cast<hipStream_t>(ctx.h2d_stream());
   auto copied = [&](int b) { return static_cast<hipEvent_t>(ctx.event(b)); };
@@ -1987,11 +2039,13 @@ uint64_t UseBF::ExecuteChainPipelined(DeviceContext& ctx, const std::vector<cons
       ps.wait_copy_s += secs_since(t0);
       t0 = Clock::now();
       const Flattened f = flatten_pinned(ctx, inputs.data() + st[i].c_lo, st[i].c_hi - st[i].c_lo, cols_[act[0]],
-                                         st[i].rows, 32 + b, 35 + b);
+                                         st[i].rows, 32 + b, 35 + b, narrow ? 70 + b : -1);
+      narrow = f.narrow;
+      ps.narrow_stages += f.narrow;
       ps.flatten_s += secs_since(t0);
       t0 = Clock::now();
       if (i >= kNB) check_hip(hipStreamWaitEvent(h, probed(b), 0), "hipStreamWaitEvent");  // stage i - kNB read them
-      kc0[b] = copy_flattened(ctx, f, st[i].rows, d_keys[0][b], d_valid[0][b], h);
+      kc0[b] = copy_flattened(ctx, f, st[i].rows, d_keys[0][b], d_valid[0][b], h, d_lo[b], d_meta[b]);
       check_hip(hipEventRecord(copied(b), h), "hipEventRecord");
       check_hip(hipStreamWaitEvent(cs[b], copied(b), 0), "hipStreamWaitEvent");
       Chain& c = ch[b];

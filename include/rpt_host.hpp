@@ -92,8 +92,8 @@ class DeviceContext {
   void synchronize();  // every stream
 
   // internal: grow-on-demand buffers (host slots 16..31: UseBF::Execute's chained key columns; 32..63: the
-  // pipelined filter chain of UseBF::ExecuteBatch)
-  static constexpr int kSlots = 64;
+  // pipelined filter chain of UseBF::ExecuteBatch; 56..59 and 64..72: narrow BIGINT staging)
+  static constexpr int kSlots = 80;
   void* host(int slot, size_t bytes);
   void* dev(int slot, size_t bytes);
   // the device address of host slot `slot`'s pinned buffer (kernels read / write it in place), cached

@@ -710,6 +710,37 @@ static void narrow_keys(int dev) {
            "lookup: %llu of %llu stages narrow (narrow_keys %d)", (unsigned long long)ctx.stats.narrow_stages,
            (unsigned long long)ctx.stats.stages, on);
   }
+  // the pipelined chain's first column narrow too: f (column 0) then an INTEGER filter on column 1
+  {
+    rpt::DeviceContext ctx(dev);
+    ctx.pipeline_rows = 1u << 20;
+    ctx.flatten_threads = 4;
+    auto f0 = std::make_shared<rpt::PTBloomFilter>(), f1 = std::make_shared<rpt::PTBloomFilter>();
+    f0->Initialize(dev, static_cast<uint32_t>(nb));
+    f1->Initialize(dev, static_cast<uint32_t>(nb));
+    f0->InsertBatch(ctx, bptrs, {0});
+    f1->InsertBatch(ctx, bptrs, {1});
+    f0->finalized_ = f1->finalized_ = true;
+    const int lnb1 = f1->LogNumBlocks();
+    const std::vector<uint64_t> w1 = f1->ExportWords();
+    rpt::UseBF ub({f0, f1}, {0, 1});
+    std::vector<rpt::SelectionVector> outs;
+    ctx.stats = {};
+    const uint64_t got = ub.ExecuteBatch(ctx, pptrs, outs);
+    size_t bad = 0, total = 0;
+    for (size_t k = 0; k < pptrs.size(); k++) {
+      const size_t lo = 2048 * k, cnt = pptrs[k]->count;
+      const std::vector<uint64_t> vp = pack(pt.v1, lo, cnt);
+      rpt::SelectionVector s1(cnt), both;
+      s1.resize(rpt_oracle_probe_i32(w1.data(), lnb1, pt.c1.data() + lo, nullptr, vp.data(), cnt, s1.data()));
+      std::set_intersection(want[k].begin(), want[k].end(), s1.begin(), s1.end(), std::back_inserter(both));
+      total += both.size();
+      bad += outs[k] != both;
+    }
+    EXPECT(bad == 0 && got == total && ctx.stats.narrow_stages == ctx.stats.stages && ctx.stats.stages >= 3,
+           "narrow first column in the chain: %zu chunks differ, %llu of %llu stages narrow", bad,
+           (unsigned long long)ctx.stats.narrow_stages, (unsigned long long)ctx.stats.stages);
+  }
   // a batch whose chunks' keys straddle high words (BIGINT keys around 0: both signs in one chunk)
   {
     Table mt = make_table(np, 33, 0, 0);

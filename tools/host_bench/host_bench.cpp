@@ -267,20 +267,21 @@ int host_path(int dev, bool trace) {
 // columns: BIGINT 10% hits, INTEGER 50% hits, BIGINT 50% hits): the pipelined chain (4 Mi-row stages, 8 worker
 // threads) beside the filter-by-filter path (the whole batch per filter, pipeline_rows beyond the batch), both
 // checked equal.
-int host_chain(int dev) {
+int host_chain(int dev, bool ids) {
   const size_t n_build = 10000000, n_probe = 1ULL << 25;
   std::mt19937_64 rng(11);
+  const uint64_t m64 = ids ? 0xFFFFFFFFULL : ~0ULL;  // --chain-ids: BIGINT keys below 2^32 (narrow over PCIe)
   std::vector<int64_t> b0(n_build), b2(n_build), p0(n_probe), p2(n_probe);
   std::vector<int32_t> b1(n_build), p1(n_probe);
   for (size_t i = 0; i < n_build; i++) {
-    b0[i] = static_cast<int64_t>(rng() >> 1);
+    b0[i] = static_cast<int64_t>((rng() >> 1) & m64);
     b1[i] = static_cast<int32_t>(rng());
-    b2[i] = static_cast<int64_t>(rng() >> 1);
+    b2[i] = static_cast<int64_t>((rng() >> 1) & m64);
   }
   for (size_t i = 0; i < n_probe; i++) {
-    p0[i] = (rng() % 10 == 0) ? b0[rng() % n_build] : static_cast<int64_t>(rng() >> 1);
+    p0[i] = (rng() % 10 == 0) ? b0[rng() % n_build] : static_cast<int64_t>((rng() >> 1) & m64);
     p1[i] = (rng() % 2 == 0) ? b1[rng() % n_build] : static_cast<int32_t>(rng());
-    p2[i] = (rng() % 2 == 0) ? b2[rng() % n_build] : static_cast<int64_t>(rng() >> 1);
+    p2[i] = (rng() % 2 == 0) ? b2[rng() % n_build] : static_cast<int64_t>((rng() >> 1) & m64);
   }
   auto chunks = [](size_t n, const int64_t* c0, const int32_t* c1, const int64_t* c2) {
     std::vector<rpt::DataChunk> cs;
@@ -344,9 +345,10 @@ int host_chain(int dev) {
         fprintf(stderr, "chain of %zu: pipelined and filter-by-filter sels differ in %zu chunks\n", k, bad);
         return 1;
       }
-      printf("{\"op\": \"host_path.ExecuteBatch.chain\", \"filters\": %zu, \"chunks_per_call\": %zu, \"worker_threads\": 8, "
+      printf("{\"op\": \"host_path.ExecuteBatch.chain\", \"keys\": \"%s\", \"filters\": %zu, \"chunks_per_call\": %zu, \"worker_threads\": 8, "
              "\"pass_fraction\": %.4f, \"filter_by_filter_rows_per_s\": %.4g, \"pipelined_rows_per_s\": %.4g, \"pipeline_rows\": %llu, ",
-             k, pall.size(), surv / rows, calls * rows / sec_ref, calls * rows / sec, static_cast<unsigned long long>(stage));
+             ids ? "BIGINT below 2^32" : "BIGINT random 63-bit", k, pall.size(), surv / rows, calls * rows / sec_ref,
+             calls * rows / sec, static_cast<unsigned long long>(stage));
       print_stats("phases_per_call", ctx.stats, calls);
       printf("}\n");
       fflush(stdout);
@@ -479,7 +481,8 @@ int main(int argc, char** argv) {
   // calls 20 ms apart: the run to take under rocprofv3 --memory-copy-trace (copy-engine busy time per call)
   if (argc > 1 && std::strcmp(argv[1], "--host-path-trace") == 0) return host_path(dev, true);
   // --chain: UseBF::ExecuteBatch with 1..3 filters, pipelined chain vs filter by filter
-  if (argc > 1 && std::strcmp(argv[1], "--chain") == 0) return host_chain(dev);
+  if (argc > 1 && std::strcmp(argv[1], "--chain") == 0) return host_chain(dev, false);
+  if (argc > 1 && std::strcmp(argv[1], "--chain-ids") == 0) return host_chain(dev, true);
   // --narrow: narrow BIGINT keys on / off
   if (argc > 1 && std::strcmp(argv[1], "--narrow") == 0) return host_narrow(dev);
   // --create: only the CREATE_BF section
