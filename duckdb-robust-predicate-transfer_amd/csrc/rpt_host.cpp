@@ -376,7 +376,7 @@ int simd_level() {
 
 // One chunk's BIGINT keys as their low 32-bit words at `lo` and the high word they all share in *hi, NULL rows
 // cleared in `valid_words` from bit row0 on (as flatten_column). False when the keys do not share their high word
-// (or for SEQUENCE vectors); `lo` and the validity bits are then partly written and the caller re-flattens.
+// `lo` and the validity bits are then partly written and the caller re-flattens.
 bool narrow_column(const Vector& v, uint64_t count, uint32_t* lo, uint32_t* hi, uint64_t* valid_words, uint64_t row0,
                    bool& any_null) {
   if (v.key_type != KeyType::I64 || count == 0) return count == 0 && v.key_type == KeyType::I64;
@@ -428,6 +428,17 @@ bool narrow_column(const Vector& v, uint64_t count, uint32_t* lo, uint32_t* hi, 
           any_null |= nulls != 0;
           clear_bits(valid_words, row0 + q, nulls, n);
         }
+      }
+      if (acc != 0) return false;
+      *hi = static_cast<uint32_t>(v0 >> 32);
+      return true;
+    }
+    case VectorType::SEQUENCE: {  // start + r * increment in two's complement, never NULL
+      const uint64_t v0 = static_cast<uint64_t>(v.seq_start), inc = static_cast<uint64_t>(v.seq_increment);
+      uint64_t acc = 0, k = v0;
+      for (uint64_t r = 0; r < count; r++, k += inc) {
+        acc |= (k ^ v0) >> 32;
+        lo[r] = static_cast<uint32_t>(k);
       }
       if (acc != 0) return false;
       *hi = static_cast<uint32_t>(v0 >> 32);

@@ -770,9 +770,200 @@ static void narrow_keys(int dev) {
   }
 }
 
+// Randomized batches through every pipelined path: ragged chunks (0..2048 rows), FLAT / DICTIONARY / CONSTANT /
+// SEQUENCE vectors, NULLs at random rates, BIGINT keys in narrow and wide ranges, small stages (many per batch),
+// 1..8 workers, narrow_keys on / off; InsertBatch against the oracle's words, LookupSelBatch and UseBF::ExecuteBatch
+// chains of 1..3 filters against the oracle's per-row hits.
+struct FuzzCol {
+  std::vector<int64_t> v64;  // logical value per row (column 0)
+  std::vector<int32_t> v32;  // (column 1)
+  std::vector<bool> ok0, ok1;
+};
+static void fuzz_chunks(std::mt19937_64& rng, size_t n_chunks, bool narrow64, FuzzCol& fc, ChunkStore& st) {
+  for (size_t k = 0; k < n_chunks; k++) {
+    const size_t cnt = (rng() % 7 == 0) ? rng() % 3 : (rng() % 2 ? 2048 : 1 + rng() % 2048);
+    const size_t lo = fc.v64.size();
+    const uint64_t hi = narrow64 ? (rng() % 3 == 0 ? 0xFFFFFFFFULL : rng() % 4) : 0;
+    const int null_rate = static_cast<int>(rng() % 4);  // 0: none, else 1 in (8 << rate)
+    rpt::DataChunk ch;
+    ch.count = cnt;
+    ch.data.resize(2);
+    for (int c = 0; c < 2; c++) {
+      const int shape = static_cast<int>(rng() % 6);  // 0-2 FLAT, 3 DICTIONARY, 4 CONSTANT, 5 SEQUENCE
+      rpt::Vector x;
+      x.key_type = c == 0 ? rpt::KeyType::I64 : rpt::KeyType::I32;
+      std::vector<int64_t> vals(cnt);
+      std::vector<bool> valid(cnt, true);
+      auto draw = [&]() -> int64_t {
+        const uint64_t r = rng() % 60000;
+        if (c == 1) return static_cast<int64_t>(static_cast<int32_t>(r) - 30000);
+        return narrow64 ? static_cast<int64_t>((hi << 32) | r) : static_cast<int64_t>(r * 0x9E3779B97F4A7C15ULL);
+      };
+      if (shape == 5 && cnt) {  // SEQUENCE: never NULL
+        x.type = rpt::VectorType::SEQUENCE;
+        x.seq_start = c == 0 ? static_cast<int64_t>((hi << 32) | (rng() % 50000)) : static_cast<int64_t>(rng() % 50000) - 25000;
+        x.seq_increment = static_cast<int64_t>(rng() % 5);
+        for (size_t i = 0; i < cnt; i++) {
+          const uint64_t v = static_cast<uint64_t>(x.seq_start) + static_cast<uint64_t>(x.seq_increment) * i;
+          vals[i] = c == 0 ? static_cast<int64_t>(v) : static_cast<int64_t>(static_cast<int32_t>(v));
+        }
+      } else if (shape == 4 && cnt) {  // CONSTANT
+        x.type = rpt::VectorType::CONSTANT;
+        const int64_t v = draw();
+        const bool ok = null_rate == 0 || rng() % 4 != 0;
+        for (size_t i = 0; i < cnt; i++) {
+          vals[i] = v;
+          valid[i] = ok;
+        }
+        if (c == 0) st.i64.push_back({v});
+        else st.i32.push_back({static_cast<int32_t>(v)});
+        st.valid.push_back({ok ? 1ULL : 0ULL});
+        x.data = c == 0 ? static_cast<const void*>(st.i64.back().data()) : static_cast<const void*>(st.i32.back().data());
+        x.validity = st.valid.back().data();
+      } else if (shape == 3 && cnt) {  // DICTIONARY over a small dictionary with NULL entries
+        x.type = rpt::VectorType::DICTIONARY;
+        const size_t nd = 1 + rng() % 300;
+        std::vector<int64_t> dict(nd);
+        std::vector<uint64_t> dv((nd + 63) / 64 + 1, ~0ULL);
+        for (size_t d = 0; d < nd; d++) {
+          dict[d] = draw();
+          if (null_rate && rng() % (8u << null_rate) == 0) dv[d / 64] &= ~(1ULL << (d % 64));
+        }
+        std::vector<uint32_t> sel(cnt);
+        for (size_t i = 0; i < cnt; i++) {
+          sel[i] = static_cast<uint32_t>(rng() % nd);
+          vals[i] = dict[sel[i]];
+          valid[i] = (dv[sel[i] / 64] >> (sel[i] % 64)) & 1;
+        }
+        if (c == 0) st.i64.push_back(dict);
+        else st.i32.push_back(std::vector<int32_t>(dict.begin(), dict.end()));
+        st.sel.push_back(std::move(sel));
+        st.valid.push_back(std::move(dv));
+        x.data = c == 0 ? static_cast<const void*>(st.i64.back().data()) : static_cast<const void*>(st.i32.back().data());
+        x.sel = st.sel.back().data();
+        x.dict_size = nd;
+        x.validity = st.valid.back().data();
+      } else {  // FLAT (also every empty chunk)
+        x.type = rpt::VectorType::FLAT;
+        std::vector<uint64_t> vw((cnt + 63) / 64 + 1, ~0ULL);
+        for (size_t i = 0; i < cnt; i++) {
+          vals[i] = draw();
+          if (null_rate && rng() % (8u << null_rate) == 0) {
+            valid[i] = false;
+            vw[i / 64] &= ~(1ULL << (i % 64));
+          }
+        }
+        if (c == 0) st.i64.push_back(vals);
+        else st.i32.push_back(std::vector<int32_t>(vals.begin(), vals.end()));
+        st.valid.push_back(std::move(vw));
+        x.data = c == 0 ? static_cast<const void*>(st.i64.back().data()) : static_cast<const void*>(st.i32.back().data());
+        x.validity = null_rate ? st.valid.back().data() : nullptr;
+      }
+      ch.data[c] = x;
+      for (size_t i = 0; i < cnt; i++) {
+        if (c == 0) {
+          fc.v64.push_back(vals[i]);
+          fc.ok0.push_back(valid[i]);
+        } else {
+          fc.v32.push_back(static_cast<int32_t>(vals[i]));
+          fc.ok1.push_back(valid[i]);
+        }
+      }
+    }
+    (void)lo;
+    st.chunks.push_back(std::move(ch));
+  }
+}
+
+static std::vector<uint64_t> pack_all(const std::vector<bool>& v) { return pack(v, 0, v.size()); }
+
+static void fuzz_pipelines(int dev) {
+  std::mt19937_64 rng(2026);
+  uint64_t stages = 0, narrow = 0;
+  const int iters = 30;
+  for (int it = 0; it < iters; it++) {
+    const bool narrow64 = rng() % 2;
+    FuzzCol bc, pc;
+    ChunkStore bst, pst;
+    fuzz_chunks(rng, 150 + rng() % 100, narrow64, bc, bst);
+    fuzz_chunks(rng, 200 + rng() % 150, narrow64, pc, pst);
+    std::vector<const rpt::DataChunk*> bptrs, pptrs;
+    for (const auto& ch : bst.chunks) bptrs.push_back(&ch);
+    for (const auto& ch : pst.chunks) pptrs.push_back(&ch);
+    const size_t nb = bc.v64.size(), np = pc.v64.size();
+    rpt::DeviceContext ctx(dev);
+    ctx.pipeline_rows = 1ULL << (15 + rng() % 3);
+    ctx.flatten_threads = 1 + static_cast<unsigned>(rng() % 8);
+    ctx.narrow_keys = rng() % 4 != 0;
+    const int lnb = rpt_oracle_log_num_blocks(nb);
+    std::vector<uint64_t> w0(1ULL << lnb, 0), w1(1ULL << lnb, 0);
+    const std::vector<uint64_t> vb0 = pack_all(bc.ok0), vb1 = pack_all(bc.ok1);
+    rpt_oracle_insert_i64(w0.data(), lnb, bc.v64.data(), nullptr, vb0.data(), nb);
+    rpt_oracle_insert_i32(w1.data(), lnb, bc.v32.data(), nullptr, vb1.data(), nb);
+    auto f0 = std::make_shared<rpt::PTBloomFilter>(), f1 = std::make_shared<rpt::PTBloomFilter>();
+    f0->Initialize(dev, static_cast<uint32_t>(nb));
+    f1->Initialize(dev, static_cast<uint32_t>(nb));
+    f0->InsertBatch(ctx, bptrs, {0});
+    f1->InsertBatch(ctx, bptrs, {1});
+    EXPECT(f0->ExportWords() == w0 && f1->ExportWords() == w1, "fuzz %d: pipelined insert words differ", it);
+    f0->finalized_ = f1->finalized_ = true;
+    // per-row hits of each filter
+    std::vector<uint32_t> s0(np), s1(np);
+    const std::vector<uint64_t> vp0 = pack_all(pc.ok0), vp1 = pack_all(pc.ok1);
+    s0.resize(rpt_oracle_probe_i64(w0.data(), lnb, pc.v64.data(), nullptr, vp0.data(), np, s0.data()));
+    s1.resize(rpt_oracle_probe_i32(w1.data(), lnb, pc.v32.data(), nullptr, vp1.data(), np, s1.data()));
+    std::vector<uint8_t> h0(np, 0), h1(np, 0);
+    for (uint32_t r : s0) h0[r] = 1;
+    for (uint32_t r : s1) h1[r] = 1;
+    struct Case { std::vector<int> order; };
+    const Case cases[] = {{{0}}, {{1}}, {{0, 1}}, {{1, 0}}, {{0, 1, 0}}};
+    ctx.stats = {};
+    for (const Case& cs : cases) {
+      std::vector<rpt::SelectionVector> want(pptrs.size());
+      size_t row = 0, total = 0;
+      for (size_t k = 0; k < pptrs.size(); k++) {
+        for (size_t r = 0; r < pptrs[k]->count; r++, row++) {
+          bool pass = true;
+          for (int f : cs.order) pass = pass && (f == 0 ? h0[row] : h1[row]);
+          if (pass) want[k].push_back(static_cast<uint32_t>(r));
+        }
+        total += want[k].size();
+      }
+      std::vector<std::shared_ptr<rpt::PTBloomFilter>> fs;
+      std::vector<uint64_t> cols;
+      for (int f : cs.order) {
+        fs.push_back(f == 0 ? f0 : f1);
+        cols.push_back(static_cast<uint64_t>(f));
+      }
+      rpt::UseBF ub(fs, cols);
+      std::vector<rpt::SelectionVector> outs;
+      const uint64_t got = ub.ExecuteBatch(ctx, pptrs, outs);
+      size_t bad = 0;
+      for (size_t k = 0; k < pptrs.size(); k++) bad += outs[k] != want[k];
+      EXPECT(bad == 0 && got == total, "fuzz %d (narrow64 %d, stage %llu, workers %u, narrow_keys %d), chain of %zu: %zu chunks differ",
+             it, narrow64 ? 1 : 0, (unsigned long long)ctx.pipeline_rows, ctx.flatten_threads, ctx.narrow_keys ? 1 : 0,
+             cs.order.size(), bad);
+      if (cs.order.size() == 1) {
+        std::vector<rpt::SelectionVector> sels;
+        fs[0]->LookupSelBatch(ctx, pptrs, sels, {cols[0]});
+        size_t bad2 = 0;
+        for (size_t k = 0; k < pptrs.size(); k++) bad2 += sels[k] != want[k];
+        EXPECT(bad2 == 0, "fuzz %d: LookupSelBatch on column %llu: %zu chunks differ", it, (unsigned long long)cols[0], bad2);
+      }
+    }
+    stages += ctx.stats.stages;
+    narrow += ctx.stats.narrow_stages;
+  }
+  printf("fuzz: %d batches, %llu pipelined stages, %llu of them narrow\n", iters, (unsigned long long)stages,
+         (unsigned long long)narrow);
+  EXPECT(stages > 100 && narrow > 10, "the fuzz reached the pipelines (%llu stages, %llu narrow)", (unsigned long long)stages,
+         (unsigned long long)narrow);
+}
+
 int main() {
   try {
     const int dev = 0;
+    fuzz_pipelines(dev);
     narrow_keys(dev);
     pinned_cache(dev);
     pipelined_workers(dev);
