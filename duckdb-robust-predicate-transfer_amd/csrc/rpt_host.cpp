@@ -375,7 +375,7 @@ int simd_level() {
 }
 
 // One chunk's BIGINT keys as their low 32-bit words at `lo` and the high word they all share in *hi, NULL rows
-// cleared in `valid_words` from bit row0 on (as flatten_column). False when the keys do not share their high word
+// cleared in `valid_words` from bit row0 on (as flatten_column). False when the keys do not share their high word:
 // `lo` and the validity bits are then partly written and the caller re-flattens.
 bool narrow_column(const Vector& v, uint64_t count, uint32_t* lo, uint32_t* hi, uint64_t* valid_words, uint64_t row0,
                    bool& any_null) {
