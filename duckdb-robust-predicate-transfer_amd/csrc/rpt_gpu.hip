@@ -1344,7 +1344,7 @@ int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, ui
 // fused selection-vector tail instead of the result bits, and *done is set: phase 2 is skipped.
 static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
                              void* workspace, size_t workspace_bytes, rpt_stream_t stream, uint32_t* out_sel,
-                             uint64_t* out_count_dev, bool* done) {
+                             uint64_t* out_count_dev, bool* done, uint64_t* bits_out = nullptr) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
   if (n >= (1ULL << 32)) return fail(RPT_ERR_INVALID_ARGUMENT, "n=%llu rows exceeds uint32 sel_t", (unsigned long long)n);
   if (n == 0) return RPT_OK;
@@ -1360,6 +1360,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
   RPT_ON_DEVICE(bf->device);
   ProbeWorkspace ws;
   workspace_layout(n, L, strategy, workspace, &ws);
+  if (bits_out) ws.bits = bits_out;  // rpt_bf_probe_bits: the result bits go to the caller's buffer
   hipStream_t s = as_stream(stream);
   RPT_SETTLE(bf, s);
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
@@ -1488,6 +1489,13 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
                         void* workspace, size_t workspace_bytes, rpt_stream_t stream) {
   bool done = false;
   return probe_phase1_impl(bf, col, row_sel, n, workspace, workspace_bytes, stream, nullptr, nullptr, &done);
+}
+
+int rpt_bf_probe_bits(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
+                      uint64_t* out_bits, void* workspace, size_t workspace_bytes, rpt_stream_t stream) {
+  if (!bf || !out_bits) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  bool done = false;
+  return probe_phase1_impl(bf, col, row_sel, n, workspace, workspace_bytes, stream, nullptr, nullptr, &done, out_bits);
 }
 
 int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, uint32_t* out_sel,

@@ -4,7 +4,7 @@
 
 #include <hip/hip_runtime_api.h>
 #include <emmintrin.h>  // SSE2 streaming stores (x86-64 baseline) for the pinned staging copies
-#include <immintrin.h>  // AVX2 (runtime-dispatched) for the narrow-key packing
+#include <immintrin.h>  // AVX-512 / AVX2 paths (runtime-dispatched): narrow-key packing, bit expansion
 
 #include <algorithm>
 #include <chrono>
@@ -708,6 +708,88 @@ void split_sel(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, 
   const size_t n_tasks = std::min<size_t>(n_chunks / 16, 4 * static_cast<size_t>(ctx.flatten_threads));
   ctx.parallel_for(n_tasks, [&](size_t t) { range(n_chunks * t / n_tasks, n_chunks * (t + 1) / n_tasks); });
 }
+
+// The set bits of x as base + bit index into tmp (room for 64 + 16), their count returned: AVX-512 compress where
+// the host has it, else branchless (every bit writes, the cursor moves by the bit). For the dense words of a high
+// pass fraction, where a ctz loop's branch on every survivor mispredicts.
+__attribute__((target("avx512f"))) uint32_t expand_word_avx512(uint64_t x, uint32_t base, uint32_t* tmp) {
+  const __m512i iota = _mm512_setr_epi32(0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15);
+  uint32_t k = 0;
+  for (int q = 0; q < 4; q++) {
+    const __mmask16 m = static_cast<__mmask16>(x >> (16 * q));
+    const __m512i idx = _mm512_add_epi32(iota, _mm512_set1_epi32(static_cast<int>(base + 16 * q)));
+    _mm512_storeu_si512(tmp + k, _mm512_maskz_compress_epi32(m, idx));
+    k += static_cast<uint32_t>(__builtin_popcount(static_cast<uint32_t>(m)));
+  }
+  return k;
+}
+uint32_t expand_word_scalar(uint64_t x, uint32_t base, uint32_t* tmp) {
+  uint32_t k = 0;
+  for (uint32_t j = 0; j < 64; j++) {
+    tmp[k] = base + j;
+    k += static_cast<uint32_t>((x >> j) & 1);
+  }
+  return k;
+}
+bool host_has_avx512() {
+  static const bool v = [] {
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx512f") != 0;
+  }();
+  return v;
+}
+
+// A stage's result bits (bit r = stage row r passes) -> per-chunk sels (ids relative to each chunk), over the
+// context's worker threads: each chunk's rows are one bit range.
+void split_bits(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, size_t c_lo, size_t c_hi,
+                const uint64_t* h_bits, std::vector<SelectionVector>& sels) {
+  const size_t n_chunks = c_hi - c_lo;
+  std::vector<uint64_t> start(n_chunks + 1, 0);
+  for (size_t c = 0; c < n_chunks; c++) start[c + 1] = start[c] + chunks[c_lo + c]->count;
+  auto word = [&](uint64_t w, uint64_t r, uint64_t e) {  // bits of word w inside rows [r, e)
+    uint64_t x = h_bits[w];
+    const uint64_t lo = w << 6;
+    if (lo < r) x &= ~0ULL << (r - lo);
+    if (e - lo < 64) x &= (1ULL << (e - lo)) - 1;
+    return x;
+  };
+  const bool avx512 = host_has_avx512();
+  auto range = [&](size_t lo_c, size_t hi_c) {
+    for (size_t c = lo_c; c < hi_c; c++) {
+      const uint64_t r = start[c], e = start[c + 1];
+      SelectionVector& out = sels[c_lo + c];
+      if (r == e) {
+        out.clear();
+        continue;
+      }
+      size_t cnt = 0;
+      for (uint64_t w = r >> 6; (w << 6) < e; w++) cnt += static_cast<size_t>(__builtin_popcountll(word(w, r, e)));
+      out.resize(cnt);
+      size_t k = 0;
+      alignas(64) uint32_t tmp[64 + 16];
+      for (uint64_t w = r >> 6; (w << 6) < e; w++) {
+        uint64_t x = word(w, r, e);
+        const uint32_t base = static_cast<uint32_t>((w << 6) - r);  // wraps below r: the sums do not
+        if (__builtin_popcountll(x) > 12) {  // dense word
+          const uint32_t m = avx512 ? expand_word_avx512(x, base, tmp) : expand_word_scalar(x, base, tmp);
+          std::memcpy(out.data() + k, tmp, m * 4);
+          k += m;
+        } else {
+          while (x) {
+            out[k++] = base + static_cast<uint32_t>(__builtin_ctzll(x));
+            x &= x - 1;
+          }
+        }
+      }
+    }
+  };
+  if (start[n_chunks] < (1u << 16) || n_chunks < 64 || ctx.flatten_threads <= 1) {
+    range(0, n_chunks);
+  } else {
+    const size_t n_tasks = std::min<size_t>(n_chunks / 16, 4 * static_cast<size_t>(ctx.flatten_threads));
+    ctx.parallel_for(n_tasks, [&](size_t t) { range(n_chunks * t / n_tasks, n_chunks * (t + 1) / n_tasks); });
+  }
+}
 }  // namespace
 
 // Persistent worker threads of a DeviceContext (parallel_for): workers sleep on a condition variable
@@ -1262,6 +1344,16 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
   auto s = static_cast<hipStream_t>(ctx.stream());
   auto d = static_cast<hipStream_t>(ctx.copy_stream());
   auto h = static_cast<hipStream_t>(ctx.h2d_stream());
+  // bits_back: each stage's result bits come back (rows / 8 bytes, no count round trip) and the workers turn them
+  // into the chunks' sels; else the survivors' sel (4 B each) after its count. Device / host slots 60 + b.
+  const bool bits = ctx.bits_back;
+  const size_t bits_bytes = (max_rows + 511) / 512 * 64;
+  uint64_t* d_bits[2] = {nullptr, nullptr};
+  uint64_t* h_bits[2] = {nullptr, nullptr};
+  for (int b = 0; bits && b < 2; b++) {
+    d_bits[b] = static_cast<uint64_t*>(ctx.dev(60 + b, bits_bytes));
+    h_bits[b] = static_cast<uint64_t*>(ctx.host(60 + b, bits_bytes));
+  }
   uint64_t counts[2] = {0, 0};
   auto count_arrived = [&](size_t j) {  // stage j's count is on the host: copy its sel back exactly
     const int b = static_cast<int>(j & 1);
@@ -1281,7 +1373,8 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
     check_hip(hipEventSynchronize(pb.returned(b)), "hipEventSynchronize");
     ps.wait_sel_s += secs_since(t0);
     t0 = Clock::now();
-    split_sel(ctx, chunks, st[j].c_lo, st[j].c_hi, pb.h_sel[b], counts[b], sels);
+    if (bits) split_bits(ctx, chunks, st[j].c_lo, st[j].c_hi, h_bits[b], sels);
+    else split_sel(ctx, chunks, st[j].c_lo, st[j].c_hi, pb.h_sel[b], counts[b], sels);
     ps.split_s += secs_since(t0);
   };
   try {
@@ -1303,15 +1396,24 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
       check_hip(hipEventRecord(pb.copied(b), h), "hipEventRecord");
       check_hip(hipStreamWaitEvent(s, pb.copied(b), 0), "hipStreamWaitEvent");
       if (i >= 2) check_hip(hipStreamWaitEvent(s, pb.returned(b), 0), "hipStreamWaitEvent");  // d_sel[b] free
-      check(rpt_bf_probe(bf_, &kc, nullptr, st[i].rows, pb.d_sel[b], pb.d_cnt[b], ws, ws_bytes, s));
-      check_hip(hipMemcpyAsync(pb.h_cnt[b], pb.d_cnt[b], 8, hipMemcpyDeviceToHost, s), "copy count");
+      if (bits) {
+        check(rpt_bf_probe_bits(bf_, &kc, nullptr, st[i].rows, d_bits[b], ws, ws_bytes, s));
+      } else {
+        check(rpt_bf_probe(bf_, &kc, nullptr, st[i].rows, pb.d_sel[b], pb.d_cnt[b], ws, ws_bytes, s));
+        check_hip(hipMemcpyAsync(pb.h_cnt[b], pb.d_cnt[b], 8, hipMemcpyDeviceToHost, s), "copy count");
+      }
       check_hip(hipEventRecord(pb.probed(b), s), "hipEventRecord");
       ps.enqueue_s += secs_since(t0);
-      if (i >= 1) count_arrived(i - 1);
-      if (i >= 2) split(i - 2);
+      if (!bits && i >= 1) count_arrived(i - 1);
+      if (i >= 2) split(i - 2);  // frees h_bits[b] / h_sel[b] for stage i
+      if (bits) {  // stage i's bits back as soon as its probe is done
+        check_hip(hipStreamWaitEvent(d, pb.probed(b), 0), "hipStreamWaitEvent");
+        check_hip(hipMemcpyAsync(h_bits[b], d_bits[b], (st[i].rows + 511) / 512 * 64, hipMemcpyDeviceToHost, d), "copy bits");
+        check_hip(hipEventRecord(pb.returned(b), d), "hipEventRecord");
+      }
     }
     const size_t n = st.size();
-    count_arrived(n - 1);
+    if (!bits) count_arrived(n - 1);
     if (n >= 2) split(n - 2);
     split(n - 1);
   } catch (...) {

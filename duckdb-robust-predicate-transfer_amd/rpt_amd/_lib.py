@@ -123,6 +123,7 @@ SIGNATURES = {
     "rpt_hash_keys": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_hash_combine": (c_int, [POINTER(KeyColumn), c_uint64, c_void_p, c_void_p]),
     "rpt_keys_widen": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_void_p]),
+    "rpt_bf_probe_bits": (c_int, [c_void_p, POINTER(KeyColumn), c_void_p, c_uint64, c_void_p, c_void_p, c_size_t, c_void_p]),
     "rpt_bf_merge_or": (c_int, [c_void_p, c_void_p, c_void_p]),
     "rpt_bf_allreduce_or": (c_int, [c_void_p, c_void_p, c_void_p]),
     "rpt_bf_allreduce_or_ws": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

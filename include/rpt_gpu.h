@@ -238,6 +238,13 @@ int rpt_bf_probe_phase1(const rpt_bf* bf, const rpt_key_column* col, const uint3
                         void* workspace, size_t workspace_bytes, rpt_stream_t stream);
 int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, uint32_t* out_sel,
                         uint64_t* out_count_dev, void* workspace, size_t workspace_bytes, rpt_stream_t stream);
+/* rpt_bf_probe's result as bits instead of a selection vector: bit i (LSB-first in uint64 words) of out_bits = the
+ * i-th probed row (row i, or row_sel[i]) passes; out_bits (device memory) holds ceil(n/512)*8 words, bits past n
+ * are 0. Same strategies and workspace (rpt_bf_probe_workspace_bytes) as rpt_bf_probe; stream-ordered, no sync. A
+ * host-resident caller copies n/8 bytes back instead of 4 bytes per survivor (the C++ host mirror's pipelined
+ * lookups do, DeviceContext::bits_back). */
+int rpt_bf_probe_bits(const rpt_bf* bf, const rpt_key_column* col, const uint32_t* row_sel, uint64_t n,
+                      uint64_t* out_bits, void* workspace, size_t workspace_bytes, rpt_stream_t stream);
 /* Arrow BlockedBloomFilter::Find(…, result_bit_vector) shape: bit i (LSB-first in uint64 words) of
  * out_bits = row i passes. out_bits must hold ceil(n/512)*8 words. */
 int rpt_bf_find_bits(const rpt_bf* bf, const rpt_key_column* col, uint64_t n, uint64_t* out_bits,

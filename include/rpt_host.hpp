@@ -126,6 +126,9 @@ class DeviceContext {
   // window) cross PCIe as 4-B low words and are widened on the device (rpt_keys_widen): half the bytes of the
   // shim's bound. A stage that does not qualify is flattened as 8-B keys and the rest of the batch stays plain.
   bool narrow_keys = true;
+  // Pipelined lookups bring each stage's result bits back (rows / 8 bytes; rpt_bf_probe_bits) and the workers
+  // expand them into the chunks' sels, instead of copying the survivors' sel (4 B each) after a count round trip.
+  bool bits_back = true;
 
   // Host-side time of the pipelined batch paths by phase (accumulated; reset by assigning {}): where a
   // host-resident batch's time goes (tools/host_bench reports it).

@@ -442,14 +442,16 @@ static void pipelined_workers(int dev) {
     }
     EXPECT(total > (1u << 17), "column %d: %zu survivors (the split must run on the workers)", c, total);
     std::vector<rpt::SelectionVector> sels;
-    for (int rep = 0; rep < 2; rep++) {  // the second call reuses the vectors the first one filled
+    for (int rep = 0; rep < 3; rep++) {  // the second call reuses the vectors the first one filled; the third copies sels back
       ctx.stats = {};
+      ctx.bits_back = rep < 2;
       f->LookupSelBatch(ctx, pptrs, sels, {static_cast<uint64_t>(c)});
       EXPECT(sels.size() == pptrs.size() && ctx.stats.stages >= 3 && ctx.stats.rows == np, "pipeline stats (column %d)", c);
       size_t bad = 0;
       for (size_t k = 0; k < pptrs.size(); k++) bad += sels[k] != want[k];
       EXPECT(bad == 0, "worker-thread pipelined lookup (column %d, call %d): %zu chunks differ", c, rep, bad);
     }
+    ctx.bits_back = true;
     rpt::UseBF ub({f}, {static_cast<uint64_t>(c)});
     std::vector<rpt::SelectionVector> outs(5, rpt::SelectionVector(7, 9));  // stale contents must not leak
     const uint64_t got = ub.ExecuteBatch(ctx, pptrs, outs);
@@ -772,7 +774,7 @@ static void narrow_keys(int dev) {
 
 // Randomized batches through every pipelined path: ragged chunks (0..2048 rows), FLAT / DICTIONARY / CONSTANT /
 // SEQUENCE vectors, NULLs at random rates, BIGINT keys in narrow and wide ranges, small stages (many per batch),
-// 1..8 workers, narrow_keys on / off; InsertBatch against the oracle's words, LookupSelBatch and UseBF::ExecuteBatch
+// 1..8 workers, narrow_keys and bits_back on / off; InsertBatch against the oracle's words, LookupSelBatch and UseBF::ExecuteBatch
 // chains of 1..3 filters against the oracle's per-row hits.
 struct FuzzCol {
   std::vector<int64_t> v64;  // logical value per row (column 0)
@@ -895,6 +897,7 @@ static void fuzz_pipelines(int dev) {
     ctx.pipeline_rows = 1ULL << (15 + rng() % 3);
     ctx.flatten_threads = 1 + static_cast<unsigned>(rng() % 8);
     ctx.narrow_keys = rng() % 4 != 0;
+    ctx.bits_back = rng() % 3 != 0;
     const int lnb = rpt_oracle_log_num_blocks(nb);
     std::vector<uint64_t> w0(1ULL << lnb, 0), w1(1ULL << lnb, 0);
     const std::vector<uint64_t> vb0 = pack_all(bc.ok0), vb1 = pack_all(bc.ok1);

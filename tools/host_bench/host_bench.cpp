@@ -108,6 +108,75 @@ int host_narrow(int dev) {
   return 0;
 }
 
+// Result bits back instead of sels (DeviceContext::bits_back): LookupSelBatch (2^25 rows, 4 Mi-row stages, 8
+// workers) of BIGINT and INTEGER keys against C2's filter at pass fractions 0.1 / 0.5 / 0.9, on / off, compared.
+int host_bits(int dev) {
+  const size_t n_build = 10000000, n_probe = 1ULL << 25;
+  std::mt19937_64 rng(23);
+  std::vector<int64_t> b(n_build);
+  for (auto& k : b) k = static_cast<int64_t>(rng() >> 1);
+  std::vector<int32_t> b32(n_build);
+  for (size_t i = 0; i < n_build; i++) b32[i] = static_cast<int32_t>(b[i]);
+  for (int i32 = 0; i32 < 2; i32++) {
+    auto chunks = [&](size_t n, const void* data) {
+      std::vector<rpt::DataChunk> cs;
+      for (size_t lo = 0; lo < n; lo += 2048) {
+        rpt::DataChunk c;
+        c.count = std::min<size_t>(2048, n - lo);
+        rpt::Vector x;
+        x.key_type = i32 ? rpt::KeyType::I32 : rpt::KeyType::I64;
+        x.data = i32 ? static_cast<const void*>(static_cast<const int32_t*>(data) + lo)
+                     : static_cast<const void*>(static_cast<const int64_t*>(data) + lo);
+        c.data.push_back(x);
+        cs.push_back(c);
+      }
+      return cs;
+    };
+    auto bch = chunks(n_build, i32 ? static_cast<const void*>(b32.data()) : static_cast<const void*>(b.data()));
+    std::vector<const rpt::DataChunk*> ball;
+    for (auto& c : bch) ball.push_back(&c);
+    rpt::DeviceContext ctx(dev);
+    rpt::PTBloomFilter bf;
+    bf.Initialize(dev, static_cast<uint32_t>(n_build));
+    bf.InsertBatch(ctx, ball, {0});
+    bf.finalized_ = true;
+    for (int pct : {10, 50, 90}) {
+      std::vector<int64_t> q(n_probe);
+      for (size_t i = 0; i < n_probe; i++) q[i] = (rng() % 100 < static_cast<uint64_t>(pct)) ? b[rng() % n_build] : static_cast<int64_t>(rng() >> 1);
+      std::vector<int32_t> q32(i32 ? n_probe : 0);
+      for (size_t i = 0; i < q32.size(); i++) q32[i] = static_cast<int32_t>(q[i]);
+      auto pch = chunks(n_probe, i32 ? static_cast<const void*>(q32.data()) : static_cast<const void*>(q.data()));
+      std::vector<const rpt::DataChunk*> pall;
+      for (auto& c : pch) pall.push_back(&c);
+      std::vector<rpt::SelectionVector> sels[2];
+      for (int on : {0, 1}) {
+        ctx.bits_back = on != 0;
+        bf.LookupSelBatch(ctx, pall, sels[on], {0});  // warm-up
+        ctx.stats = {};
+        const int calls = 4;
+        double sec = 0;
+        for (int c = 0; c < calls; c++) {
+          const auto t0 = clk::now();
+          bf.LookupSelBatch(ctx, pall, sels[on], {0});
+          sec += since(t0);
+        }
+        size_t surv = 0;
+        for (auto& sv : sels[on]) surv += sv.size();
+        printf("{\"op\": \"host_path.bits_back\", \"keys\": \"%s\", \"bits_back\": %s, \"lookup_rows_per_s\": %.4g, \"pass_fraction\": %.4f, ",
+               i32 ? "int32" : "int64", on ? "true" : "false", calls * double(n_probe) / sec, surv / double(n_probe));
+        print_stats("phases_per_call", ctx.stats, calls);
+        printf("}\n");
+        fflush(stdout);
+      }
+      if (sels[0] != sels[1]) {
+        fprintf(stderr, "bits_back on / off differ\n");
+        return 1;
+      }
+    }
+  }
+  return 0;
+}
+
 // The host -> device path of a DuckDB shim for JOB's INTEGER keys and for BIGINT keys:
 // FLAT int64, FLAT int32 and DICTIONARY int32 2048-row chunks through LookupSelBatch's pipeline (4 Mi-row
 // stages) with 1..16 worker threads per call, the host-side time of each phase per call (DeviceContext::
@@ -485,6 +554,8 @@ int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "--chain-ids") == 0) return host_chain(dev, true);
   // --narrow: narrow BIGINT keys on / off
   if (argc > 1 && std::strcmp(argv[1], "--narrow") == 0) return host_narrow(dev);
+  // --bits: result bits back vs sels back at pass fractions 0.1 / 0.5 / 0.9
+  if (argc > 1 && std::strcmp(argv[1], "--bits") == 0) return host_bits(dev);
   // --create: only the CREATE_BF section
   if (argc > 1 && std::strcmp(argv[1], "--create") == 0) return create_bf(dev);
   // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
