@@ -615,6 +615,16 @@ std::vector<StageRange> pipeline_stages(const std::vector<const DataChunk*>& chu
   return st;
 }
 
+// Rows per stage of a pipelined batch of `total` rows, 0 = one piece: a quarter of the batch, at least 512 Ki and at
+// most DeviceContext::pipeline_rows; batches under 2 Mi rows (or two stages) run in one piece. Mid-size batches
+// gain from the overlap (r05, tools/host_bench --batch-sizes, profiles/r05/host_batch_sizes.jsonl: 4 Mi-row batches
+// 3.1 -> 4.0e9 rows/s, 8 Mi-row 4.1 -> 4.7e9); 1 Mi-row batches in 256 Ki stages lose to the single piece.
+uint64_t stage_rows_for(const DeviceContext& ctx, uint64_t total) {
+  const uint64_t cap = std::max<uint64_t>(ctx.pipeline_rows, 1), floor_rows = 1u << 19;
+  const uint64_t st = std::min(cap, std::max(floor_rows, total / 4));
+  return (total >= 2 * st && total >= std::min(4 * floor_rows, 2 * cap)) ? st : 0;
+}
+
 }  // namespace
 
 // Double-buffered staging of the pipelined batch paths, sized once for the largest stage (a slot that
@@ -1153,7 +1163,7 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:72-74
   if (cols.size() == 1) NoteKeyType(chunks[0]->data.at(cols[0]).key_type);  // (composite keys carry no min/max)
-  if (cols.size() == 1 && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
+  if (cols.size() == 1 && stage_rows_for(ctx, total)) {
     InsertPipelined(ctx, chunks, cols[0]);
     return;
   }
@@ -1179,7 +1189,7 @@ void PTBloomFilter::InsertBatch(DeviceContext& ctx, const std::vector<const Data
 void PTBloomFilter::InsertPipelined(DeviceContext& ctx, const std::vector<const DataChunk*>& chunks, uint64_t col) {
   const Clock::time_point t_begin = Clock::now();
   DeviceContext::PipelineStats& ps = ctx.stats;
-  const std::vector<StageRange> st = pipeline_stages(chunks, col, ctx.pipeline_rows);
+  const std::vector<StageRange> st = pipeline_stages(chunks, col, stage_rows_for(ctx, total_rows(chunks)));
   uint64_t max_rows = 0, total = 0;
   size_t ws_bytes = 0;
   for (const StageRange& r : st) {
@@ -1252,7 +1262,7 @@ void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const D
   reset_sels(sels, chunks.size());
   const uint64_t total = total_rows(chunks);
   if (total == 0) return;  // bloom_filter.cpp:63-65
-  if (cols.size() == 1 && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
+  if (cols.size() == 1 && stage_rows_for(ctx, total)) {
     LookupSelPipelined(ctx, chunks, sels, cols[0]);
     return;
   }
@@ -1326,7 +1336,7 @@ void PTBloomFilter::LookupSelPipelined(DeviceContext& ctx, const std::vector<con
                                        std::vector<SelectionVector>& sels, uint64_t col) const {
   const Clock::time_point t_begin = Clock::now();
   DeviceContext::PipelineStats& ps = ctx.stats;
-  const std::vector<StageRange> st = pipeline_stages(chunks, col, ctx.pipeline_rows);
+  const std::vector<StageRange> st = pipeline_stages(chunks, col, stage_rows_for(ctx, total_rows(chunks)));
   uint64_t max_rows = 0, total = 0;
   size_t ws_bytes = 16;
   for (const StageRange& r : st) {
@@ -1784,7 +1794,7 @@ uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChu
       if (bf->IsEmpty()) return 0;           // cpp:145-155
       act.push_back(i);
     }
-    if (!act.empty() && total >= 2 * std::max<uint64_t>(ctx.pipeline_rows, 1)) {
+    if (!act.empty() && stage_rows_for(ctx, total)) {
       uint64_t count = 0;
       if (act.size() == 1) {
         filters_[act[0]]->LookupSelBatch(ctx, inputs, outs, {cols_[act[0]]});
@@ -1994,7 +2004,7 @@ uint64_t UseBF::ExecuteChainPipelined(DeviceContext& ctx, const std::vector<cons
   const Clock::time_point t_begin = Clock::now();
   DeviceContext::PipelineStats& ps = ctx.stats;
   const size_t k = act.size();
-  std::vector<StageRange> st = pipeline_stages(inputs, cols_[act[0]], ctx.pipeline_rows);
+  std::vector<StageRange> st = pipeline_stages(inputs, cols_[act[0]], stage_rows_for(ctx, total_rows(inputs)));
   for (size_t f = 1; f < k; f++) (void)pipeline_stages(inputs, cols_[act[f]], ~0ULL);  // every column one key type
   uint64_t max_rows = 0;
   size_t ws_bytes = 16;

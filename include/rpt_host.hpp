@@ -114,9 +114,9 @@ class DeviceContext {
   // exception a task threw, after every task has finished.
   void parallel_for(size_t n, const std::function<void(size_t)>& fn);
 
-  // Single-column batches of at least 2 * pipeline_rows rows are staged in stages of about this many
-  // rows (whole chunks): flattening stage i+1 on the host overlaps the copy of stage i, the probe of
-  // stage i-1 and the copy back of stage i-2's selection vector.
+  // Batches of at least 2 Mi rows (or 2 * pipeline_rows when that is smaller) are staged in stages of a quarter of
+  // the batch, at least 512 Ki rows and at most pipeline_rows (whole chunks): flattening stage i+1 on the host
+  // overlaps the copy of stage i, the probe of stage i-1 and the copy back of stage i-2's result.
   uint64_t pipeline_rows = 1ULL << 22;
   // Host threads (the calling one included) that flatten a batch or stage of >= 128 Ki rows into pinned
   // memory and split a stage's selection vector into per-chunk ones. DuckDB's operator threads each own a

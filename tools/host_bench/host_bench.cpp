@@ -177,6 +177,62 @@ int host_bits(int dev) {
   return 0;
 }
 
+// Mid-size batches (a caching USE_BF flushing every 128 .. 4096 chunks): UseBF::ExecuteBatch with the default
+// stages (4 Mi rows: batches under 8 Mi rows run unpipelined) against stages of a quarter of the batch (>= 128 Ki
+// rows), one operator thread, 8 workers, C2's filter, p = 0.1.
+int host_batch_sizes(int dev) {
+  const size_t n_build = 10000000, n_probe = 1ULL << 24;
+  std::mt19937_64 rng(29);
+  std::vector<int64_t> b(n_build), q(n_probe);
+  for (auto& k : b) k = static_cast<int64_t>(rng() >> 1);
+  for (size_t i = 0; i < n_probe; i++) q[i] = (rng() % 10 == 0) ? b[rng() % n_build] : static_cast<int64_t>(rng() >> 1);
+  auto chunks = [](const std::vector<int64_t>& v) {
+    std::vector<rpt::DataChunk> cs;
+    for (size_t lo = 0; lo < v.size(); lo += 2048) {
+      rpt::DataChunk c;
+      c.count = std::min<size_t>(2048, v.size() - lo);
+      rpt::Vector x;
+      x.key_type = rpt::KeyType::I64;
+      x.data = v.data() + lo;
+      c.data.push_back(x);
+      cs.push_back(c);
+    }
+    return cs;
+  };
+  auto bch = chunks(b), pch = chunks(q);
+  std::vector<const rpt::DataChunk*> ball;
+  for (auto& c : bch) ball.push_back(&c);
+  rpt::DeviceContext ctx(dev);
+  auto bf = std::make_shared<rpt::PTBloomFilter>();
+  bf->Initialize(dev, static_cast<uint32_t>(n_build));
+  bf->InsertBatch(ctx, ball, {0});
+  bf->finalized_ = true;
+  rpt::UseBF ub({bf}, {0});
+  for (size_t per : {128, 512, 1024, 2048, 4096}) {
+    const size_t calls = pch.size() / per;
+    double rate[2];
+    for (int quarter = 0; quarter < 2; quarter++) {
+      ctx.pipeline_rows = quarter ? std::max<uint64_t>(1u << 17, per * 2048 / 4) : (1ULL << 22);
+      std::vector<rpt::SelectionVector> outs;
+      std::vector<const rpt::DataChunk*> bt;
+      for (size_t k = 0; k < per; k++) bt.push_back(&pch[k]);
+      ub.ExecuteBatch(ctx, bt, outs);  // warm-up
+      const auto t0 = clk::now();
+      for (size_t c = 0; c < calls; c++) {
+        bt.clear();
+        for (size_t k = 0; k < per; k++) bt.push_back(&pch[c * per + k]);
+        ub.ExecuteBatch(ctx, bt, outs);
+      }
+      rate[quarter] = static_cast<double>(calls) * per * 2048 / since(t0);
+    }
+    printf("{\"op\": \"host_path.batch_size\", \"chunks_per_call\": %zu, \"default_stages_rows_per_s\": %.4g, "
+           "\"quarter_stages_rows_per_s\": %.4g}\n", per, rate[0], rate[1]);
+    fflush(stdout);
+  }
+  ctx.pipeline_rows = 1ULL << 22;
+  return 0;
+}
+
 // The host -> device path of a DuckDB shim for JOB's INTEGER keys and for BIGINT keys:
 // FLAT int64, FLAT int32 and DICTIONARY int32 2048-row chunks through LookupSelBatch's pipeline (4 Mi-row
 // stages) with 1..16 worker threads per call, the host-side time of each phase per call (DeviceContext::
@@ -556,6 +612,8 @@ int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "--narrow") == 0) return host_narrow(dev);
   // --bits: result bits back vs sels back at pass fractions 0.1 / 0.5 / 0.9
   if (argc > 1 && std::strcmp(argv[1], "--bits") == 0) return host_bits(dev);
+  // --batch-sizes: mid-size batches, default stages vs quarter-batch stages
+  if (argc > 1 && std::strcmp(argv[1], "--batch-sizes") == 0) return host_batch_sizes(dev);
   // --create: only the CREATE_BF section
   if (argc > 1 && std::strcmp(argv[1], "--create") == 0) return create_bf(dev);
   // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
