@@ -1275,11 +1275,21 @@ void PTBloomFilter::LookupSelBatch(DeviceContext& ctx, const std::vector<const D
   void* ws = ctx.dev(2, ws_bytes);
   // [count (8 B) | sel]: small batches bring both back in ONE copy (one sync per call); larger ones
   // copy the count first and then exactly `count` ids
+  auto s = static_cast<hipStream_t>(ctx.stream());
+  if (ctx.bits_back && total > kSingleCopyRows) {  // the result bits back in one copy, one sync (no count first)
+    const size_t bits_bytes = (total + 511) / 512 * 64;
+    auto* d_bits = static_cast<uint64_t*>(ctx.dev(3, bits_bytes));
+    check(rpt_bf_probe_bits(bf_, &kc, nullptr, total, d_bits, ws, ws_bytes, s));
+    auto* h_bits = static_cast<uint64_t*>(ctx.host(3, bits_bytes));
+    check_hip(hipMemcpyAsync(h_bits, d_bits, bits_bytes, hipMemcpyDeviceToHost, s), "copy bits");
+    ctx.synchronize();
+    split_bits(ctx, chunks, 0, chunks.size(), h_bits, sels);
+    return;
+  }
   auto* d_out = static_cast<uint8_t*>(ctx.dev(3, 8 + total * 4));
   auto* d_cnt = reinterpret_cast<uint64_t*>(d_out);
   auto* d_sel = reinterpret_cast<uint32_t*>(d_out + 8);
-  check(rpt_bf_probe(bf_, &kc, nullptr, total, d_sel, d_cnt, ws, ws_bytes, ctx.stream()));
-  auto s = static_cast<hipStream_t>(ctx.stream());
+  check(rpt_bf_probe(bf_, &kc, nullptr, total, d_sel, d_cnt, ws, ws_bytes, s));
   const bool one_copy = total <= kSingleCopyRows;
   auto* h_out = static_cast<uint8_t*>(ctx.host(2, one_copy ? 8 + total * 4 : 8));
   check_hip(hipMemcpyAsync(h_out, d_out, one_copy ? 8 + total * 4 : 8, hipMemcpyDeviceToHost, s), "copy count");
@@ -1785,8 +1795,9 @@ uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChu
   }
   if (total >= (1ULL << 32)) throw GpuError(RPT_ERR_INVALID_ARGUMENT, "batch exceeds uint32 row ids");
   {
-    // large batches take the pipeline (flatten, copy, probe and copy back of successive stages overlap): one
-    // applicable filter through LookupSelBatch's, several through the chained one; same per-chunk sels
+    // one applicable filter: LookupSelBatch (fused, one piece with the result bits back, or pipelined, by size);
+    // several over a large batch: the chained pipeline (flatten, copy, probe and copy back of successive stages
+    // overlap); same per-chunk sels as the filter loop below
     std::vector<size_t> act;
     for (size_t i = 0; i < filters_.size(); i++) {
       const auto& bf = filters_[i];
@@ -1794,9 +1805,9 @@ uint64_t UseBF::ExecuteBatch(DeviceContext& ctx, const std::vector<const DataChu
       if (bf->IsEmpty()) return 0;           // cpp:145-155
       act.push_back(i);
     }
-    if (!act.empty() && stage_rows_for(ctx, total)) {
+    if (act.size() == 1 || (!act.empty() && stage_rows_for(ctx, total))) {
       uint64_t count = 0;
-      if (act.size() == 1) {
+      if (act.size() == 1) {  // any size: LookupSelBatch picks the fused, single-piece or pipelined route
         filters_[act[0]]->LookupSelBatch(ctx, inputs, outs, {cols_[act[0]]});
         for (const SelectionVector& o : outs) count += o.size();
       } else {
