@@ -207,6 +207,46 @@ int host_batch_sizes(int dev) {
   bf->Initialize(dev, static_cast<uint32_t>(n_build));
   bf->InsertBatch(ctx, ball, {0});
   bf->finalized_ = true;
+  // a second filter on a second (INTEGER, 50 % hits) column for the two-filter chain below
+  std::vector<int32_t> b1(n_build), q1(n_probe);
+  for (auto& k : b1) k = static_cast<int32_t>(rng());
+  for (size_t i = 0; i < n_probe; i++) q1[i] = (rng() % 2 == 0) ? b1[rng() % n_build] : static_cast<int32_t>(rng());
+  for (size_t i = 0; i < bch.size(); i++) {
+    rpt::Vector x;
+    x.key_type = rpt::KeyType::I32;
+    x.data = b1.data() + 2048 * i;
+    bch[i].data.push_back(x);
+  }
+  for (size_t i = 0; i < pch.size(); i++) {
+    rpt::Vector x;
+    x.key_type = rpt::KeyType::I32;
+    x.data = q1.data() + 2048 * i;
+    pch[i].data.push_back(x);
+  }
+  auto bf1 = std::make_shared<rpt::PTBloomFilter>();
+  bf1->Initialize(dev, static_cast<uint32_t>(n_build));
+  bf1->InsertBatch(ctx, ball, {1});
+  bf1->finalized_ = true;
+  rpt::UseBF ub2({bf, bf1}, {0, 1});
+  for (size_t per : {128, 512, 1024, 2048}) {
+    const size_t calls = pch.size() / per;
+    std::vector<rpt::SelectionVector> outs;
+    std::vector<const rpt::DataChunk*> bt;
+    for (size_t k = 0; k < per; k++) bt.push_back(&pch[k]);
+    ub2.ExecuteBatch(ctx, bt, outs);  // warm-up
+    double best = 0;
+    for (int rep = 0; rep < 3; rep++) {  // best of 3 passes (small calls are latency-bound and noisy)
+      const auto t0 = clk::now();
+      for (size_t c = 0; c < calls; c++) {
+        bt.clear();
+        for (size_t k = 0; k < per; k++) bt.push_back(&pch[c * per + k]);
+        ub2.ExecuteBatch(ctx, bt, outs);
+      }
+      best = std::max(best, static_cast<double>(calls) * per * 2048 / since(t0));
+    }
+    printf("{\"op\": \"host_path.batch_size.chain2\", \"chunks_per_call\": %zu, \"rows_per_s\": %.4g}\n", per, best);
+    fflush(stdout);
+  }
   rpt::UseBF ub({bf}, {0});
   for (size_t per : {128, 512, 1024, 2048, 4096}) {
     const size_t calls = pch.size() / per;
@@ -217,13 +257,16 @@ int host_batch_sizes(int dev) {
       std::vector<const rpt::DataChunk*> bt;
       for (size_t k = 0; k < per; k++) bt.push_back(&pch[k]);
       ub.ExecuteBatch(ctx, bt, outs);  // warm-up
-      const auto t0 = clk::now();
-      for (size_t c = 0; c < calls; c++) {
-        bt.clear();
-        for (size_t k = 0; k < per; k++) bt.push_back(&pch[c * per + k]);
-        ub.ExecuteBatch(ctx, bt, outs);
+      rate[quarter] = 0;
+      for (int rep = 0; rep < 3; rep++) {  // best of 3 passes
+        const auto t0 = clk::now();
+        for (size_t c = 0; c < calls; c++) {
+          bt.clear();
+          for (size_t k = 0; k < per; k++) bt.push_back(&pch[c * per + k]);
+          ub.ExecuteBatch(ctx, bt, outs);
+        }
+        rate[quarter] = std::max(rate[quarter], static_cast<double>(calls) * per * 2048 / since(t0));
       }
-      rate[quarter] = static_cast<double>(calls) * per * 2048 / since(t0);
     }
     printf("{\"op\": \"host_path.batch_size\", \"chunks_per_call\": %zu, \"default_stages_rows_per_s\": %.4g, "
            "\"quarter_stages_rows_per_s\": %.4g}\n", per, rate[0], rate[1]);
