@@ -1535,11 +1535,12 @@ CreateBF::CreateBF(int device, uint64_t estimated_cardinality, std::vector<uint6
 void CreateBF::Sink(LocalState& local, const DataChunk& chunk) const {
   // materialize the chunk (every column, flattened, owned): the source re-emits it
   // (physical_create_bf.cpp:211-218). The copies are bump-allocated from 1 MiB blocks the state owns (one
-  // allocation per ~64 chunks, nothing zero-filled first).
+  // allocation per ~64 chunks, nothing zero-filled first; 4 MiB blocks advised as transparent huge pages
+  // measured no faster).
   const Clock::time_point t0 = Clock::now();
   auto alloc = [&local](size_t words) {
     if (words > local.arena_left) {
-      const size_t blk = std::max<size_t>(words, size_t(1) << 17);
+      const size_t blk = std::max<size_t>(words, kSinkBlockWords);
       local.storage.emplace_back(new uint64_t[blk]);
       local.arena = local.storage.back().get();
       local.arena_left = blk;
@@ -1590,11 +1591,21 @@ void CreateBF::Flush(LocalState& local) const {
   const int b = async ? static_cast<int>(local.flushes & 1) : 0;
   auto done = static_cast<hipEvent_t>(local.ctx.event(b));
   if (async && local.flushes >= 2) check_hip(hipEventSynchronize(done), "hipEventSynchronize");
+  // Once the rows flushed by all states make Finalize's resize certain (its predicate only grows with the row
+  // count), inserting into this filter is wasted: Finalize reinitializes it and rehashes every row from HBM. An
+  // under-estimated filter is also the small one whose atomic inserts contend on a few words (1e8 rows into the
+  // 1 KiB filter of an estimate of 1000: 26 ms of the sink's 64; profiles/r05/host_create_split.jsonl).
+  const uint64_t flushed = flushed_rows_.fetch_add(local.pending_rows) + local.pending_rows;
   for (size_t i = 0; i < cols_.size(); i++) {
     const int slot = async ? 8 + 4 * static_cast<int>(i) + 2 * b : 0;
     const DeviceKeyColumn::Segment& g = local.keys[i].Append(local.ctx, batch, cols_[i], slot);
     filters_[i]->NoteKeyType(batch[0]->data.at(cols_[i]).key_type);
-    filters_[i]->InsertDevice(local.ctx, g.col, g.rows, /*synchronize=*/!async);
+    if (WillResize(i, flushed)) {
+      skipped_insert_rows_.fetch_add(g.rows);
+      if (!async) local.ctx.synchronize();  // the copy out of staging slot 0 is done before the slot is refilled
+    } else {
+      filters_[i]->InsertDevice(local.ctx, g.col, g.rows, /*synchronize=*/!async);
+    }
   }
   if (async) check_hip(hipEventRecord(done, static_cast<hipStream_t>(local.ctx.stream())), "hipEventRecord");
   local.flushes++;
@@ -1620,6 +1631,12 @@ void CreateBF::Combine(LocalState& local) {
   local.pending_from = 0;
 }
 
+bool CreateBF::WillResize(size_t i, uint64_t actual_rows) const {
+  const PTBloomFilter& bf = *filters_[i];
+  return resize_rule_ == ResizeRule::kReferenceFormula ? rpt_bf_needs_resize(bf.SizedForRows(), actual_rows) == 1
+                                                       : bf.NeedsResize(actual_rows);
+}
+
 void CreateBF::Finalize() {
   const uint64_t actual_rows = total_rows_;
   if (actual_rows > 0) {
@@ -1629,10 +1646,7 @@ void CreateBF::Finalize() {
       // physical_create_bf.cpp:383-398: resize iff the allocated filter gives < 8 bits per actual row,
       // on this filter's real allocation (default) or by the reference's formula verbatim (ResizeRule);
       // the rehash reads the build column from HBM
-      const bool resize = resize_rule_ == ResizeRule::kReferenceFormula
-                              ? rpt_bf_needs_resize(bf.SizedForRows(), actual_rows) == 1
-                              : bf.NeedsResize(actual_rows);
-      if (resize) {
+      if (WillResize(i, actual_rows)) {
         bf.ReinitializeAndRehash(ctx, actual_rows, all_keys_[i]);
         resized_[i] = true;
       }

@@ -288,6 +288,7 @@ class CreateBF {
     double materialize_s = 0, flush_s = 0;  // host time in Sink's materialization / in the flushes
   };
   static constexpr size_t kAsyncFlushColumns = 12;
+  static constexpr size_t kSinkBlockWords = size_t(1) << 17;  // materialization blocks of 1 MiB
   // CreateBFGlobalSourceState (physical_create_bf.cpp:441-485): chunk ranges, one per source thread
   struct GlobalSourceState {
     std::vector<std::pair<size_t, size_t>> chunks_todo;
@@ -317,6 +318,10 @@ class CreateBF {
   bool Resized(size_t build_column) const { return resized_.at(build_column); }
   // The build column's keys in HBM (after Combine): a device-side consumer can read them directly.
   const DeviceKeyColumn& DeviceKeys(size_t build_column) const { return all_keys_.at(build_column); }
+  // Rows whose sink-time insert was skipped because the rows flushed so far already make Finalize resize the
+  // filter (the resize rule is monotone in the row count), so Finalize's rehash from HBM inserts them instead;
+  // the finalized filter is the same either way.
+  uint64_t SkippedInsertRows() const { return skipped_insert_rows_.load(); }
   // CreateBFGlobalSinkState::column_min_max[i] (physical_create_bf.cpp:229-272): min / max of the
   // valid keys of build column i, computed by the insert kernels; false when no valid key was seen.
   bool MinMax(size_t build_column, int64_t& min_value, int64_t& max_value) const;
@@ -328,6 +333,7 @@ class CreateBF {
 
  private:
   void Flush(LocalState& local) const;  // stage + insert the pending chunks' build columns
+  bool WillResize(size_t build_column, uint64_t actual_rows) const;  // Finalize's resize predicate
 
   int device_;
   uint64_t estimated_cardinality_;
@@ -341,6 +347,8 @@ class CreateBF {
   std::vector<std::unique_ptr<uint64_t[]>> all_storage_;
   std::vector<DeviceKeyColumn> all_keys_;
   uint64_t total_rows_ = 0;
+  mutable std::atomic<uint64_t> flushed_rows_{0};        // rows handed to Flush by every sink state so far
+  mutable std::atomic<uint64_t> skipped_insert_rows_{0};
 };
 
 // PhysicalUseBF::ExecuteInternal (physical_use_bf.cpp:60-198): AND of the filters over the chunk,

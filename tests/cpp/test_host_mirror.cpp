@@ -991,6 +991,8 @@ int main() {
     create.Finalize();
     EXPECT(create.MaterializedRows() == nb, "materialized %llu", (unsigned long long)create.MaterializedRows());
     EXPECT(create.Resized(0) && create.Resized(1), "under-estimated filters must be resized");
+    // the first flush (>= 5000 rows) already makes the resize certain: no sink-time insert, Finalize rehashes all
+    EXPECT(create.SkippedInsertRows() == 2 * nb, "skipped sink inserts %llu", (unsigned long long)create.SkippedInsertRows());
     const int lnb = rpt_oracle_log_num_blocks(nb);
     std::vector<uint64_t> w0(1ULL << lnb, 0), w1(1ULL << lnb, 0);
     {
@@ -1021,6 +1023,30 @@ int main() {
       EXPECT(sync_create.GetBloomFilter(0)->ExportWords() == w0 && sync_create.GetBloomFilter(1)->ExportWords() == w1,
              "synchronous sink flushes: words differ from the oracle");
       EXPECT(ls[0]->flushes >= 3 && ls[0]->materialize_s > 0 && ls[0]->flush_s > 0, "sink stats");
+    }
+    {  // estimate 20000 (2^12 blocks: resize above 32768 rows): the first flushes insert, the later ones are skipped
+      rpt::CreateBF part(dev, 20000, {0, 1}, 5000);
+      std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> ls;
+      for (int t = 0; t < 4; t++) ls.push_back(part.MakeLocalState());
+      std::vector<std::thread> st;
+      for (int t = 0; t < 4; t++)
+        st.emplace_back([&, t] {
+          for (size_t k = t; k < bst.chunks.size(); k += 4) part.Sink(*ls[t], bst.chunks[k]);
+          part.Combine(*ls[t]);
+        });
+      for (auto& th : st) th.join();
+      EXPECT(part.GetBloomFilter(0)->LogNumBlocks() == 12, "estimate 20000: 2^%d blocks", part.GetBloomFilter(0)->LogNumBlocks());
+      const uint64_t skipped = part.SkippedInsertRows();
+      part.Finalize();
+      EXPECT(part.Resized(0) && part.Resized(1), "estimate 20000: resized");
+      EXPECT(skipped > 0 && skipped < 2 * nb, "estimate 20000: skipped %llu of %llu", (unsigned long long)skipped,
+             (unsigned long long)(2 * nb));
+      EXPECT(part.GetBloomFilter(0)->ExportWords() == w0 && part.GetBloomFilter(1)->ExportWords() == w1,
+             "estimate 20000: words differ from the oracle");
+      int64_t mn = 0, mx = 0, e0[2];
+      std::vector<uint64_t> va = pack(bt.v0, 0, nb);
+      rpt_oracle_minmax_i64(bt.c0.data(), nullptr, va.data(), nb, e0);
+      EXPECT(part.MinMax(0, mn, mx) && mn == e0[0] && mx == e0[1], "estimate 20000: min/max");
     }
     // min/max dynamic filter per build column (physical_create_bf.cpp:229-272), NULLs skipped
     {
@@ -1183,7 +1209,7 @@ int main() {
       for (const auto& ch : bst.chunks) c2.Sink(*l, ch);
       c2.Combine(*l);
       c2.Finalize();
-      EXPECT(!c2.Resized(0), "no resize at the right estimate");
+      EXPECT(!c2.Resized(0) && c2.SkippedInsertRows() == 0, "no resize (and no skipped insert) at the right estimate");
       EXPECT(c2.GetBloomFilter(0)->ExportWords() == w0, "batched-sink filter differs from the oracle");
     }
 

@@ -639,6 +639,71 @@ int create_bf(int dev) {
   return 0;
 }
 
+// Where CREATE_BF's sink time goes: per sink thread, when its Sink loop ends and when its Combine returns
+// (ms from the start), for an under-estimated filter (tiny: atomic inserts, resized at Finalize) and a
+// right-sized one (128 MiB: partitioned inserts), flushes synchronous and asynchronous.
+int create_split(int dev) {
+  const size_t n_cb = 100000000;
+  std::mt19937_64 rng(43);
+  std::vector<int64_t> cb(n_cb);
+  for (auto& k : cb) k = static_cast<int64_t>(rng() >> 1);
+  std::vector<rpt::DataChunk> cchunks;
+  for (size_t lo = 0; lo < cb.size(); lo += 2048) {
+    rpt::DataChunk c;
+    c.count = std::min<size_t>(2048, cb.size() - lo);
+    rpt::Vector x;
+    x.key_type = rpt::KeyType::I64;
+    x.data = cb.data() + lo;
+    c.data.push_back(x);
+    cchunks.push_back(c);
+  }
+  for (int rep = 0; rep < 2; rep++)
+  for (uint64_t est : {uint64_t(1000), uint64_t(n_cb)})
+  for (bool async : {false, true}) {
+    rpt::CreateBF create(dev, est, {0});
+    const int T = 8;
+    std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> locals;
+    for (int t = 0; t < T; t++) {
+      locals.push_back(create.MakeLocalState());
+      locals.back()->async_flush = async;
+      locals.back()->ctx.flatten_threads = 2;
+    }
+    const int log_blocks0 = create.GetBloomFilter(0)->LogNumBlocks();
+    std::vector<double> sink_end(T), comb_end(T);
+    auto t0 = clk::now();
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; t++)
+      th.emplace_back([&, t] {
+        for (size_t k = t; k < cchunks.size(); k += T) create.Sink(*locals[t], cchunks[k]);
+        sink_end[t] = since(t0) * 1e3;
+        create.Combine(*locals[t]);
+        comb_end[t] = since(t0) * 1e3;
+      });
+    for (auto& x : th) x.join();
+    const double total_ms = since(t0) * 1e3;
+    t0 = clk::now();
+    create.Finalize();
+    const double fin_ms = since(t0) * 1e3;
+    double mat = 0, fl = 0, se = 0, ce = 0, se_max = 0;
+    for (int t = 0; t < T; t++) {
+      mat += locals[t]->materialize_s * 1e3 / T;
+      fl += locals[t]->flush_s * 1e3 / T;
+      se += sink_end[t] / T;
+      ce += comb_end[t] / T;
+      se_max = std::max(se_max, sink_end[t]);
+    }
+    printf("{\"op\": \"CreateBF split\", \"rep\": %d, \"rows\": %zu, \"estimated_cardinality\": %llu, \"async_flush\": %s, "
+           "\"resized\": %s, \"log_blocks_during_sink\": %d, \"sink_combine_rows_per_s\": %.4g, \"total_ms\": %.2f, "
+           "\"sink_loop_end_ms_avg\": %.2f, \"sink_loop_end_ms_max\": %.2f, \"combine_end_ms_avg\": %.2f, "
+           "\"materialize_ms_per_thread\": %.2f, \"flush_ms_per_thread\": %.2f, \"finalize_ms\": %.2f}\n",
+           rep, n_cb, static_cast<unsigned long long>(est), async ? "true" : "false", create.Resized(0) ? "true" : "false",
+           log_blocks0,
+           n_cb / (total_ms * 1e-3), total_ms, se, se_max, ce, mat, fl, fin_ms);
+    fflush(stdout);
+  }
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -659,6 +724,8 @@ int main(int argc, char** argv) {
   if (argc > 1 && std::strcmp(argv[1], "--batch-sizes") == 0) return host_batch_sizes(dev);
   // --create: only the CREATE_BF section
   if (argc > 1 && std::strcmp(argv[1], "--create") == 0) return create_bf(dev);
+  // --create-split: CREATE_BF sink loop vs Combine wait per thread, tiny vs right-sized filter
+  if (argc > 1 && std::strcmp(argv[1], "--create-split") == 0) return create_split(dev);
   // --spin: host threads spin (hipDeviceScheduleSpin) instead of the runtime's default wait while a
   // synchronize waits for the device (per-vector call latency experiment)
   if (argc > 1 && std::strcmp(argv[1], "--spin") == 0) {
