@@ -70,6 +70,19 @@ def test_resize_rule_matches_oracle():
             assert lib.rpt_bf_needs_resize(s, a) == orc.lib().rpt_oracle_needs_resize(s, a)
 
 
+def test_resize_rules_monotone_in_rows():
+    """rpt::CreateBF skips a sink flush's insert once the rows flushed so far make Finalize resize: sound only
+    because both resize rules, once true, stay true as the row count grows (physical_create_bf.cpp:383-398)."""
+    lib = _lib.load()
+    for s in [0, 1, 42, 1000, 20000, 10**7]:
+        rows = sorted({0, 1, 64, 65, 512, 1024, 1025, 2048, 2049, s * 8, s * 8 + 1, s * 12, s * 16, s * 16 + 1, 10**9})
+        ref = [lib.rpt_bf_needs_resize(s, a) for a in rows]
+        assert ref == sorted(ref), (s, ref)  # 0 ... 0 1 ... 1
+        L = orc.log_num_blocks(max(s, 1))
+        alloc = [orc.needs_resize_alloc(L, a) for a in rows]
+        assert alloc == sorted(alloc), (s, alloc)
+
+
 def test_workspace_size_grows_with_rows():
     lib = _lib.load()
     prev = 0
