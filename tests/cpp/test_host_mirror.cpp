@@ -882,6 +882,7 @@ static std::vector<uint64_t> pack_all(const std::vector<bool>& v) { return pack(
 static void fuzz_pipelines(int dev) {
   std::mt19937_64 rng(2026);
   uint64_t stages = 0, narrow = 0;
+  int create_skipped = 0;
   const int iters = 30;
   for (int it = 0; it < iters; it++) {
     const bool narrow64 = rng() % 2;
@@ -956,9 +957,49 @@ static void fuzz_pipelines(int dev) {
     }
     stages += ctx.stats.stages;
     narrow += ctx.stats.narrow_stages;
+    {  // CREATE_BF over the same build chunks: random estimate, flush size, sink threads, flush mode and resize rule
+      const uint64_t ests[] = {1000, nb / 8 + 1, nb / 2 + 1, nb, 2 * nb};
+      const uint64_t est = ests[rng() % 5];
+      const uint64_t flush = 2048 + rng() % 60000;
+      const int T = 1 + static_cast<int>(rng() % 4);
+      const bool async = rng() % 2;
+      const auto rule = rng() % 2 ? rpt::CreateBF::ResizeRule::kReferenceFormula : rpt::CreateBF::ResizeRule::kOnAllocation;
+      rpt::CreateBF cb(dev, est, {0, 1}, flush, rule);
+      std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> ls;
+      for (int t = 0; t < T; t++) {
+        ls.push_back(cb.MakeLocalState());
+        ls.back()->async_flush = async;
+      }
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+          for (size_t k = t; k < bst.chunks.size(); k += T) cb.Sink(*ls[t], bst.chunks[k]);
+          cb.Combine(*ls[t]);
+        });
+      for (auto& x : th) x.join();
+      cb.Finalize();
+      const int lest = rpt_oracle_log_num_blocks(static_cast<uint32_t>(est));
+      const bool want_resize = rule == rpt::CreateBF::ResizeRule::kReferenceFormula
+                                   ? rpt_oracle_needs_resize(static_cast<uint32_t>(est), nb) > 0
+                                   : rpt_oracle_needs_resize_alloc(lest, nb) > 0;
+      const int l = want_resize ? lnb : lest;
+      std::vector<uint64_t> c0(1ULL << l, 0), c1(1ULL << l, 0);
+      rpt_oracle_insert_i64(c0.data(), l, bc.v64.data(), nullptr, vb0.data(), nb);
+      rpt_oracle_insert_i32(c1.data(), l, bc.v32.data(), nullptr, vb1.data(), nb);
+      EXPECT(cb.Resized(0) == want_resize && cb.Resized(1) == want_resize &&
+                 cb.GetBloomFilter(0)->ExportWords() == c0 && cb.GetBloomFilter(1)->ExportWords() == c1,
+             "fuzz %d: CREATE_BF (estimate %llu, flush %llu, %d threads, async %d, rule %d): resized %d, words differ",
+             it, (unsigned long long)est, (unsigned long long)flush, T, async ? 1 : 0,
+             rule == rpt::CreateBF::ResizeRule::kReferenceFormula ? 1 : 0, cb.Resized(0) ? 1 : 0);
+      EXPECT(want_resize || cb.SkippedInsertRows() == 0, "fuzz %d: inserts skipped without a resize", it);
+      int64_t e[2], mn = 0, mx = 0;
+      if (rpt_oracle_minmax_i64(bc.v64.data(), nullptr, vb0.data(), nb, e))
+        EXPECT(cb.MinMax(0, mn, mx) && mn == e[0] && mx == e[1], "fuzz %d: CREATE_BF min/max", it);
+      create_skipped += cb.SkippedInsertRows() > 0 && cb.SkippedInsertRows() < 2 * nb;
+    }
   }
-  printf("fuzz: %d batches, %llu pipelined stages, %llu of them narrow\n", iters, (unsigned long long)stages,
-         (unsigned long long)narrow);
+  printf("fuzz: %d batches, %llu pipelined stages, %llu of them narrow, %d builds with skipped inserts after inserted ones\n",
+         iters, (unsigned long long)stages, (unsigned long long)narrow, create_skipped);
   EXPECT(stages > 100 && narrow > 10, "the fuzz reached the pipelines (%llu stages, %llu narrow)", (unsigned long long)stages,
          (unsigned long long)narrow);
 }
