@@ -222,8 +222,10 @@ class PTBloomFilter {
   // bloom_filter.cpp:34-58: reallocate for actual_rows and re-insert the materialized chunks
   void ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const std::vector<DataChunk>& data,
                              const std::vector<uint64_t>& cols);
-  // ... or re-insert a key column already in HBM (no PCIe traffic)
+  // ... or re-insert a key column already in HBM (no PCIe traffic); NULL-free segments are inserted in groups
+  // of up to kRehashGroupRows rows, copied back to back into one device buffer (context slot 7)
   void ReinitializeAndRehash(DeviceContext& ctx, uint64_t actual_rows, const DeviceKeyColumn& keys);
+  static constexpr uint64_t kRehashGroupRows = 1ULL << 27;
 
   uint64_t SizedForRows() const;
   // Finalize's resize predicate on this filter's real allocation (rpt_bf_needs_resize_alloc)

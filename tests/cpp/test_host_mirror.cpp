@@ -653,6 +653,18 @@ static void pinned_cache(int dev) {
   rpt::SetPinnedCacheLimit(size_t(4) << 30);
   rpt::ReleasePinnedCache();
   EXPECT(rpt::PinnedCacheBytes() == 0, "released");
+  // streams and events of an ended context serve the next one (drained, not capturing)
+  // (every later test's contexts run on pooled streams)
+  void *s0 = nullptr, *e0 = nullptr;
+  {
+    rpt::DeviceContext a(dev);
+    s0 = a.stream();
+    e0 = a.event(0);
+  }
+  {
+    rpt::DeviceContext b(dev);
+    EXPECT(b.stream() == s0 && b.event(0) == e0, "pooled stream / event reused");
+  }
 }
 
 // Narrow BIGINT keys (DeviceContext::narrow_keys): chunks whose keys share their high 32 bits (0, 5 and 0xFFFFFFFF,
@@ -1088,6 +1100,37 @@ int main() {
       std::vector<uint64_t> va = pack(bt.v0, 0, nb);
       rpt_oracle_minmax_i64(bt.c0.data(), nullptr, va.data(), nb, e0);
       EXPECT(part.MinMax(0, mn, mx) && mn == e0[0] && mx == e0[1], "estimate 20000: min/max");
+    }
+    // the rehash from HBM groups NULL-free segments into one insert: a NULL-free build, and one with NULLs in a few
+    // segments only (grouped and single segments interleaved)
+    for (const int null_every : {0, 70000}) {
+      const size_t ng = 150001;
+      Table gt = make_table(ng, 5, null_every, 0);
+      ChunkStore gst;
+      make_chunks(gt, ng, gst, false);
+      rpt::CreateBF g(dev, 1000, {0, 1}, 6000);
+      std::vector<std::unique_ptr<rpt::CreateBF::LocalState>> ls;
+      for (int t = 0; t < 3; t++) ls.push_back(g.MakeLocalState());
+      std::vector<std::thread> st;
+      for (int t = 0; t < 3; t++)
+        st.emplace_back([&, t] {
+          for (size_t k = t; k < gst.chunks.size(); k += 3) g.Sink(*ls[t], gst.chunks[k]);
+          g.Combine(*ls[t]);
+        });
+      for (auto& th : st) th.join();
+      g.Finalize();
+      const int lg = rpt_oracle_log_num_blocks(ng);
+      std::vector<uint64_t> g0(1ULL << lg, 0), g1(1ULL << lg, 0);
+      std::vector<uint64_t> va = pack(gt.v0, 0, ng), vb = pack(gt.v1, 0, ng);
+      rpt_oracle_insert_i64(g0.data(), lg, gt.c0.data(), nullptr, va.data(), ng);
+      rpt_oracle_insert_i32(g1.data(), lg, gt.c1.data(), nullptr, vb.data(), ng);
+      size_t with_nulls = 0;
+      for (const auto& sg : g.DeviceKeys(0).segments()) with_nulls += sg.col.validity != nullptr;
+      EXPECT(g.Resized(0) && g.DeviceKeys(0).segments().size() >= 20 && (null_every == 0) == (with_nulls == 0),
+             "grouped rehash (NULLs every %d): resized %d, %zu segments, %zu with NULLs", null_every, g.Resized(0) ? 1 : 0,
+             g.DeviceKeys(0).segments().size(), with_nulls);
+      EXPECT(g.GetBloomFilter(0)->ExportWords() == g0 && g.GetBloomFilter(1)->ExportWords() == g1,
+             "grouped rehash (NULLs every %d): words differ from the oracle", null_every);
     }
     // min/max dynamic filter per build column (physical_create_bf.cpp:229-272), NULLs skipped
     {

@@ -684,6 +684,35 @@ int create_split(int dev) {
     t0 = clk::now();
     create.Finalize();
     const double fin_ms = since(t0) * 1e3;
+    // Finalize's parts: the rehash from HBM with a warm context, and the reinitialization alone
+    double rehash_warm_ms = 0, reinit_ms = 0;
+    {
+      rpt::DeviceContext c2(dev);
+      auto bfh = create.GetBloomFilter(0);
+      bfh->ReinitializeAndRehash(c2, n_cb, create.DeviceKeys(0));  // warm-up
+      auto t1 = clk::now();
+      bfh->ReinitializeAndRehash(c2, n_cb, create.DeviceKeys(0));
+      rehash_warm_ms = since(t1) * 1e3;
+      rpt::DeviceKeyColumn none(dev);
+      t1 = clk::now();
+      bfh->ReinitializeAndRehash(c2, n_cb, none);
+      reinit_ms = since(t1) * 1e3;
+      bfh->ReinitializeAndRehash(c2, n_cb, create.DeviceKeys(0));
+    }
+    // a short-lived context's own costs: create, two large device buffers (the rehash's sizes), destroy
+    double ctor_ms, alloc_ms, dtor_ms;
+    {
+      auto t1 = clk::now();
+      auto c3 = std::make_unique<rpt::DeviceContext>(dev);
+      ctor_ms = since(t1) * 1e3;
+      t1 = clk::now();
+      (void)c3->dev(6, size_t(1) << 30);
+      (void)c3->dev(7, n_cb * 8);
+      alloc_ms = since(t1) * 1e3;
+      t1 = clk::now();
+      c3.reset();
+      dtor_ms = since(t1) * 1e3;
+    }
     double mat = 0, fl = 0, se = 0, ce = 0, se_max = 0;
     for (int t = 0; t < T; t++) {
       mat += locals[t]->materialize_s * 1e3 / T;
@@ -695,10 +724,13 @@ int create_split(int dev) {
     printf("{\"op\": \"CreateBF split\", \"rep\": %d, \"rows\": %zu, \"estimated_cardinality\": %llu, \"async_flush\": %s, "
            "\"resized\": %s, \"log_blocks_during_sink\": %d, \"sink_combine_rows_per_s\": %.4g, \"total_ms\": %.2f, "
            "\"sink_loop_end_ms_avg\": %.2f, \"sink_loop_end_ms_max\": %.2f, \"combine_end_ms_avg\": %.2f, "
-           "\"materialize_ms_per_thread\": %.2f, \"flush_ms_per_thread\": %.2f, \"finalize_ms\": %.2f}\n",
+           "\"materialize_ms_per_thread\": %.2f, \"flush_ms_per_thread\": %.2f, \"finalize_ms\": %.2f, "
+           "\"segments\": %zu, \"rehash_warm_ctx_ms\": %.2f, \"reinit_only_ms\": %.2f, \"ctx_create_ms\": %.2f, "
+           "\"ctx_alloc_1g_800m_ms\": %.2f, \"ctx_destroy_ms\": %.2f}\n",
            rep, n_cb, static_cast<unsigned long long>(est), async ? "true" : "false", create.Resized(0) ? "true" : "false",
            log_blocks0,
-           n_cb / (total_ms * 1e-3), total_ms, se, se_max, ce, mat, fl, fin_ms);
+           n_cb / (total_ms * 1e-3), total_ms, se, se_max, ce, mat, fl, fin_ms, create.DeviceKeys(0).segments().size(),
+           rehash_warm_ms, reinit_ms, ctor_ms, alloc_ms, dtor_ms);
     fflush(stdout);
   }
   return 0;
