@@ -273,6 +273,39 @@ def test_partitioned_insert_vs_oracle(rpt, log_nb, dtype):
         assert np.array_equal(bf.export_words(), w), strategy
 
 
+@pytest.mark.parametrize("log_nb", [7, 14])
+@pytest.mark.parametrize("dtype", [np.int64, np.int32])
+@pytest.mark.parametrize("shape", ["one_key", "runs", "pairs", "dictionary"])
+def test_atomic_insert_repeated_keys_vs_oracle(rpt, log_nb, dtype, shape):
+    """The atomic insert drops a row whose hash equals the previous row's (within a lane and across lanes,
+    never from lane 0): runs of equal keys of every length, NULLs inside runs, ragged ends and the
+    dictionary (key_sel) path give the oracle's words."""
+    rng = np.random.default_rng(7 + log_nb)
+    n = 5 * 4096 + 131
+    if shape == "one_key":
+        keys = np.full(n, 123456789, dtype=np.int64)
+    elif shape == "runs":  # run lengths 1..300
+        vals = rng.integers(-2**40, 2**40, size=n, dtype=np.int64)
+        keys = np.repeat(vals, rng.integers(1, 300, size=n))[:n]
+    elif shape == "pairs":  # every key twice in a row: duplicates at odd rows, across lane boundaries
+        keys = np.repeat(rng.integers(-2**40, 2**40, size=n // 2 + 1, dtype=np.int64), 2)[:n]
+    else:
+        keys = rng.integers(-2**40, 2**40, size=37, dtype=np.int64)
+    keys = keys.astype(dtype)
+    valid = rng.random(n) > 0.05
+    vw = gu.validity_words(valid)
+    w = orc.new_words(log_nb)
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    if shape == "dictionary":
+        sel = np.repeat(rng.integers(0, keys.size, size=n).astype(np.uint32), 3)[:n]
+        orc.insert_keys(w, log_nb, keys, key_sel=sel, validity=vw)
+        bf.insert(dev(keys), key_sel=dev(sel), validity=dev(vw), strategy=rpt.RPT_INSERT_ATOMIC)
+    else:
+        orc.insert_keys(w, log_nb, keys, validity=vw)
+        bf.insert(dev(keys), validity=dev(vw), strategy=rpt.RPT_INSERT_ATOMIC)
+    assert np.array_equal(bf.export_words(), w)
+
+
 def test_concurrent_inserts_on_two_streams(rpt):
     keys = orc.synth_build_keys(400000)
     bf = rpt.BloomFilter(keys.size)
