@@ -569,6 +569,9 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
 #ifndef RPT_EXP_STORE_SKIP_ZERO
 #define RPT_EXP_STORE_SKIP_ZERO 0
 #endif
+#ifndef RPT_SLICE_INSERT_DEDUP
+#define RPT_SLICE_INSERT_DEDUP 1  // drop a record equal to its slot's previous one (below)
+#endif
 constexpr int kSliceMergeAtomic = 0, kSliceMergeStore = 1, kSliceMergeAdaptive = 2, kSliceMergeStoreAll = 3;
 __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* __restrict__ words, uint32_t splits,
                                                                     uint64_t n_tiles,
@@ -662,9 +665,11 @@ __global__ __launch_bounds__(kSliceThreads) void slice_insert_kernel(uint64_t* _
 #pragma unroll
       for (int u = 0; u < RPT_SLICE_UNROLL; u++) {
         if (w0 + u * 64 >= total) break;  // uniform
+        // a record equal to the slot's previous one (same word, same mask) ORs nothing new: LDS atomics on one
+        // word serialize (one key repeated 4 Mi times: 3.7 ms, profiles/r05/insert_duplicates.jsonl)
 #pragma unroll
         for (uint32_t e = 0; e < kRunPad; e++) {
-          if (e < nreal[u]) {
+          if (e < nreal[u] && (!RPT_SLICE_INSERT_DEDUP || e == 0 || rec[u][e >> 2][e & 3] != rec[u][(e - 1) >> 2][(e - 1) & 3])) {
             const uint32_t rec1 = rec[u][e >> 2][e & 3];
             atomicOr(reinterpret_cast<unsigned long long*>(&s_slice[rec_word(rec1)]),
                      static_cast<unsigned long long>(rec_mask(s_rmasks, rec1)));
