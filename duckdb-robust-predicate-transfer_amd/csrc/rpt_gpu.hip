@@ -416,6 +416,11 @@ uint32_t bucket_count(int log_num_blocks) {
   return 1u << std::max(0, log_num_blocks - rpt::kSliceLog - rpt::kBucketSliceLog);
 }
 
+// (slice, split) work items of the slice probe: RPT_SLICE_SPLIT_MULT x one resident round (the grid stays one round
+// and walks them)
+#ifndef RPT_SLICE_SPLIT_MULT
+#define RPT_SLICE_SPLIT_MULT 1
+#endif
 int strategy_supported(int strategy, int log_num_blocks) {
   constexpr int kBucketLog = rpt::kSliceLog + rpt::kBucketSliceLog;  // log2 blocks per bucket (22)
   switch (strategy) {
@@ -1421,7 +1426,8 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     const uint64_t slice_lds = rpt::kSliceWords * 8 + 8ULL * rpt::kRotMasks;
     const uint64_t per_cu = std::max<uint64_t>(1, (160ULL << 10) / slice_lds);
     const uint64_t resident = static_cast<uint64_t>(cus) * per_cu;
-    const uint32_t splits = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, resident / grid_slices)));
+    const uint32_t splits = static_cast<uint32_t>(
+        std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, RPT_SLICE_SPLIT_MULT * resident / grid_slices)));
     const uint32_t n_items = grid_slices * splits;
     ProfScope prof6_("slice_probe_kernel", s);
     hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(n_items, resident))),
