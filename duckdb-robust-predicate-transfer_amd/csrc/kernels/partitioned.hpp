@@ -346,9 +346,14 @@ __global__ __launch_bounds__(kTileThreads, TM == 1 ? RPT_PARTITION_MIN_WAVES : 4
 }
 
 // runs_sm[slice][tile] = runs_tm[tile][slice], through 64 x 64 LDS tiles (both sides coalesced).
+// heavy != nullptr: a slice with a run longer than heavy_run in any tile is stamped heavy[slice] = epoch (a probe
+// key skewed onto that slice; the slice probe then gives it more work items). Stale stamps of other calls only
+// change how the work is divided, never a result.
 __global__ __launch_bounds__(kBlockThreads) void runs_transpose_kernel(const uint32_t* __restrict__ runs_tm,
                                                                       uint32_t n_slices, uint64_t n_tiles,
-                                                                      uint32_t* __restrict__ runs_sm) {
+                                                                      uint32_t* __restrict__ runs_sm,
+                                                                      uint32_t* __restrict__ heavy, uint32_t heavy_run,
+                                                                      uint32_t epoch) {
   __shared__ uint32_t s_t[64][65];
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * 64;
   const uint32_t s0 = blockIdx.y * 64;
@@ -360,7 +365,11 @@ __global__ __launch_bounds__(kBlockThreads) void runs_transpose_kernel(const uin
   __syncthreads();
   for (uint32_t r = r0; r < 64; r += 4) {
     const uint64_t t = t0 + c;
-    if (t < n_tiles && s0 + r < n_slices) runs_sm[static_cast<uint64_t>(s0 + r) * n_tiles + t] = s_t[c][r];
+    if (t < n_tiles && s0 + r < n_slices) {
+      const uint32_t v = s_t[c][r];
+      runs_sm[static_cast<uint64_t>(s0 + r) * n_tiles + t] = v;
+      if (heavy != nullptr && (v & 0xFFFFu) > heavy_run) heavy[s0 + r] = epoch;
+    }
   }
 }
 
@@ -492,14 +501,58 @@ __device__ __forceinline__ void probe_slice_runs_tbl(const uint64_t* s_slice, co
   }
 }
 
-// First work item >= item (stepping by gridDim.x) that has tiles; n_items if none.
-__device__ __forceinline__ uint32_t next_item(uint32_t item, uint32_t n_items, uint32_t splits, uint64_t n_tiles,
-                                              const uint32_t* bucket_tiles, SliceWork& sw) {
-  for (; item < n_items; item += gridDim.x) {
-    sw = slice_work(xcd_item(item, n_items), splits, n_tiles, bucket_tiles);
-    if (sw.t_lo < sw.t_hi) break;
+// Skewed probe keys (partitioned strategy): items [0, base) are the (slice, split) items above, except that a
+// heavy slice's are empty; items [base, base * (1 + mult)) split every slice mult times finer and are empty
+// except for the heavy slices'. A uniform batch (no heavy slice) keeps the base items' work.
+struct SkewItems {
+  const uint32_t* heavy = nullptr;  // nullptr: no skew handling (n_items == base)
+  uint32_t epoch = 0, base = 0, mult = 1;
+};
+__device__ __forceinline__ SliceWork slice_work_skew(uint32_t item, uint32_t splits, uint64_t n_tiles, const SkewItems& k) {
+  if (item < k.base) {
+    const uint32_t slice = item / splits, part = item % splits;
+    if (k.heavy[slice] == k.epoch) return SliceWork{slice, slice, 0, 0};
+    return SliceWork{slice, slice, n_tiles * part / splits, n_tiles * (part + 1) / splits};
   }
-  return item;
+  const uint32_t fs = splits * k.mult, x = item - k.base, slice = x / fs, part = x % fs;
+  if (k.heavy[slice] != k.epoch) return SliceWork{slice, slice, 0, 0};
+  return SliceWork{slice, slice, n_tiles * part / fs, n_tiles * (part + 1) / fs};
+}
+
+// First work item >= item (stepping by gridDim.x) that has tiles; n_items if none. With skew items most of the
+// fine items are empty: each lane of the wave tests one candidate (item + lane * gridDim.x) and a ballot picks
+// the first with tiles, one memory round trip per 64 candidates.
+__device__ __forceinline__ uint32_t next_item(uint32_t item, uint32_t n_items, uint32_t splits, uint64_t n_tiles,
+                                              const uint32_t* bucket_tiles, SliceWork& sw, const SkewItems& k) {
+  if (k.heavy == nullptr) {
+    for (; item < n_items; item += gridDim.x) {
+      sw = slice_work(xcd_item(item, n_items), splits, n_tiles, bucket_tiles);
+      if (sw.t_lo < sw.t_hi) break;
+    }
+    return item;
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  for (; item < n_items; item += 64 * gridDim.x) {
+    const uint64_t cand = static_cast<uint64_t>(item) + static_cast<uint64_t>(lane) * gridDim.x;
+    SliceWork w{0, 0, 0, 0};
+    if (cand < n_items) {  // each range XCD-mapped on its own: the base items land where they would without skew items
+      const uint32_t c = static_cast<uint32_t>(cand);
+      const uint32_t m = c < k.base ? xcd_item(c, k.base) : k.base + xcd_item(c - k.base, n_items - k.base);
+      w = slice_work_skew(m, splits, n_tiles, k);
+    }
+    const uint64_t has = __ballot(w.t_lo < w.t_hi);
+    if (has != 0) {
+      const int f = __builtin_ctzll(has);
+      sw.slice = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w.slice), f));
+      sw.run_row = sw.slice;
+      sw.t_lo = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w.t_lo >> 32), f))) << 32) |
+                static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(w.t_lo)), f));
+      sw.t_hi = (static_cast<uint64_t>(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(w.t_hi >> 32), f))) << 32) |
+                static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(static_cast<uint32_t>(w.t_hi)), f));
+      return item + static_cast<uint32_t>(f) * gridDim.x;
+    }
+  }
+  return n_items;
 }
 
 // Work items (slice, split) are walked by a resident grid; when a workgroup has several (filters with
@@ -512,7 +565,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
                                                                    uint8_t* __restrict__ passbits,
                                                                    uint32_t tile_cap,
                                                                    const uint32_t* __restrict__ bucket_tiles,
-                                                                   uint32_t n_items) {
+                                                                   uint32_t n_items, SkewItems skew) {
   // one LDS array, table first: the slice's base offset folds into the ds_read immediate
   __shared__ uint64_t s_lds[kRotMasks + kSliceWords];
   uint64_t* const s_rmasks = s_lds;
@@ -521,7 +574,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   __shared__ uint32_t s_win[kSliceThreads * RPT_SLICE_UNROLL];  // per-wave slot windows (16 KiB)
   constexpr uint32_t kPre = kSliceWords / 2 / kSliceThreads;  // 16-B pieces of a slice per thread
   SliceWork cur;
-  uint32_t item = next_item(blockIdx.x, n_items, splits, n_tiles, bucket_tiles, cur);
+  uint32_t item = next_item(blockIdx.x, n_items, splits, n_tiles, bucket_tiles, cur, skew);
   if (item >= n_items) return;  // uniform
   {
     const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(cur.slice) * kSliceWords);
@@ -532,7 +585,7 @@ __global__ __launch_bounds__(kSliceThreads) void slice_probe_kernel(const uint64
   while (true) {
     __syncthreads();
     SliceWork nxt;
-    const uint32_t nitem = next_item(item + gridDim.x, n_items, splits, n_tiles, bucket_tiles, nxt);
+    const uint32_t nitem = next_item(item + gridDim.x, n_items, splits, n_tiles, bucket_tiles, nxt, skew);
     u64x2 pre[kPre];
     if (nitem < n_items) {
       const u64x2* src = reinterpret_cast<const u64x2*>(words + static_cast<uint64_t>(nxt.slice) * kSliceWords);

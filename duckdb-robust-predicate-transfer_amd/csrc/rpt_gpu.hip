@@ -405,6 +405,7 @@ struct ProbeWorkspace {
   uint8_t* hash_hi;        // and bits 32..39
   uint16_t* pos1;          // row -> position in its level-1 tile's bucket-sorted order
   uint64_t* bits2;         // level-2 result bits (w-space order)
+  uint32_t* heavy;         // partitioned: [slice] epoch stamp of a slice skewed probe keys overload (rpt::SkewItems)
 };
 
 uint32_t slice_count(int log_num_blocks) {
@@ -421,6 +422,11 @@ uint32_t bucket_count(int log_num_blocks) {
 #ifndef RPT_SLICE_SPLIT_MULT
 #define RPT_SLICE_SPLIT_MULT 1
 #endif
+// Work items of a slice skewed probe keys overload: RPT_SLICE_SKEW_MULT x finer (1: off; rpt::SkewItems)
+#ifndef RPT_SLICE_SKEW_MULT
+#define RPT_SLICE_SKEW_MULT 8
+#endif
+std::atomic<uint32_t> g_skew_epoch{0};
 int strategy_supported(int strategy, int log_num_blocks) {
   constexpr int kBucketLog = rpt::kSliceLog + rpt::kBucketSliceLog;  // log2 blocks per bucket (22)
   switch (strategy) {
@@ -518,7 +524,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
   const uint64_t T = rpt::kTileRows;
-  constexpr int kParts = 20;
+  constexpr int kParts = 21;
   size_t sz[kParts] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
                        align256(n_groups * 4), align256(n_groups * 4)};
   const bool part = strategy == RPT_PROBE_PARTITIONED, buck = strategy == RPT_PROBE_BUCKETED;
@@ -532,6 +538,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     sz[6] = align256(tiles * cap / 8);
     sz[7] = align256(static_cast<uint64_t>(slices) * tiles * 4);
     sz[8] = sz[7];
+    if (part) sz[20] = align256(static_cast<uint64_t>(slices) * 4);
   }
   if (buck) {
     const L1Geom g = l1_geom(n, log_num_blocks);
@@ -574,6 +581,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     ws->pos1 = static_cast<uint16_t*>(at(17));
     ws->bits2 = static_cast<uint64_t*>(at(18));
     ws->hash_hi = static_cast<uint8_t*>(at(19));
+    ws->heavy = static_cast<uint32_t*>(at(20));
   }
   return total;
 }
@@ -820,11 +828,12 @@ void launch_bucket_scatter_t(unsigned grid, hipStream_t s, const rpt::KeyArgs& a
   } while (0)
 
 // [rows][cols] u32 matrix -> [cols][rows] (the run-table transpose kernel).
-int transpose_u32(hipStream_t s, const uint32_t* in, uint64_t rows, uint64_t cols, uint32_t* out) {
+int transpose_u32(hipStream_t s, const uint32_t* in, uint64_t rows, uint64_t cols, uint32_t* out, uint32_t* heavy = nullptr,
+                  uint32_t heavy_run = 0, uint32_t epoch = 0) {
   if (ceil_div(cols, 64) > 65535) return fail(RPT_ERR_INVALID_ARGUMENT, "transpose of %llu columns", (unsigned long long)cols);
   ProfScope prof_t("runs_transpose_kernel", s);
   hipLaunchKernelGGL(rpt::runs_transpose_kernel, dim3(static_cast<unsigned>(ceil_div(rows, 64)), static_cast<unsigned>(ceil_div(cols, 64))),
-                     dim3(rpt::kBlockThreads), 0, s, in, static_cast<uint32_t>(cols), rows, out);
+                     dim3(rpt::kBlockThreads), 0, s, in, static_cast<uint32_t>(cols), rows, out, heavy, heavy_run, epoch);
   prof_t.end();
   RPT_LAUNCHED("runs_transpose_kernel");
   return RPT_OK;
@@ -1419,7 +1428,16 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
       RPT_DISPATCH_KD(launch_partition_t, col->key_type, dense, static_cast<unsigned>(n_tiles), s, pa, n_part, tile_slices - 1,
                       n_tiles, ws.recs, ws.pos, ws.runs_tm, static_cast<int64_t*>(nullptr), dev_n_tiles, tm);
     RPT_LAUNCHED("partition_kernel");
-    int st2 = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs);
+    // skewed probe keys: slices whose run in some tile is over 4x the mean get mult x finer work items
+    rpt::SkewItems skew;
+    const bool skewed = !buck && RPT_SLICE_SKEW_MULT > 1 && tile_slices >= 16 && ws.heavy != nullptr;
+    if (skewed) {
+      skew.heavy = ws.heavy;
+      skew.epoch = g_skew_epoch.fetch_add(1) + 1;
+      skew.mult = RPT_SLICE_SKEW_MULT;
+    }
+    int st2 = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs, skewed ? ws.heavy : nullptr,
+                            static_cast<uint32_t>(4 * rpt::kTileRows * tm / tile_slices), skew.epoch);
     if (st2 != RPT_OK) return st2;
     // exactly one resident round of slice workgroups (LDS decides how many fit per CU), never more
     // splits than tiles
@@ -1428,11 +1446,12 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     const uint64_t resident = static_cast<uint64_t>(cus) * per_cu;
     const uint32_t splits = static_cast<uint32_t>(
         std::max<uint64_t>(1, std::min<uint64_t>(n_tiles, RPT_SLICE_SPLIT_MULT * resident / grid_slices)));
-    const uint32_t n_items = grid_slices * splits;
+    skew.base = grid_slices * splits;
+    const uint32_t n_items = skew.base * (skewed ? 1 + skew.mult : 1);
     ProfScope prof6_("slice_probe_kernel", s);
-    hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(n_items, resident))),
+    hipLaunchKernelGGL(rpt::slice_probe_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(skew.base, resident))),
                        dim3(rpt::kSliceThreads), 0, s, bf->words, splits, n_tiles, ws.recs, ws.runs, ws.passb,
-                       static_cast<uint32_t>(rpt::tile_cap_for(tile_slices, tm)), bucket_tiles, n_items);
+                       static_cast<uint32_t>(rpt::tile_cap_for(tile_slices, tm)), bucket_tiles, n_items, skew);
     prof6_.end();
     RPT_LAUNCHED("slice_probe_kernel");
     const uint64_t cap = rpt::tile_cap_for(tile_slices, tm);

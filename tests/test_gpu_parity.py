@@ -151,6 +151,29 @@ def test_large_filters_vs_oracle(rpt, strategy, log_nb):
     assert np.array_equal(sel, orc.probe_keys(w, log_nb, probe))
 
 
+@pytest.mark.parametrize("log_nb", [18, 21, 24])
+@pytest.mark.parametrize("hot", [0.0, 0.02, 0.3, 1.0])
+def test_skewed_probe_keys_vs_oracle(rpt, log_nb, hot):
+    """Probe keys skewed onto a few slices (a fraction `hot` of the rows on one key, a tenth of that on a second,
+    in and out of the filter): the partitioned probe then gives the overloaded slices finer work items
+    (rpt::SkewItems); the selection vector must stay the oracle's, over ragged tiles and repeated calls."""
+    rng = np.random.default_rng(int(hot * 100) + log_nb)
+    build = orc.synth_build_keys(200000)
+    n = 6 * 32768 + 777
+    probe = orc.synth_probe_keys(n, 200000, 300).copy()
+    u = rng.random(n)
+    probe[u < hot] = build[4242]
+    probe[(u >= hot) & (u < hot * 1.1)] = -99
+    bf = with_strategy(rpt.BloomFilter(log_num_blocks=log_nb), "partitioned")
+    bf.insert(dev(build))
+    w = orc.new_words(log_nb)
+    orc.insert_keys(w, log_nb, build)
+    want = orc.probe_keys(w, log_nb, probe)
+    for _ in range(2):
+        sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
+        assert np.array_equal(sel, want)
+
+
 @pytest.mark.parametrize("log_nb", [21, 22, 24])
 @pytest.mark.parametrize("nulls", [False, True])
 def test_large_filters_int32_vs_oracle(rpt, log_nb, nulls):
