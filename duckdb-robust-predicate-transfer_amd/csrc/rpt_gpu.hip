@@ -424,7 +424,7 @@ uint32_t bucket_count(int log_num_blocks) {
 #endif
 // Work items of a slice skewed probe keys overload: RPT_SLICE_SKEW_MULT x finer (1: off; rpt::SkewItems)
 #ifndef RPT_SLICE_SKEW_MULT
-#define RPT_SLICE_SKEW_MULT 8
+#define RPT_SLICE_SKEW_MULT 32
 #endif
 std::atomic<uint32_t> g_skew_epoch{0};
 int strategy_supported(int strategy, int log_num_blocks) {
