@@ -56,11 +56,15 @@ SEL_BYTES = 4           # uint32 sel entry written per survivor (algorithmic)
 C5_FILTER_ROWS = 8 * 10**9  # BASELINE config 4: the filter of 8e9 rows (2^30 blocks = 8 GiB)
 C5_ROWS_PER_RANK = 10**9
 
-CONFIGS = {  # name -> (global build rows at N GPUs, filter sized for, description)
+CONFIGS = {  # name -> (global build rows at N GPUs, filter sized for)
     "C2": (lambda n: 10**7, lambda n: 10**7),
     "C3": (lambda n: 10**8, lambda n: 10**8),
     "C5": (lambda n: n * 10**9, lambda n: 8 * 10**9),
+    # supplementary (not a BASELINE config): a JOB-sized dimension filter, 1e5 keys -> 128 KiB, the whole filter
+    # in LDS
+    "JOBDIM": (lambda n: 10**5, lambda n: 10**5),
 }
+STREAM_CAL_BYTES = 8 << 30  # stream calibration buffer (>= 8 GB: well past the 256 MiB Infinity Cache)
 
 
 def cpu_share() -> int:
@@ -120,7 +124,52 @@ def parse():
     ap.add_argument("--c5-merge-reps", type=int, default=3, help="C5 section: timed merges (after one warm-up)")
     ap.add_argument("--collective-timeout-ms", type=int, default=None,
                     help="bound of every OR all-reduce's waits (rpt_collective_set_timeout_ms; default the library's)")
+    ap.add_argument("--no-stream-calibration", action="store_true",
+                    help="skip the (untimed) read / copy stream calibration the roofline fractions are set beside")
     return ap.parse_args()
+
+
+def stream_calibration(device, nbytes: int = STREAM_CAL_BYTES, reps: int = 5) -> dict:
+    """What this box's HBM streams, measured in this process before the timed steps (so the kernels' fractions
+    of the 8 TB/s spec can be read against the box they ran on): a plain 16-B-load read stream over `nbytes`
+    (rpt_stream_read) and a read + write copy of nbytes / 2 into the other half (rpt_stream_copy), each the
+    best of `reps` after one warm-up, timed with HIP events on the launch stream."""
+    import torch
+
+    import rpt_amd
+    from rpt_amd._lib import check
+
+    lib = rpt_amd.load()
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    buf.fill_(0x5A)
+    sink = torch.empty(int(lib.rpt_stream_sink_words(device.index or 0)), dtype=torch.int64, device=device)
+    stream = torch.cuda.current_stream(device)
+    sh = stream.cuda_stream
+    half = nbytes // 2
+
+    def timed(fn):
+        fn()
+        best = float("inf")
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            fn()
+            b.record(stream)
+            b.synchronize()
+            best = min(best, a.elapsed_time(b) * 1e-3)
+        return best
+
+    t_read = timed(lambda: check(lib.rpt_stream_read(buf.data_ptr(), nbytes, sink.data_ptr(), sh)))
+    t_copy = timed(lambda: check(lib.rpt_stream_copy(buf.data_ptr() + half, buf.data_ptr(), half, sh)))
+    del buf, sink
+    torch.cuda.empty_cache()
+    return {
+        "read_GBps": nbytes / t_read / 1e9,
+        "copy_GBps": 2 * half / t_copy / 1e9,  # bytes read + bytes written
+        "bytes": nbytes,
+        "how": ("rpt_stream_read: 16-B non-temporal loads over 8 GiB, 4 x 256-thread workgroups per CU; "
+                "rpt_stream_copy: 4 GiB -> 4 GiB, read + write bytes; best of 5 after a warm-up, HIP events"),
+    }
 
 
 def config_tag(cfg: str, key_type: str) -> str:
@@ -240,9 +289,18 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
             allreduce_or_native(bf, comm, workspace=ws)
     else:
         ws = None
+        # the host-staged gloo composition of an 8 GiB filter takes many seconds per merge: rank 0 reports its
+        # rounds, so a long rehearsal keeps showing progress
+        t_m = [time.perf_counter()]
+
+        def progress(done, total):
+            if rank == 0 and (done == total or time.perf_counter() - t_m[0] > 10):
+                t_m[0] = time.perf_counter()
+                print(f"[bench c5] torch merge: {done}/{total} rounds at {t_m[0] - mem.t0:.1f} s", file=sys.stderr,
+                      flush=True)
 
         def merge():
-            allreduce_or_filter(bf)
+            allreduce_or_filter(bf, progress=progress)
     merge()  # warm-up merge: OR is idempotent, the words do not change
     mem.sample("merge")
     merge_s = []
@@ -254,19 +312,17 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
         torch.cuda.synchronize()
         merge_s.append(time.perf_counter() - t0)
     del ws
-    # untimed: the merged filter against a single build of all world * rows rows (inserted piece by piece)
+    torch.cuda.empty_cache()  # the merge's staging (RCCL rounds, or the torch composition's word copy)
+    # untimed: the merged filter against a single build of all world * rows rows (inserted piece by piece),
+    # compared on the device (rpt_bf_is_same_as: no word copies, so a rank holds its filter + the reference)
     ref = rpt_amd.BloomFilter(C5_FILTER_ROWS, device=device)
     for r in range(world):
         rpt_amd.synth_build_keys(rows, start=r * rows, device=device, out=keys)
         ref.insert(keys)
     del keys
-    a = torch.empty(bf.num_blocks, dtype=torch.int64, device=device)
-    b = torch.empty_like(a)
-    bf.copy_words_to(a)
-    ref.copy_words_to(b)
-    same = bool(torch.equal(a, b)) and bf.minmax() == ref.minmax() and not bf.is_empty()
+    same = bf.is_same_as(ref) and bf.minmax() == ref.minmax() and not bf.is_empty()
     mem.sample("merge_check")
-    del a, b, ref
+    del ref
     torch.cuda.empty_cache()
     ok = all_ok(same)
     check = ("bit-identical (words + key min/max) to a single-GPU build of all rows on every rank" if ok
@@ -499,6 +555,12 @@ def main():
     def keys_of(t):
         return t.to(torch.int32) if args.key_type == "i32" else t
 
+    # ---- what this box streams (untimed, before anything else is resident) ------------------------
+    shared_device = backend == "gloo" and world > max(1, torch.cuda.device_count())
+    stream_cal = None
+    if not args.no_stream_calibration and not shared_device:
+        stream_cal = stream_calibration(device)
+
     # ---- CREATE_BF: sharded build + OR merge (reported, not the headline) -------------------------
     lo, hi = shard_range(n_build, rank, world)
     build_keys = keys_of(rpt_amd.synth_build_keys(hi - lo, start=lo, device=device))
@@ -551,16 +613,12 @@ def main():
         piece = 10**9
         for s0 in range(0, n_build, piece):
             ref.insert(keys_of(rpt_amd.synth_build_keys(min(piece, n_build - s0), start=s0, device=device)))
-        a = torch.empty(bf.num_blocks, dtype=torch.int64, device=device)
-        b = torch.empty_like(a)
-        bf.copy_words_to(a)
-        ref.copy_words_to(b)
-        same = torch.equal(a, b) and bf.minmax() == ref.minmax()
+        same = bf.is_same_as(ref) and bf.minmax() == ref.minmax()  # rpt_bf_is_same_as: compared on the device
         ok = torch.tensor([1 if same else 0], dtype=torch.int64, device=device if backend == "nccl" else "cpu")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         merge_check = ("bit-identical (words + key min/max) to a single-GPU build of all rows on every rank"
                        if ok.item() else "MISMATCH")
-        del ref, a, b
+        del ref
         torch.cuda.empty_cache()
         if not ok.item():
             raise SystemExit("OR-merged filter differs from the single-GPU build")
@@ -693,6 +751,9 @@ def main():
                              f"per GPU against a blocked Bloom filter built from {n_build:.0e} keys (sized for "
                              f"{n_filter:.0e}: 2^{bf.log_num_blocks} blocks = {filter_bytes / 2**20:.0f} MiB), p={args.p}"),
                 "config": cfg,
+                "supplementary": (None if cfg != "JOBDIM" else
+                                  "not a BASELINE config: a JOB-sized dimension filter (1e5 keys, 128 KiB, whole "
+                                  "filter in LDS), where the 60 % whole-probe target is plausible"),
                 "probe_rows_per_gpu": n_probe,
                 "build_rows": n_build,
                 "filter_bytes": filter_bytes,
@@ -714,7 +775,17 @@ def main():
                 "avg_launch_ms": dom_ms,
                 "launches_per_step": dom_calls_per_step,
                 "algorithmic_bytes_per_launch": dom_bytes,
+                # the same kernel against what this box streams (measured in this process, untimed): separates the
+                # box from the code
+                "stream_GBps": stream_cal["read_GBps"] if stream_cal else None,
+                "copy_GBps": stream_cal["copy_GBps"] if stream_cal else None,
+                "frac_of_stream": achieved / 1e9 / stream_cal["read_GBps"] if stream_cal else None,
+                # the kernel's real HBM traffic rate (PMC bytes / its duration) against the box's read + write copy
+                "traffic_frac_of_copy": (traffic["bytes_per_launch"] / (dom_ms * 1e-3) / 1e9 / stream_cal["copy_GBps"]
+                                         if stream_cal and traffic else None),
             },
+            "stream_calibration": stream_cal if stream_cal else (
+                "skipped: ranks share one GPU (gloo rehearsal)" if shared_device else "skipped (--no-stream-calibration)"),
             "kernels_ms": {k: v[1] / v[0] for k, v in sorted(ktimes.items(), key=lambda kv: -kv[1][1])},
             "kernels_launches_per_step": {k: v[0] / args.steps for k, v in ktimes.items()},
             "probe_total": {
@@ -722,9 +793,12 @@ def main():
                 "algorithmic_bytes": probe_bytes,
                 "achieved_GBps": probe_bytes / (probe_ms * 1e-3) / 1e9,
                 "frac": probe_bytes / (probe_ms * 1e-3) / HBM_PEAK_BPS,
+                "frac_of_stream": probe_bytes / (probe_ms * 1e-3) / 1e9 / stream_cal["read_GBps"] if stream_cal else None,
                 # HBM bytes the whole step moves (PMC, every kernel) and their rate over the step
                 "traffic": step_traffic if not unprofiled else None,
                 "traffic_GBps": step_traffic / (probe_ms * 1e-3) / 1e9 if not unprofiled else None,
+                "traffic_frac_of_copy": (step_traffic / (probe_ms * 1e-3) / 1e9 / stream_cal["copy_GBps"]
+                                         if stream_cal and not unprofiled else None),
                 "traffic_unprofiled_kernels": unprofiled,
             },
             "build": {

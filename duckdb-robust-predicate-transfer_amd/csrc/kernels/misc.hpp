@@ -128,6 +128,69 @@ __global__ __launch_bounds__(kBlockThreads) void popcount_kernel(const uint64_t*
   }
 }
 
+// ---- word equality (BlockedBloomFilter::IsSameAs) -------------------------------------------------
+// Number of word positions where a and b differ, 16-B loads (both 16-B aligned: filters are hipMalloc'd).
+__global__ __launch_bounds__(kBlockThreads) void diff_count_kernel(const uint64_t* __restrict__ a,
+                                                                  const uint64_t* __restrict__ b, uint64_t n_words,
+                                                                  unsigned long long* __restrict__ out) {
+  __shared__ uint32_t s_part[kWavesPerBlock];
+  uint32_t d = 0;
+  const uint64_t n_pairs = n_words / 2;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n_pairs; i += stride) {
+    const u64x2 x = reinterpret_cast<const u64x2*>(a)[i], y = reinterpret_cast<const u64x2*>(b)[i];
+    d += (x[0] != y[0]) + (x[1] != y[1]);
+  }
+  if ((n_words & 1) && blockIdx.x == 0 && threadIdx.x == 0) d += a[n_words - 1] != b[n_words - 1];
+  d = wave_sum(d);
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = d;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+    if (t) atomicAdd(out, static_cast<unsigned long long>(t));
+  }
+}
+
+// ---- stream calibration (bench.py: the box's achievable HBM rates beside the kernels' fractions) --
+// Read: every lane streams 16-B non-temporal loads, 4 in flight, and folds them into one word per
+// workgroup (written, so nothing is dead code). Copy: the same loads stored to dst (non-temporal).
+// n16: number of 16-B units; grid-stride over them.
+constexpr int kStreamUnroll = 4;
+__global__ __launch_bounds__(kBlockThreads) void stream_read_kernel(const u64x2* __restrict__ src, uint64_t n16,
+                                                                   uint64_t* __restrict__ sink) {
+  __shared__ uint64_t s_part[kWavesPerBlock];
+  u64x2 acc = {0, 0};
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + (kStreamUnroll - 1) * stride < n16; i += kStreamUnroll * stride) {
+    u64x2 v[kStreamUnroll];
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; u++) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; u++) acc ^= v[u];
+  }
+  for (; i < n16; i += stride) acc ^= __builtin_nontemporal_load(src + i);
+  uint64_t x = acc[0] ^ acc[1];
+  for (int off = 32; off > 0; off >>= 1) x ^= shfl_u64(x, static_cast<int>(((threadIdx.x + off) & 63) << 2));
+  if ((threadIdx.x & 63) == 0) s_part[threadIdx.x >> 6] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) sink[blockIdx.x] = s_part[0] ^ s_part[1] ^ s_part[2] ^ s_part[3];
+}
+
+__global__ __launch_bounds__(kBlockThreads) void stream_copy_kernel(const u64x2* __restrict__ src, uint64_t n16,
+                                                                   u64x2* __restrict__ dst) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  for (; i + (kStreamUnroll - 1) * stride < n16; i += kStreamUnroll * stride) {
+    u64x2 v[kStreamUnroll];
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; u++) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < kStreamUnroll; u++) __builtin_nontemporal_store(v[u], dst + i + u * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 // ---- synthetic workload (bench / tests) ----------------------------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;

@@ -233,6 +233,18 @@ bool stream_capturing(hipStream_t s) {
   return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 
+// Has `ev` (recorded outside any capture) completed, asked while the calling thread's stream is capturing?
+// Querying an event is a potentially unsafe call under hipStreamCaptureModeGlobal (torch.cuda.graph's default)
+// and would invalidate the caller's capture, so the thread's capture mode is relaxed around the query and
+// restored after it.
+bool event_done_during_capture(hipEvent_t ev) {
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
+  const bool done = hipEventQuery(ev) == hipSuccess;
+  if (swapped) (void)hipThreadExchangeStreamCaptureMode(&mode);
+  return done;
+}
+
 // Writes captured into a graph. A graph replays its kernels, not this library's host-side
 // bookkeeping, so a captured write must not depend on host state that changes between replays:
 // * a deferred clear (clear_pending) would be settled by a memset (or whole-slice stores) recorded in the
@@ -251,7 +263,7 @@ int refuse_capture_write(rpt_bf* bf, hipStream_t s, const char* what) {
     return fail(RPT_ERR_INVALID_ARGUMENT,
                 "%s of a cleared filter inside stream capture: call rpt_bf_settle() before capturing", what);
   std::lock_guard<std::mutex> lk(bf->order_mu);
-  if (bf->order_pending && hipEventQuery(bf->order_ev) != hipSuccess)
+  if (bf->order_pending && !event_done_during_capture(bf->order_ev))
     return fail(RPT_ERR_INVALID_ARGUMENT,
                 "%s inside stream capture while an earlier write to the filter is in flight: synchronize it (or "
                 "call rpt_bf_settle()) before capturing", what);
@@ -285,7 +297,7 @@ struct WriteOrder {
   WriteOrder(rpt_bf* b, hipStream_t st) : bf(b), s(st), lk(b->order_mu), captured(stream_capturing(st)) {
     if (!bf->order_pending) return;
     if (!captured) (void)hipStreamWaitEvent(s, bf->order_ev, 0);
-    else in_flight = hipEventQuery(bf->order_ev) != hipSuccess;
+    else in_flight = !event_done_during_capture(bf->order_ev);
   }
   // pristine_after: every word is zero once this operation completes
   void done(bool pristine_after) {
@@ -1433,8 +1445,15 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     const bool skewed = !buck && RPT_SLICE_SKEW_MULT > 1 && tile_slices >= 16 && ws.heavy != nullptr;
     if (skewed) {
       skew.heavy = ws.heavy;
-      skew.epoch = g_skew_epoch.fetch_add(1) + 1;
       skew.mult = RPT_SLICE_SKEW_MULT;
+      if (stream_capturing(s)) {
+        // a graph replays the epoch it was captured with: the stamps are reset by a captured
+        // memset instead, so every replay stamps only the slices its own keys overload
+        skew.epoch = 1;
+        RPT_HIP(hipMemsetAsync(ws.heavy, 0, sizeof(uint32_t) * tile_slices, s));
+      } else {
+        skew.epoch = g_skew_epoch.fetch_add(1) + 1;  // a fresh stamp per call: nothing to clear
+      }
     }
     int st2 = transpose_u32(s, ws.runs_tm, n_tiles, tile_slices, ws.runs, skewed ? ws.heavy : nullptr,
                             static_cast<uint32_t>(4 * rpt::kTileRows * tm / tile_slices), skew.epoch);
@@ -2280,6 +2299,39 @@ int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out) {
   return RPT_OK;
 }
 
+int rpt_bf_is_same_as(const rpt_bf* a, const rpt_bf* b, int* out_same, uint64_t* out_diff_words) {
+  if (!a || !b || !out_same) return fail(RPT_ERR_INVALID_ARGUMENT, "null argument");
+  *out_same = 0;
+  if (out_diff_words) *out_diff_words = 0;
+  if (a->device != b->device) return fail(RPT_ERR_SHAPE_MISMATCH, "filters on devices %d and %d", a->device, b->device);
+  if (a->log_num_blocks != b->log_num_blocks) {  // Arrow IsSameAs: different geometry is simply not the same
+    if (out_diff_words) *out_diff_words = ~0ULL;
+    return RPT_OK;
+  }
+  RPT_ON_DEVICE(a->device);
+  RPT_SETTLE(a, nullptr);
+  RPT_SETTLE(b, nullptr);
+  RPT_HIP(hipDeviceSynchronize());  // every stream's writes to either filter have landed
+  unsigned long long* d = nullptr;
+  RPT_HIP(hipMalloc(&d, sizeof(unsigned long long)));
+  hipError_t e = hipMemset(d, 0, sizeof(unsigned long long));
+  const uint64_t nw = 1ULL << a->log_num_blocks;
+  const unsigned grid =
+      static_cast<unsigned>(std::max<uint64_t>(1, std::min<uint64_t>(ceil_div(nw / 2, rpt::kBlockThreads),
+                                                                      static_cast<uint64_t>(num_cus(a->device)) * rpt::kBlocksPerCU)));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(rpt::diff_count_kernel, dim3(grid), dim3(rpt::kBlockThreads), 0, nullptr, a->words, b->words, nw, d);
+    e = hipGetLastError();
+  }
+  unsigned long long h = 0;
+  if (e == hipSuccess) e = hipMemcpy(&h, d, sizeof h, hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(RPT_ERR_HIP, "is_same_as: %s", hipGetErrorString(e));
+  *out_same = h == 0;
+  if (out_diff_words) *out_diff_words = h;
+  return RPT_OK;
+}
+
 int rpt_bf_fold(rpt_bf* bf, int* out_new_log_num_blocks) {
   if (!bf) return fail(RPT_ERR_INVALID_ARGUMENT, "null filter");
   RPT_ON_DEVICE(bf->device);
@@ -2443,6 +2495,45 @@ int rpt_synth_probe_keys(int64_t* out, uint64_t n_build, uint32_t p_permille, ui
                      p_permille, start, n);
   prof16_.end();
   RPT_LAUNCHED("synth_probe_kernel");
+  return RPT_OK;
+}
+
+uint64_t rpt_stream_sink_words(int device) { return static_cast<uint64_t>(num_cus(device)) * rpt::kBlocksPerCU; }
+
+static int stream_check(const void* p, uint64_t bytes, int* dev) {
+  if (!p) return fail(RPT_ERR_INVALID_ARGUMENT, "null pointer");
+  if ((reinterpret_cast<uintptr_t>(p) & 15) || (bytes & 15))
+    return fail(RPT_ERR_INVALID_ARGUMENT, "stream calibration needs 16-B aligned pointers and sizes");
+  RPT_HIP(hipGetDevice(dev));
+  return RPT_OK;
+}
+
+int rpt_stream_read(const void* src, uint64_t bytes, uint64_t* sink, rpt_stream_t stream) {
+  int dev = 0;
+  int st = stream_check(src, bytes, &dev);
+  if (st != RPT_OK) return st;
+  if (!sink) return fail(RPT_ERR_INVALID_ARGUMENT, "null sink");
+  if (bytes == 0) return RPT_OK;
+  ProfScope prof_("stream_read_kernel", as_stream(stream));
+  hipLaunchKernelGGL(rpt::stream_read_kernel, dim3(static_cast<unsigned>(rpt_stream_sink_words(dev))),
+                     dim3(rpt::kBlockThreads), 0, as_stream(stream), static_cast<const rpt::u64x2*>(src), bytes / 16, sink);
+  prof_.end();
+  RPT_LAUNCHED("stream_read_kernel");
+  return RPT_OK;
+}
+
+int rpt_stream_copy(void* dst, const void* src, uint64_t bytes, rpt_stream_t stream) {
+  int dev = 0;
+  int st = stream_check(src, bytes, &dev);
+  if (st == RPT_OK) st = stream_check(dst, bytes, &dev);
+  if (st != RPT_OK) return st;
+  if (bytes == 0) return RPT_OK;
+  ProfScope prof_("stream_copy_kernel", as_stream(stream));
+  hipLaunchKernelGGL(rpt::stream_copy_kernel, dim3(static_cast<unsigned>(rpt_stream_sink_words(dev))),
+                     dim3(rpt::kBlockThreads), 0, as_stream(stream), static_cast<const rpt::u64x2*>(src), bytes / 16,
+                     static_cast<rpt::u64x2*>(dst));
+  prof_.end();
+  RPT_LAUNCHED("stream_copy_kernel");
   return RPT_OK;
 }
 

@@ -1708,6 +1708,11 @@ bool CreateBF::WillResize(size_t i, uint64_t actual_rows) const {
 
 void CreateBF::Finalize() {
   const uint64_t actual_rows = total_rows_;
+  // The sink skipped inserts once the rows flushed by every state made the resize certain (Flush). Those rows
+  // reach the filter only through the rehash below, so a filter is rehashed whenever any insert was skipped,
+  // even if the rows actually combined no longer call for the resize (a state that flushed but never combined:
+  // flushed_rows_ > total_rows_). Fail safe: a false negative is never possible.
+  const bool skipped = skipped_insert_rows_.load() > 0;
   if (actual_rows > 0) {
     std::unique_ptr<DeviceContext> ctx;  // made only when a filter is rehashed
     for (size_t i = 0; i < filters_.size(); i++) {
@@ -1715,10 +1720,12 @@ void CreateBF::Finalize() {
       // physical_create_bf.cpp:383-398: resize iff the allocated filter gives < 8 bits per actual row,
       // on this filter's real allocation (default) or by the reference's formula verbatim (ResizeRule);
       // the rehash reads the build column from HBM
-      if (WillResize(i, actual_rows)) {
+      const bool resize = WillResize(i, actual_rows);
+      if (resize || skipped) {
         if (!ctx) ctx = std::make_unique<DeviceContext>(device_);
-        bf.ReinitializeAndRehash(*ctx, actual_rows, all_keys_[i]);
-        resized_[i] = true;
+        // no resize: rehash into a filter of the same size (reinitialized for the estimate it was sized for)
+        bf.ReinitializeAndRehash(*ctx, resize ? actual_rows : bf.SizedForRows(), all_keys_[i]);
+        resized_[i] = resize;
       }
     }
   }
@@ -2281,7 +2288,10 @@ uint64_t UseBF::ExecuteChainPipelined(DeviceContext& ctx, const std::vector<cons
     }
     for (size_t i = st.size() > kNB ? st.size() - kNB : 0; i < st.size(); i++) advance(ch[i % kNB], true);
   } catch (...) {
-    for (hipStream_t x : {h, cs[0], cs[1]}) (void)hipStreamSynchronize(x);  // nothing may still use the staging buffers
+    // nothing may still use the staging buffers: the copy stream and EVERY stage stream (the third
+    // stage's stream was left running, so its late copies could land in the next call's pinned buffers)
+    (void)hipStreamSynchronize(h);
+    for (int b = 0; b < kNB; b++) (void)hipStreamSynchronize(cs[b]);
     throw;
   }
   ps.stages += st.size();

@@ -140,6 +140,7 @@ SIGNATURES = {
     "rpt_words_or": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
     "rpt_words_or_slices": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p]),
     "rpt_bf_count_bits": (c_int, [c_void_p, POINTER(c_uint64)]),
+    "rpt_bf_is_same_as": (c_int, [c_void_p, c_void_p, POINTER(c_int), POINTER(c_uint64)]),
     "rpt_bf_fold": (c_int, [c_void_p, POINTER(c_int)]),
     "rpt_bf_export_words": (c_int, [c_void_p, c_void_p, c_uint64]),
     "rpt_bf_import_words": (c_int, [c_void_p, c_void_p, c_uint64]),
@@ -151,6 +152,9 @@ SIGNATURES = {
     "rpt_profiling_read": (c_int, [POINTER(KernelStat), c_int]),
     "rpt_synth_build_keys": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
     "rpt_synth_probe_keys": (c_int, [c_void_p, c_uint64, c_uint32, c_uint64, c_uint64, c_void_p]),
+    "rpt_stream_sink_words": (c_uint64, [c_int]),
+    "rpt_stream_read": (c_int, [c_void_p, c_uint64, c_void_p, c_void_p]),
+    "rpt_stream_copy": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p]),
 }
 
 _lib = None

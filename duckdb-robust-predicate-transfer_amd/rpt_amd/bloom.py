@@ -343,6 +343,18 @@ class BloomFilter:
         check(self._lib.rpt_bf_count_bits(self._h, ctypes.byref(v)))
         return v.value
 
+    def is_same_as(self, other: "BloomFilter") -> bool:
+        """BlockedBloomFilter::IsSameAs on the device (rpt_bf_is_same_as): same geometry, every word equal."""
+        same, diff = ctypes.c_int(), ctypes.c_uint64()
+        check(self._lib.rpt_bf_is_same_as(self._h, other._h, ctypes.byref(same), ctypes.byref(diff)))
+        return bool(same.value)
+
+    def diff_words(self, other: "BloomFilter") -> int:
+        """Number of words that differ from `other` (rpt_bf_is_same_as; 2^64 - 1 for different geometry)."""
+        same, diff = ctypes.c_int(), ctypes.c_uint64()
+        check(self._lib.rpt_bf_is_same_as(self._h, other._h, ctypes.byref(same), ctypes.byref(diff)))
+        return diff.value
+
     def fold(self) -> int:
         v = ctypes.c_int()
         check(self._lib.rpt_bf_fold(self._h, ctypes.byref(v)))

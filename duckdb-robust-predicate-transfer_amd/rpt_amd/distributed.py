@@ -206,17 +206,19 @@ def allreduce_or_native(bf, comm: RcclComm, stream=None, workspace: Optional[tor
 TORCH_MERGE_ROUND_WORDS = 32 << 20  # 256 MiB of words per round of the torch composition
 
 
-def or_allreduce_words_rounds(full: torch.Tensor, group=None, round_words: int = TORCH_MERGE_ROUND_WORDS) -> None:
+def or_allreduce_words_rounds(full: torch.Tensor, group=None, round_words: int = TORCH_MERGE_ROUND_WORDS,
+                              progress: Optional[Callable[[int, int], None]] = None) -> None:
     """or_allreduce_words over `full` in rounds of at most round_words words (rounded down to a multiple of the
     world size, at least one word per rank). A CUDA tensor under a gloo group is staged through host memory one
-    round at a time; a CPU tensor is reduced in place."""
+    round at a time; a CPU tensor is reduced in place. progress(done, total) is called after every round."""
     world = dist.get_world_size(group)
     total = full.numel()
     if total % world:
         raise ValueError("word count must be a multiple of the world size (use padded_words)")
     stage = full.is_cuda and dist.get_backend(group) == "gloo"
     step = max(world, (int(round_words) // world) * world)
-    for lo in range(0, total, step):
+    rounds = (total + step - 1) // step
+    for i, lo in enumerate(range(0, total, step)):
         view = full[lo: min(total, lo + step)]  # a multiple of world words: total and step both are
         if stage:
             host = view.cpu()
@@ -224,9 +226,12 @@ def or_allreduce_words_rounds(full: torch.Tensor, group=None, round_words: int =
             view.copy_(host)
         else:
             or_allreduce_words(view, group)
+        if progress is not None:
+            progress(i + 1, rounds)
 
 
-def allreduce_or_filter(bf, group=None, round_words: int = TORCH_MERGE_ROUND_WORDS) -> None:
+def allreduce_or_filter(bf, group=None, round_words: int = TORCH_MERGE_ROUND_WORDS,
+                        progress: Optional[Callable[[int, int], None]] = None) -> None:
     """OR-merge a BloomFilter across all ranks (all ranks must hold the same log_num_blocks), and
     reduce its has_data flag and key min/max (CreateBF Combine, physical_create_bf.cpp:244-275).
 
@@ -239,7 +244,7 @@ def allreduce_or_filter(bf, group=None, round_words: int = TORCH_MERGE_ROUND_WOR
     buf = torch.zeros(padded_words(bf.num_blocks, world), dtype=torch.int64, device=bf.device)
     bf.copy_words_to(buf)
     on_device = dist.get_backend(group) != "gloo"
-    or_allreduce_words_rounds(buf, group, round_words)
+    or_allreduce_words_rounds(buf, group, round_words, progress)
     bf.copy_words_from(buf)
     del buf
     mm, has = allreduce_minmax_flag(bf.minmax(), not bf.is_empty(), group,

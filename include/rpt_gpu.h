@@ -345,6 +345,11 @@ int rpt_words_or(uint64_t* dst, const uint64_t* src, uint64_t n_words, rpt_strea
 /* dst[i] = src_0[i] | src_1[i] | ... | src_{k-1}[i], srcs given as k contiguous slices of
  * n_words words starting at `srcs` (a receive buffer of k peer slices). */
 int rpt_words_or_slices(uint64_t* dst, const uint64_t* srcs, uint32_t k, uint64_t n_words, rpt_stream_t stream);
+/* BlockedBloomFilter::IsSameAs (pyarrow 25 arrow/acero/bloom_filter.h:131): *out_same = 1 iff both filters
+ * have the same log_num_blocks and every word is equal, compared on the device (no host copy of either
+ * filter; bench.py's multi-GPU merge check of C5's 8 GiB filters). *out_diff_words (nullable) = the number of
+ * differing words (~0 for different geometry). Filters on one device. Synchronous (waits for the device). */
+int rpt_bf_is_same_as(const rpt_bf* a, const rpt_bf* b, int* out_same, uint64_t* out_diff_words);
 /* Number of set bits (BlockedBloomFilter::NumBitsSet). Synchronous. */
 int rpt_bf_count_bits(const rpt_bf* bf, uint64_t* out);
 /* BlockedBloomFilter::Fold (bloom_filter.h:135-158): while fewer than 1/4 of the bits are set and

@@ -30,6 +30,14 @@ int rpt_synth_build_keys(int64_t* out, uint64_t start, uint64_t n, rpt_stream_t 
 int rpt_synth_probe_keys(int64_t* out, uint64_t n_build, uint32_t p_permille, uint64_t start, uint64_t n,
                          rpt_stream_t stream);
 
+/* Stream calibration (bench.py reports the kernels' HBM fractions against what this box streams, beside the
+ * 8 TB/s spec): read `bytes` bytes at `src` with 16-B non-temporal loads over a grid of 4 x 256-thread
+ * workgroups per CU (sink: one word per workgroup, rpt_stream_sink_words(device) words), or copy them to
+ * `dst`. Device pointers, 16-B aligned, bytes a multiple of 16. Stream-ordered, no sync. */
+uint64_t rpt_stream_sink_words(int device);
+int rpt_stream_read(const void* src, uint64_t bytes, uint64_t* sink, rpt_stream_t stream);
+int rpt_stream_copy(void* dst, const void* src, uint64_t bytes, rpt_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,8 +7,8 @@ rows on every rank, and every rank probes its slice (the cross-GPU counterpart o
 reference src/operators/physical_create_bf.cpp:244-275). The driver's 8-GPU node runs it over RCCL; a
 one-GPU box cannot (RCCL refuses two ranks on one device), so here the same script runs with
 RPT_BENCH_BACKEND=gloo: N ranks share cuda:0, and every merge is the torch.distributed composition
-(reported as torch_merge_ms, never as or_merge_ms). What this executes at N = 2 and 3 is everything of that
-run except the RCCL transport: the rank launch, the sharding, the merge check, the reductions over ranks,
+(reported as torch_merge_ms, never as or_merge_ms). What this executes at N = 2, 4 and 8 (the driver's scaling
+run makes N = 2, 4, 8) is everything of that run except the RCCL transport: the rank launch, the sharding, the merge check, the reductions over ranks,
 the per-rank device-memory report and the record assembly.
 
 bench.py starts its ranks itself (torch.distributed.run, before any GPU call in the ranks); this test starts
@@ -53,7 +53,7 @@ def run_bench(world: int, tmp_path):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_multi_rank_rehearsal(world, tmp_path):
     t0 = time.monotonic()
     line = run_bench(world, tmp_path)
@@ -63,6 +63,9 @@ def test_bench_multi_rank_rehearsal(world, tmp_path):
     assert line["build"]["merge_check"].startswith("bit-identical"), line["build"]
     assert line["build"]["or_merge_ms"] is None and line["build"]["torch_merge_ms"] > 0
     assert "cpu_baseline" not in line
+    # ranks sharing one GPU: the stream calibration would time 8 concurrent streams, so it is skipped and says so
+    assert line["stream_calibration"].startswith("skipped: ranks share one GPU"), line["stream_calibration"]
+    assert line["roofline"]["stream_GBps"] is None
     # the C5 section at this N
     c5 = line["c5_merge"]
     assert c5["n_gpus"] == world and c5["rows_per_rank"] == ROWS and c5["build_rows"] == world * ROWS

@@ -202,8 +202,9 @@ def test_clear_settled_by_a_reader_orders_other_streams(rpt):
     assert not out.any()
 
 
+@pytest.mark.parametrize("mode", [2, 0])  # hipStreamCaptureModeRelaxed, hipStreamCaptureModeGlobal (torch's default)
 @pytest.mark.parametrize("log_nb,n", [(14, 200_000), (21, 5_000_000)])  # LDS probe; partitioned probe
-def test_graph_capture_of_a_cleared_filter(rpt, log_nb, n):
+def test_graph_capture_of_a_cleared_filter(rpt, log_nb, n, mode):
     """a probe captured into a HIP graph must not carry the deferred clear's zeroing (each replay
     would wipe the bits inserted since). A capture that would have to settle the clear is refused
     (RPT_ERR_INVALID_ARGUMENT, the capture itself stays valid); after rpt_bf_settle the probe captures, and
@@ -232,7 +233,7 @@ def test_graph_capture_of_a_cleared_filter(rpt, log_nb, n):
     graph, exe = ctypes.c_void_p(), ctypes.c_void_p()
 
     def capture():
-        assert hip.hipStreamBeginCapture(sh, 2) == 0  # hipStreamCaptureModeRelaxed
+        assert hip.hipStreamBeginCapture(sh, mode) == 0
         err = None
         try:
             bf.probe_async(kp, n=n, out_sel=out_sel, out_count=out_count, workspace=ws, stream=s)
@@ -264,9 +265,10 @@ def test_graph_capture_of_a_cleared_filter(rpt, log_nb, n):
     assert hip.hipGraphExecDestroy(exe) == 0 and hip.hipGraphDestroy(graph) == 0
 
 
+@pytest.mark.parametrize("mode", [2, 0])  # relaxed; global, where the library's event query must not break the capture
 @pytest.mark.parametrize("strategy,log_nb", [(INS_ATOMIC, 22), (INS_PARTITIONED, 21), (INS_PARTITIONED, 24),
                                              (INS_BUCKETED, 25)])
-def test_graph_capture_of_inserts(rpt, strategy, log_nb):
+def test_graph_capture_of_inserts(rpt, strategy, log_nb, mode):
     """writes captured into a HIP graph. (1) An insert captured after a clear is refused (its
     settling memset / whole-slice stores would replay with the graph and wipe what was inserted between
     replays), and so is a clear inside a capture; each capture stays valid. (2) After rpt_bf_settle the insert
@@ -296,7 +298,7 @@ def test_graph_capture_of_inserts(rpt, strategy, log_nb):
 
     def capture(op):
         torch.cuda.synchronize()
-        assert hip.hipStreamBeginCapture(sh, 2) == 0  # hipStreamCaptureModeRelaxed
+        assert hip.hipStreamBeginCapture(sh, mode) == 0
         st = op()
         assert hip.hipStreamEndCapture(sh, ctypes.byref(graph)) == 0  # still a valid capture
         return st

@@ -174,6 +174,117 @@ def test_skewed_probe_keys_vs_oracle(rpt, log_nb, hot):
         assert np.array_equal(sel, want)
 
 
+def _skewed_column(rpt, n, n_build, hot, hot_key, miss_share=0.1, seed=1):
+    """n synthetic probe keys (p = 0.1) on the device with a fraction `hot` of the rows replaced by hot_key and
+    a further hot * miss_share by a key that is in no filter (-99): the shape of a foreign-key column's hot
+    values (physical_use_bf.cpp:163 probes whatever the column holds)."""
+    probe = rpt.synth_probe_keys(n, n_build, 100)
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(seed)
+    u = torch.rand(n, device="cuda:0", generator=g)
+    probe[u < hot] = hot_key
+    probe[(u >= hot) & (u < hot * (1 + miss_share))] = -99
+    del u
+    return probe
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("log_nb,n_build", [(21, 10**7), (24, 10**8)])
+@pytest.mark.parametrize("hot", [0.1, 1.0])
+def test_full_size_skewed_probe_vs_oracle(rpt, log_nb, n_build, hot):
+    """one hot key on 10 % / 100 % of 2^27 + 777 probe rows against C2's 16 MiB (2^21 blocks)
+    and C3's 128 MiB (2^24) filters, AUTO strategy (partitioned: 2^13 tiles, the hot slice stamped and split into
+    the 32x finer skew items), every row against the oracle, twice (the second call's stamps are fresh)."""
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    n = 2**27 + 777
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    build = rpt.synth_build_keys(n_build)
+    bf.insert(build)
+    hot_key = int(build[4242].item())
+    del build
+    assert bf.probe_strategy_for(n) == 3  # partitioned
+    ow = orc.new_words(log_nb)
+    orc.build_mt(ow, log_nb, orc.synth_build_keys(n_build), threads)
+    probe = _skewed_column(rpt, n, n_build, hot, hot_key)
+    for _ in range(2):
+        sel_t, cnt = bf.probe_async(probe)
+        count = int(cnt.item())
+        sel = sel_t[:count].cpu().numpy().astype(np.int64)
+        del sel_t
+        assert np.all(sel[1:] > sel[:-1])
+        _full_check(ow, log_nb, probe, sel, piece=1 << 24)
+        assert count >= int(hot * n * 0.99)
+    del probe
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("hot", [0.5, 1.0])
+def test_full_size_hot_bucket_vs_oracle(rpt, hot):
+    """The bucketed strategy with one level-1 bucket (32 MiB filter region) holding half / all of 2^27 + 777 rows
+    (one hot key): its chunk lists grow through the extent pool far past an even split; every row against the
+    oracle (a hit on the bound would degrade to every row passing, and fail here)."""
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    log_nb, n_build, n = 26, 10**7, 2**27 + 777
+    bf = rpt.BloomFilter(log_num_blocks=log_nb)
+    bf.probe_strategy = 4  # bucketed
+    build = rpt.synth_build_keys(n_build)
+    bf.insert(build)
+    hot_key = int(build[777].item())
+    del build
+    ow = orc.new_words(log_nb)
+    orc.build_mt(ow, log_nb, orc.synth_build_keys(n_build), threads)
+    probe = _skewed_column(rpt, n, n_build, hot, hot_key, seed=2)
+    sel_t, cnt = bf.probe_async(probe)
+    count = int(cnt.item())
+    sel = sel_t[:count].cpu().numpy().astype(np.int64)
+    del sel_t
+    assert np.all(sel[1:] > sel[:-1])
+    _full_check(ow, log_nb, probe, sel, piece=1 << 24)
+    assert count < n or hot == 1.0
+    del probe
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("log_nb,n", [(4, 10), (14, 100_000), (21, 3_000_000), (27, 2_000_000)])
+def test_is_same_as_on_device(rpt, log_nb, n):
+    """rpt_bf_is_same_as (Arrow BlockedBloomFilter::IsSameAs): equal builds compare equal; one extra key, a cleared
+    filter and a different geometry do not; the differing-word count equals the host comparison's."""
+    k = orc.synth_build_keys(n)
+    a, b = rpt.BloomFilter(log_num_blocks=log_nb), rpt.BloomFilter(log_num_blocks=log_nb)
+    a.insert(dev(k))
+    b.insert(dev(k[::-1].copy()))
+    assert a.is_same_as(b) and b.is_same_as(a) and a.diff_words(b) == 0
+    b.insert(dev(np.array([-12345], dtype=np.int64)))
+    assert not a.is_same_as(b)
+    assert a.diff_words(b) == int((a.export_words() != b.export_words()).sum()) >= 1
+    b.clear()  # deferred clear: the comparison settles it first
+    assert b.diff_words(rpt.BloomFilter(log_num_blocks=log_nb)) == 0
+    assert not rpt.BloomFilter(log_num_blocks=log_nb + 1).is_same_as(a)
+
+
+def test_stream_calibration_kernels(rpt):
+    """bench.py's stream calibration entry points: the copy moves the bytes exactly, the read runs, both report
+    rates below the 8 TB/s spec."""
+    from rpt_amd._lib import RPT_ERR_INVALID_ARGUMENT
+
+    lib = rpt.load()
+    nbytes = 1 << 28
+    src = torch.randint(-2**62, 2**62, (nbytes // 8,), dtype=torch.int64, device="cuda:0")
+    dst = torch.zeros_like(src)
+    sink = torch.empty(int(lib.rpt_stream_sink_words(0)), dtype=torch.int64, device="cuda:0")
+    s = torch.cuda.current_stream().cuda_stream
+    assert lib.rpt_stream_copy(dst.data_ptr(), src.data_ptr(), nbytes, s) == 0
+    assert lib.rpt_stream_read(src.data_ptr(), nbytes, sink.data_ptr(), s) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(src, dst)
+    assert lib.rpt_stream_read(src.data_ptr() + 8, 16, sink.data_ptr(), s) == RPT_ERR_INVALID_ARGUMENT
+    import bench
+
+    cal = bench.stream_calibration(torch.device("cuda", 0), nbytes=1 << 30, reps=2)
+    assert 1000 < cal["read_GBps"] < 8000 and 1000 < cal["copy_GBps"] < 8000, cal
+
+
 @pytest.mark.parametrize("log_nb", [21, 22, 24])
 @pytest.mark.parametrize("nulls", [False, True])
 def test_large_filters_int32_vs_oracle(rpt, log_nb, nulls):
