@@ -98,6 +98,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("RPT_CPU_THREADS", "0")) or None,
                     help="CPU-baseline threads (default: this process's CPU share, see cpu_share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-lag", type=int, default=0,
+                    help="CPU baseline: rows between a row's hash + prefetch and its filter test (0: the default, 24; "
+                         "2048: the whole vector hashed first, the pre-r05 loop)")
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="print only the cpu_baseline object for this config (no GPU; e.g. to put the CPU "
                          "restatement at T threads beside the host-resident GPU path of tools/host_bench)")
@@ -384,7 +387,7 @@ def pmc_traffic(kernel: str, tag: str):
 
 
 def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, threads: int, threads_src: str,
-                 key_type: str = "i64") -> dict:
+                 key_type: str = "i64", lag: int = 0) -> dict:
     """The C++ restatement of the reference CPU path, morsel-parallel in 2048-row vectors, against the
     SAME filter geometry the GPU probes (sized for n_filter rows, n_build keys inserted). int32 keys run
     zero-extended to int64: DuckDB hashes an INTEGER through uint32 -> uint64, so hashes and survivors
@@ -393,6 +396,7 @@ def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, thre
     import numpy as np
     import rpt_oracle as orc
 
+    orc.set_probe_lag(lag)
     lnb = orc.log_num_blocks(n_filter)
     words = orc.new_words(lnb)
     as_i32 = (lambda k: k.astype(np.int32).view(np.uint32).astype(np.int64)) if key_type == "i32" else (lambda k: k)
@@ -416,6 +420,7 @@ def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, thre
                    f"hash included; median of 5 after 1 warm-up; build of the filter {n_build / build_s:.3e} keys/s"),
         "cpu_model": _cpu_model(),
         "survivors": runs[0][1],
+        "prefetch_lag_rows": int(orc.lib().rpt_oracle_probe_lag()),
     }
 
 
@@ -490,7 +495,8 @@ def main():
             print(json.dumps({"cpu_baseline": cb, "config": cfg}), flush=True)
             return
         cb = cpu_baseline(n_build, n_filter, int(round(args.p * 1000)), sample, threads,
-                          "--cpu-threads" if args.cpu_threads else "this process's CPU share", args.key_type)
+                          "--cpu-threads" if args.cpu_threads else "this process's CPU share", args.key_type,
+                          args.cpu_lag)
         print(json.dumps({"cpu_baseline": cb, "config": cfg, "key_type": args.key_type}), flush=True)
         return
     world = int(os.environ.get("WORLD_SIZE", "0"))
@@ -825,7 +831,7 @@ def main():
             sample = int(args.cpu_sample) if args.cpu_sample else n_probe
             threads = args.cpu_threads or cpu_share()
             src = "--cpu-threads" if args.cpu_threads else "this process's CPU share: affinity mask capped by the cgroup quota"
-            cb = cpu_baseline(n_build, n_filter, p_permille, sample, threads, src, args.key_type)
+            cb = cpu_baseline(n_build, n_filter, p_permille, sample, threads, src, args.key_type, args.cpu_lag)
             if sample == n_probe:  # same rows, same filter: a full-size cross-check of the survivor count
                 cb["survivors_match_gpu"] = cb["survivors"] == survivors
             line["cpu_baseline"] = cb

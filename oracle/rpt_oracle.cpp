@@ -411,8 +411,15 @@ double rpt_oracle_probe_mt(const uint64_t* words, int log_nb, const int64_t* key
 // USE_BF's filter loop per vector (physical_use_bf.cpp:137-183): filter 0 over every row of the vector, each
 // further filter over the previous one's survivors (its own key column, same rows), stopping when none are left;
 // per 2048-row vector on `threads` threads, hash included. The final survivors are counted (*out_count).
+// Rows between a row's hash + prefetch and its filter test (default 24; set for the prefetch-distance sweep of
+// 2048 = the whole vector hashed and prefetched before any row is tested, the pre-r05 loop).
+static std::atomic<uint64_t> g_probe_lag{24};
+void rpt_oracle_set_probe_lag(uint64_t lag) { g_probe_lag.store(lag ? lag : 24); }
+uint64_t rpt_oracle_probe_lag(void) { return g_probe_lag.load(); }
+
 double rpt_oracle_probe_chain_mt(const uint64_t* const* words, const int* log_nb, const int64_t* const* keys, int k,
                                  uint64_t n, int threads, uint64_t* out_count) {
+  const uint64_t kLag = g_probe_lag.load();
   std::atomic<uint64_t> next{0};
   std::atomic<uint64_t> total{0};
   auto t0 = std::chrono::steady_clock::now();
@@ -437,7 +444,6 @@ double rpt_oracle_probe_chain_mt(const uint64_t* const* words, const int* log_nb
             sel[c] = sel[j];
             c += (w[block_of(h, nb)] & m) == m;
           };
-          constexpr uint64_t kLag = 24;
           for (uint64_t j = 0; j < cnt; j++) {
             hashes[j] = murmur64(static_cast<uint64_t>(kf[sel[j]]));
             __builtin_prefetch(&w[block_of(hashes[j], nb)]);

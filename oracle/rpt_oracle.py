@@ -46,6 +46,8 @@ _SIG = {
     "rpt_oracle_build_mt": (c_double, [c_void_p, c_int, c_void_p, c_uint64, c_int]),
     "rpt_oracle_probe_mt": (c_double, [c_void_p, c_int, c_void_p, c_uint64, c_int, POINTER(c_uint64)]),
     "rpt_oracle_probe_chain_mt": (c_double, [c_void_p, c_void_p, c_void_p, c_int, c_uint64, c_int, POINTER(c_uint64)]),
+    "rpt_oracle_set_probe_lag": (None, [c_uint64]),
+    "rpt_oracle_probe_lag": (c_uint64, []),
 }
 
 _lib = None
@@ -204,6 +206,11 @@ def probe_mt(words: np.ndarray, log_nb: int, keys: np.ndarray, threads: int) -> 
     cnt = c_uint64()
     s = lib().rpt_oracle_probe_mt(_p(words), log_nb, _p(keys), keys.size, threads, ctypes.byref(cnt))
     return float(s), int(cnt.value)
+
+
+def set_probe_lag(lag: int) -> None:
+    """Rows between a row's hash + prefetch and its test in the CPU-baseline probe loop (0: the default, 24)."""
+    lib().rpt_oracle_set_probe_lag(int(lag))
 
 
 def probe_chain_mt(words: list, log_nbs: list, keys: list, threads: int) -> tuple[float, int]:

@@ -595,8 +595,10 @@ static void pipelined_chain(int dev) {
   // a chunk whose column-1 dictionary indices are out of range: the gather for f1 (on a worker thread, mid
   // chain) throws, the pipeline drains its streams and ExecuteBatch raises INVALID_ARGUMENT; the context stays
   // usable
-  {
-    const size_t victim = pptrs.size() / 2 + 7;
+  // (with every stage stream synchronized before the error leaves, including the third stage's) at
+  // several positions, with stages of 256 Ki rows so all three stage streams are busy when the gather throws
+  ctx.pipeline_rows = 1u << 18;
+  for (const size_t victim : {pptrs.size() / 2 + 7, size_t(300), pptrs.size() - 2, size_t(1400)}) {
     rpt::DataChunk broken = *pptrs[victim];
     std::vector<uint32_t> bad_sel(broken.count, 1u << 30);
     std::vector<int32_t> dict(4, 1);
@@ -625,8 +627,9 @@ static void pipelined_chain(int dev) {
       total += w.size();
       bad += outs[k] != w;
     }
-    EXPECT(bad == 0 && got == total, "the context after a failed chain: %zu chunks differ", bad);
+    EXPECT(bad == 0 && got == total, "the context after a failed chain (bad chunk %zu): %zu chunks differ", victim, bad);
   }
+  ctx.pipeline_rows = 1u << 20;
 }
 
 // The process-wide pinned staging cache: a destroyed context's buffers are cached and handed to the next
@@ -1100,6 +1103,27 @@ int main() {
       std::vector<uint64_t> va = pack(bt.v0, 0, nb);
       rpt_oracle_minmax_i64(bt.c0.data(), nullptr, va.data(), nb, e0);
       EXPECT(part.MinMax(0, mn, mx) && mn == e0[0] && mx == e0[1], "estimate 20000: min/max");
+    }
+    {  // a sink state that flushed (making the resize look certain, so later flushes skip their inserts)
+       // but is never combined; the combined rows alone do not call for the resize. Finalize must still rehash them.
+      rpt::CreateBF lone(dev, 1000, {0}, 5000);
+      auto a = lone.MakeLocalState(), b = lone.MakeLocalState();
+      for (size_t k = 0; k < 4; k++) lone.Sink(*a, bst.chunks[k]);  // 8192 rows: flushed, resize "certain"
+      rpt::DataChunk few = bst.chunks[5];
+      few.count = 500;
+      lone.Sink(*b, few);
+      lone.Combine(*b);  // a is dropped without Combine (its rows never reach the operator's result)
+      a.reset();
+      EXPECT(lone.SkippedInsertRows() > 0, "the lone state's insert was skipped");
+      lone.Finalize();
+      const int ll = rpt_oracle_log_num_blocks(1000);
+      std::vector<uint64_t> wl(1ULL << ll, 0);
+      std::vector<uint64_t> vl = pack(bt.v0, 5 * 2048, 500);
+      // chunk 5 is FLAT or DICTIONARY (k % 3 == 2: FLAT): its first 500 rows are rows 10240.. of the table
+      rpt_oracle_insert_i64(wl.data(), ll, bt.c0.data() + 5 * 2048, nullptr, vl.data(), 500);
+      EXPECT(!lone.Resized(0) && lone.GetBloomFilter(0)->LogNumBlocks() == ll &&
+                 lone.GetBloomFilter(0)->ExportWords() == wl,
+             "uncombined flushing state: the combined rows' filter differs from the oracle (false negatives)");
     }
     // the rehash from HBM groups NULL-free segments into one insert: a NULL-free build, and one with NULLs in a few
     // segments only (grouped and single segments interleaved)
