@@ -101,6 +101,11 @@ def parse():
     ap.add_argument("--cpu-lag", type=int, default=0,
                     help="CPU baseline: rows between a row's hash + prefetch and its filter test (0: the default, 24; "
                          "2048: the whole vector hashed first, the pre-r05 loop)")
+    ap.add_argument("--cpu-lag-sweep", default=None,
+                    help="with --cpu-baseline-only: comma-separated prefetch lags timed interleaved (A B C A B C ...) "
+                         "in one process against one filter and sample, with the cgroup's CPU throttling and the "
+                         "host's load average around each measurement (VERDICT r05 item 6)")
+    ap.add_argument("--cpu-sweep-rounds", type=int, default=3)
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="print only the cpu_baseline object for this config (no GPU; e.g. to put the CPU "
                          "restatement at T threads beside the host-resident GPU path of tools/host_bench)")
@@ -170,8 +175,9 @@ def stream_calibration(device, nbytes: int = STREAM_CAL_BYTES, reps: int = 5) ->
         "read_GBps": nbytes / t_read / 1e9,
         "copy_GBps": 2 * half / t_copy / 1e9,  # bytes read + bytes written
         "bytes": nbytes,
-        "how": ("rpt_stream_read: 16-B non-temporal loads over 8 GiB, 4 x 256-thread workgroups per CU; "
-                "rpt_stream_copy: 4 GiB -> 4 GiB, read + write bytes; best of 5 after a warm-up, HIP events"),
+        "how": ("rpt_stream_read: 16-B non-temporal loads over 8 GiB, 8 in flight per lane, 16 x 256-thread "
+                "workgroups per CU; rpt_stream_copy: 4 GiB -> 4 GiB, one 16-B unit per lane, read + write bytes; "
+                "best of 5 after a warm-up, HIP events (the fastest variants of tools/ubench/ubench_stream.hip)"),
     }
 
 
@@ -248,6 +254,16 @@ class DeviceMemTracker:
         self.base = self.total - free
         self.peak = self.base
         self.phases = {}
+        # this process's own share, which stays meaningful when ranks share a device: torch's caching allocator
+        # (reserved) plus the filters the library allocated itself (note_filters), sampled at the same points
+        torch.cuda.reset_peak_memory_stats(device)
+        self.filters = 0
+        self.own_peak = 0
+        self.own_phases = {}
+
+    def note_filters(self, nbytes: int) -> None:
+        """Bytes of library-allocated filters (hipMalloc in rpt_bf_create) this rank holds from now on."""
+        self.filters = nbytes
 
     def sample(self, phase: str) -> None:
         self._torch.cuda.synchronize(self.device)
@@ -255,6 +271,10 @@ class DeviceMemTracker:
         used = self.total - free
         self.phases[phase] = used
         self.peak = max(self.peak, used)
+        own = self._torch.cuda.max_memory_reserved(self.device) + self.filters
+        self._torch.cuda.reset_peak_memory_stats(self.device)
+        self.own_phases[phase] = own
+        self.own_peak = max(self.own_peak, own)
         if self.progress:
             print(f"[bench c5] {phase} done at {time.perf_counter() - self.t0:.1f} s, device memory in use "
                   f"{used / 2**30:.1f} GiB", file=sys.stderr, flush=True)
@@ -275,6 +295,7 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
     native = comm is not None
     rows = int(args.c5_rows_per_rank)
     bf = rpt_amd.BloomFilter(C5_FILTER_ROWS, device=device)
+    mem.note_filters(bf.num_blocks * 8)
     keys = rpt_amd.synth_build_keys(rows, start=rank * rows, device=device)
     bf.insert(keys)  # warm-up (workspace, code objects)
     torch.cuda.synchronize()
@@ -319,6 +340,7 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
     # untimed: the merged filter against a single build of all world * rows rows (inserted piece by piece),
     # compared on the device (rpt_bf_is_same_as: no word copies, so a rank holds its filter + the reference)
     ref = rpt_amd.BloomFilter(C5_FILTER_ROWS, device=device)
+    mem.note_filters(2 * bf.num_blocks * 8)
     for r in range(world):
         rpt_amd.synth_build_keys(rows, start=r * rows, device=device, out=keys)
         ref.insert(keys)
@@ -326,6 +348,7 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
     same = bf.is_same_as(ref) and bf.minmax() == ref.minmax() and not bf.is_empty()
     mem.sample("merge_check")
     del ref
+    mem.note_filters(bf.num_blocks * 8)
     torch.cuda.empty_cache()
     ok = all_ok(same)
     check = ("bit-identical (words + key min/max) to a single-GPU build of all rows on every rank" if ok
@@ -352,7 +375,7 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
     del pkeys, out_sel, pws, bf
     torch.cuda.empty_cache()
     insert_s, probe_s, *merge_s = reduce_max([insert_s, probe_s] + merge_s)
-    peaks = gather_ints([mem.peak - mem.base, mem.peak])
+    peaks = gather_ints([mem.peak - mem.base, mem.peak, mem.own_peak])
     wall_s = reduce_max([time.perf_counter() - t_section])[0]
     mem_rec = {
         "source": "hipMemGetInfo (torch.cuda.mem_get_info): total - free, sampled after each phase",
@@ -360,6 +383,10 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
         "rank0_phase_used_bytes": mem.phases,
         "section_peak_bytes_per_rank": [p[0] for p in peaks],
         "device_peak_used_bytes_per_rank": [p[1] for p in peaks],
+        # each rank's own footprint (torch's reserved peak + the library's filters), per phase on rank 0: what one
+        # rank of the driver's N-GPU run holds, whether or not ranks share a device here
+        "rank_own_peak_bytes_per_rank": [p[2] for p in peaks],
+        "rank0_own_phase_bytes": mem.own_phases,
         "ranks_per_device": shared_device_ranks,
     }
     rec = c5_merge_record(world, nbytes, rows, insert_s * 1e3, merge_s, probe_s * 1e3, survivors, check,
@@ -422,6 +449,45 @@ def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, thre
         "survivors": runs[0][1],
         "prefetch_lag_rows": int(orc.lib().rpt_oracle_probe_lag()),
     }
+
+
+def _cgroup_cpu_stat() -> dict:
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            return {k: int(v) for k, v in (line.split() for line in f if line.strip())}
+    except (OSError, ValueError):
+        return {}
+
+
+def cpu_lag_sweep(n_build: int, n_filter: int, p_permille: int, sample: int, threads: int, lags: list,
+                  rounds: int) -> dict:
+    """The CPU baseline's probe loop at several prefetch lags, interleaved round by round in one process (same filter,
+    same sample), so a neighbour's load on the shared host or the cgroup's CPU quota shows up in every lag alike
+    instead of as a difference between them; each measurement is the median of 5 runs after a warm-up."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import rpt_oracle as orc
+
+    lnb = orc.log_num_blocks(n_filter)
+    words = orc.new_words(lnb)
+    orc.build_mt(words, lnb, orc.synth_build_keys(n_build), threads)
+    keys = orc.synth_probe_keys(sample, n_build, p_permille)
+    out = []
+    for r in range(rounds):
+        for lag in lags:
+            orc.set_probe_lag(lag)
+            orc.probe_mt(words, lnb, keys, threads)  # warm-up
+            st0, la0, t0 = _cgroup_cpu_stat(), os.getloadavg(), time.perf_counter()
+            runs = [orc.probe_mt(words, lnb, keys, threads) for _ in range(5)]
+            st1, wall = _cgroup_cpu_stat(), time.perf_counter() - t0
+            d = {k: st1[k] - st0.get(k, 0) for k in st1}
+            out.append({"round": r, "lag": lag, "keys_per_s": sample / statistics.median(x[0] for x in runs),
+                        "runs_s": [x[0] for x in runs], "wall_s": wall, "loadavg_1m_before": la0[0],
+                        "cpu_usage_s": d.get("usage_usec", 0) / 1e6,
+                        "throttled_s": d.get("throttled_usec", 0) / 1e6, "nr_throttled": d.get("nr_throttled", 0),
+                        "survivors": runs[0][1]})
+    orc.set_probe_lag(0)
+    return {"threads": threads, "sample": sample, "filter_log_blocks": lnb, "cpu_model": _cpu_model(),
+            "host_cpus": os.cpu_count(), "cpu_share": cpu_share(), "measurements": out}
 
 
 def cpu_chain_baseline(k: int, n_build: int, n_filter: int, sample: int, threads: int) -> dict:
@@ -490,6 +556,12 @@ def main():
         n_filter = int(args.filter_rows) if args.filter_rows else (CONFIGS[cfg][1](1) if not args.build_rows else n_build)
         sample = int(args.cpu_sample) if args.cpu_sample else int(args.probe_rows)
         threads = args.cpu_threads or cpu_share()
+        if args.cpu_lag_sweep:
+            lags = [int(x) for x in args.cpu_lag_sweep.split(",")]
+            sw = cpu_lag_sweep(n_build, n_filter, int(round(args.p * 1000)), sample, threads, lags,
+                               args.cpu_sweep_rounds)
+            print(json.dumps({"cpu_lag_sweep": sw, "config": cfg}), flush=True)
+            return
         if args.cpu_chain:
             cb = cpu_chain_baseline(args.cpu_chain, n_build, n_filter, sample, threads)
             print(json.dumps({"cpu_baseline": cb, "config": cfg}), flush=True)

@@ -152,10 +152,12 @@ __global__ __launch_bounds__(kBlockThreads) void diff_count_kernel(const uint64_
 }
 
 // ---- stream calibration (bench.py: the box's achievable HBM rates beside the kernels' fractions) --
-// Read: every lane streams 16-B non-temporal loads, 4 in flight, and folds them into one word per
-// workgroup (written, so nothing is dead code). Copy: the same loads stored to dst (non-temporal).
-// n16: number of 16-B units; grid-stride over them.
-constexpr int kStreamUnroll = 4;
+// The fastest of the variants tools/ubench/ubench_stream.hip measured (profiles/r06/ubench_stream.txt):
+// read: grid-stride 16-B non-temporal loads, 8 in flight per lane, 16 x 256-thread workgroups per CU (6.6 TB/s),
+// folded into one word per workgroup (written, so nothing is dead code); copy: a one-shot grid, one 16-B unit per
+// lane, non-temporal store (6.3 TB/s of read + write bytes; a grid-stride copy reached only 4.9).
+constexpr int kStreamUnroll = 8;
+constexpr int kStreamBlocksPerCU = 16;
 __global__ __launch_bounds__(kBlockThreads) void stream_read_kernel(const u64x2* __restrict__ src, uint64_t n16,
                                                                    uint64_t* __restrict__ sink) {
   __shared__ uint64_t s_part[kWavesPerBlock];
@@ -179,16 +181,8 @@ __global__ __launch_bounds__(kBlockThreads) void stream_read_kernel(const u64x2*
 
 __global__ __launch_bounds__(kBlockThreads) void stream_copy_kernel(const u64x2* __restrict__ src, uint64_t n16,
                                                                    u64x2* __restrict__ dst) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  for (; i + (kStreamUnroll - 1) * stride < n16; i += kStreamUnroll * stride) {
-    u64x2 v[kStreamUnroll];
-#pragma unroll
-    for (int u = 0; u < kStreamUnroll; u++) v[u] = __builtin_nontemporal_load(src + i + u * stride);
-#pragma unroll
-    for (int u = 0; u < kStreamUnroll; u++) __builtin_nontemporal_store(v[u], dst + i + u * stride);
-  }
-  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n16) __builtin_nontemporal_store(src[i], dst + i);
 }
 
 // ---- synthetic workload (bench / tests) ----------------------------------------------

@@ -2498,7 +2498,7 @@ int rpt_synth_probe_keys(int64_t* out, uint64_t n_build, uint32_t p_permille, ui
   return RPT_OK;
 }
 
-uint64_t rpt_stream_sink_words(int device) { return static_cast<uint64_t>(num_cus(device)) * rpt::kBlocksPerCU; }
+uint64_t rpt_stream_sink_words(int device) { return static_cast<uint64_t>(num_cus(device)) * rpt::kStreamBlocksPerCU; }
 
 static int stream_check(const void* p, uint64_t bytes, int* dev) {
   if (!p) return fail(RPT_ERR_INVALID_ARGUMENT, "null pointer");
@@ -2528,8 +2528,9 @@ int rpt_stream_copy(void* dst, const void* src, uint64_t bytes, rpt_stream_t str
   if (st == RPT_OK) st = stream_check(dst, bytes, &dev);
   if (st != RPT_OK) return st;
   if (bytes == 0) return RPT_OK;
+  if (ceil_div(bytes / 16, rpt::kBlockThreads) > 0x7fffffffULL) return fail(RPT_ERR_INVALID_ARGUMENT, "copy too large");
   ProfScope prof_("stream_copy_kernel", as_stream(stream));
-  hipLaunchKernelGGL(rpt::stream_copy_kernel, dim3(static_cast<unsigned>(rpt_stream_sink_words(dev))),
+  hipLaunchKernelGGL(rpt::stream_copy_kernel, dim3(static_cast<unsigned>(ceil_div(bytes / 16, rpt::kBlockThreads))),
                      dim3(rpt::kBlockThreads), 0, as_stream(stream), static_cast<const rpt::u64x2*>(src), bytes / 16,
                      static_cast<rpt::u64x2*>(dst));
   prof_.end();

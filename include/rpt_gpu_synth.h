@@ -31,9 +31,10 @@ int rpt_synth_probe_keys(int64_t* out, uint64_t n_build, uint32_t p_permille, ui
                          rpt_stream_t stream);
 
 /* Stream calibration (bench.py reports the kernels' HBM fractions against what this box streams, beside the
- * 8 TB/s spec): read `bytes` bytes at `src` with 16-B non-temporal loads over a grid of 4 x 256-thread
- * workgroups per CU (sink: one word per workgroup, rpt_stream_sink_words(device) words), or copy them to
- * `dst`. Device pointers, 16-B aligned, bytes a multiple of 16. Stream-ordered, no sync. */
+ * 8 TB/s spec): read `bytes` bytes at `src` with 16-B non-temporal loads, 8 in flight per lane, over a grid of
+ * 16 x 256-thread workgroups per CU (sink: one word per workgroup, rpt_stream_sink_words(device) words), or copy
+ * them to `dst` (one 16-B unit per lane). The fastest of the variants tools/ubench/ubench_stream.hip times.
+ * Device pointers, 16-B aligned, bytes a multiple of 16. Stream-ordered, no sync. */
 uint64_t rpt_stream_sink_words(int device);
 int rpt_stream_read(const void* src, uint64_t bytes, uint64_t* sink, rpt_stream_t stream);
 int rpt_stream_copy(void* dst, const void* src, uint64_t bytes, rpt_stream_t stream);
