@@ -1766,6 +1766,41 @@ bool CreateBF::MinMax(size_t build_column, int64_t& min_value, int64_t& max_valu
   return filters_.at(build_column)->MinMax(min_value, max_value);
 }
 
+// ---- where the filter runs: scan pushdown or USE_BF ---------------------------------
+PushdownPlan PlanPushdown(Device device, FilterType filter_type, bool is_forward_pass, bool has_targets,
+                          uint64_t build_rows, bool bf_empty, bool has_minmax) {
+  PushdownPlan p;
+  // backward-pass CREATE_BFs and forward ones without scan targets push nothing; their USE_BF probes
+  // (PushDynamicFilters' early return, physical_create_bf.cpp:284-286; only forward USE_BFs with targets are
+  // marked passthrough, rpt_optimizer.cpp:1436-1440,1493-1494)
+  if (!is_forward_pass || !has_targets) return p;
+  const bool bf = filter_type == FilterType::kAll || filter_type == FilterType::kBfOnly;
+  const bool minmax = filter_type == FilterType::kAll || filter_type == FilterType::kMinMaxOnly;
+  if (device == Device::kCpu) {
+    // the reference: the forward USE_BF passes through and the scan filters do the work
+    p.use_bf_passthrough = true;
+    p.bf_probed_in_use_bf = false;
+    if (build_rows == 0) {
+      p.push_always_false = true;  // cpp:288-297 (and nothing else)
+      return p;
+    }
+    p.push_bf = bf && !bf_empty;  // cpp:321-323: the filter of a non-empty build
+    p.push_minmax = minmax && has_minmax;
+    return p;
+  }
+  // GPU mode: no BFTableFilter (it would run the filter in DuckDB's CPU scan); the forward USE_BF keeps the probe on
+  // the device unless the filter type leaves the BF out (minmax_only: passthrough, as the reference drops it too).
+  // Min/max and the empty build's always-false filter stay in the scan: they skip row groups for nothing.
+  p.use_bf_passthrough = !bf;
+  p.bf_probed_in_use_bf = bf;
+  if (build_rows == 0) {
+    p.push_always_false = true;
+    return p;
+  }
+  p.push_minmax = minmax && has_minmax;
+  return p;
+}
+
 // ---- UseBF ---------------------------------------------------------------------------------------
 UseBF::UseBF(std::vector<std::shared_ptr<PTBloomFilter>> filters, std::vector<uint64_t> bound_column_indices,
              bool passthrough)

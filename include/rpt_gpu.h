@@ -166,7 +166,12 @@ int rpt_bf_clear(rpt_bf* bf, rpt_stream_t stream);
  * (otherwise RPT_ERR_INVALID_ARGUMENT: synchronize first); a captured insert merges with atomics, so each
  * replay ORs its keys in whatever the filter holds by then, and replays are ordered by the stream the
  * graph is launched on (a captured write takes no part in the filter's cross-stream write order).
- * rpt_bf_clear and rpt_bf_allreduce_or[_ws] are refused inside a capture. */
+ * rpt_bf_clear and rpt_bf_allreduce_or[_ws] are refused inside a capture. Any capture mode works: the one event
+ * query a captured write makes runs with the thread's capture mode relaxed around it. Under
+ * hipStreamCaptureModeGlobal (torch.cuda.graph's default) no thread of the process may make an unsafe HIP call
+ * while the capture is open, and rpt_bf_destroy / rpt_bf_create / rpt_bf_reinitialize are such calls (hipFree /
+ * hipMalloc): create and destroy filters outside capture windows (collect garbage that may hold filters first,
+ * as torch.cuda.graph does). */
 int rpt_bf_settle(rpt_bf* bf, rpt_stream_t stream);
 
 /* ---- build ------------------------------------------------------------------------------- */

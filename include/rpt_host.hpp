@@ -353,6 +353,29 @@ class CreateBF {
   mutable std::atomic<uint64_t> skipped_insert_rows_{0};
 };
 
+// Where a CREATE_BF's filter is applied: the reference's forward pass pushes its filter into the
+// probe table's scan (PhysicalCreateBF::Finalize -> PushDynamicFilters, physical_create_bf.cpp:282-350: a
+// BFTableFilter wrapped in SelectivityOptionalFilter(.., 1, 1000000), min/max ConstantFilters, always-false for an
+// empty build) and marks that forward USE_BF passthrough (SetupDynamicFilterPushdown, rpt_optimizer.cpp:1493-1494),
+// so those probes run inside DuckDB's CPU scan. The GPU mode (the `rpt_device` setting) keeps the BF
+// probe in USE_BF, on the device, and pushes only the cheap scan filters. A DuckDB shim calls PlanPushdown in
+// SetupDynamicFilterPushdown (to decide is_passthrough) and in PushDynamicFilters (to decide what to push).
+enum class FilterType { kAll, kBfOnly, kMinMaxOnly };  // rpt_filter_type ('all' | 'bf_only' | 'minmax_only')
+enum class Device { kCpu, kGpu };                       // rpt_device ('cpu' = the reference | 'gpu')
+struct PushdownPlan {
+  bool use_bf_passthrough = false;  // the USE_BF operator references its input unchanged (physical_use_bf.cpp:62-66)
+  bool push_always_false = false;   // empty build side: every target scan gets `col > MAX` (cpp:288-297)
+  bool push_bf = false;             // BFTableFilter into the target scans (cpp:321-333)
+  bool push_minmax = false;         // `col >= min` and `col <= max` into the target scans (cpp:335-345)
+  bool bf_probed_in_use_bf = true;  // the BF probe runs in USE_BF (rpt::UseBF): false when the scan runs it, or
+                                    // when nothing probes it (minmax_only drops the forward BF, as the reference)
+};
+// is_forward_pass / has_targets: the CREATE_BF's pass and whether SetupDynamicFilterPushdown found scan targets for
+// it; build_rows == 0: the build side was empty; bf_empty: the filter holds no key (IsEmpty); has_minmax: the build
+// column kept a min/max (CreateBF::MinMax).
+PushdownPlan PlanPushdown(Device device, FilterType filter_type, bool is_forward_pass, bool has_targets,
+                          uint64_t build_rows, bool bf_empty, bool has_minmax);
+
 // PhysicalUseBF::ExecuteInternal (physical_use_bf.cpp:60-198): AND of the filters over the chunk,
 // in filter order, with its early exits (empty filter -> 0 rows, 0 survivors -> stop) and skips
 // (filter not finalized). Returns the surviving row ids of the input chunk (ascending). A chunk of at

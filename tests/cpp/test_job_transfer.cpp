@@ -186,10 +186,11 @@ struct UseResult {
 };
 
 static void use_bf(int dev, const std::string& name, const std::vector<std::shared_ptr<rpt::PTBloomFilter>>& filters,
-                   const std::vector<uint64_t>& cols, const std::vector<rpt::DataChunk>& in, bool batch, UseResult& out) {
+                   const std::vector<uint64_t>& cols, const std::vector<rpt::DataChunk>& in, bool batch, UseResult& out,
+                   bool passthrough = false) {
   rpt::DeviceContext ctx(dev);
   ctx.pipeline_rows = 1ULL << 16;  // stages of 64 Ki rows: a pipelined chain over several stages
-  rpt::UseBF op(filters, cols);
+  rpt::UseBF op(filters, cols, passthrough);
   std::vector<rpt::SelectionVector> sels(in.size());
   uint64_t rows_in = 0;
   if (batch) {
@@ -211,7 +212,7 @@ static void use_bf(int dev, const std::string& name, const std::vector<std::shar
     for (size_t i = 0; i < s.size(); i++) out.ids.push_back(row_id_at(out.chunks.back(), i));
     kept += s.size();
   }
-  EXPECT(op.rows_in() == rows_in && op.rows_out() == kept, "%s: operator counters %llu/%llu vs %llu/%llu", name.c_str(),
+  EXPECT(passthrough || (op.rows_in() == rows_in && op.rows_out() == kept), "%s: operator counters %llu/%llu vs %llu/%llu", name.c_str(),
          (unsigned long long)op.rows_in(), (unsigned long long)op.rows_out(), (unsigned long long)rows_in,
          (unsigned long long)kept);
   write_file("use_" + name + ".i64", out.ids);
@@ -266,6 +267,22 @@ static std::vector<rpt::DataChunk> create_bf(rpt::CreateBF& op, const std::vecto
   return out;
 }
 
+// The forward CREATE_BF's pushdown in the GPU mode (rpt_device = gpu, filter type 'all', scan targets found):
+// SURVEY §8 a10. The BF stays out of the scan and its USE_BF probes on the device; min/max still go to the scan.
+static bool forward_passthrough(const rpt::CreateBF& op, size_t col, const char* name) {
+  int64_t mn = 0, mx = 0;
+  const bool mm = op.MinMax(col, mn, mx);
+  const rpt::PushdownPlan p = rpt::PlanPushdown(rpt::Device::kGpu, rpt::FilterType::kAll, /*is_forward_pass=*/true,
+                                                /*has_targets=*/true, op.MaterializedRows(),
+                                                op.GetBloomFilter(col)->IsEmpty(), mm);
+  EXPECT(!p.use_bf_passthrough && p.bf_probed_in_use_bf && !p.push_bf && p.push_minmax == mm && !p.push_always_false,
+         "%s: GPU-mode pushdown plan", name);
+  const rpt::PushdownPlan c = rpt::PlanPushdown(rpt::Device::kCpu, rpt::FilterType::kAll, true, true,
+                                                op.MaterializedRows(), op.GetBloomFilter(col)->IsEmpty(), mm);
+  EXPECT(c.use_bf_passthrough && c.push_bf && !c.bf_probed_in_use_bf, "%s: the reference's (CPU) plan", name);
+  return p.use_bf_passthrough;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: test_job_transfer DIR\n");
@@ -293,12 +310,15 @@ int main(int argc, char** argv) {
     rpt::CreateBF c_it(dev, est.at("f_it"), {0});
     const std::vector<rpt::DataChunk> it_src = create_bf(c_it, {"f_it"}, it.chunks, 2);
     UseResult t_fwd;
-    use_bf(dev, "t_fwd", {c_mc.GetBloomFilter(0)}, {0}, t.chunks, /*batch=*/false, t_fwd);
+    use_bf(dev, "t_fwd", {c_mc.GetBloomFilter(0)}, {0}, t.chunks, /*batch=*/false, t_fwd,
+           forward_passthrough(c_mc, 0, "f_mc"));
     rpt::CreateBF c_t(dev, est.at("f_t"), {0}, 1 << 15);  // under-estimated: Finalize resizes + rehashes from HBM
     const std::vector<rpt::DataChunk> t_src = create_bf(c_t, {"f_t"}, t_fwd.chunks, 3);
     // mi (root): its two forward USE_BFs as one filter chain (AND), over the whole scan as a caching operator
     UseResult mi_fwd;
-    use_bf(dev, "mi_fwd", {c_it.GetBloomFilter(0), c_t.GetBloomFilter(0)}, {1, 0}, mi.chunks, /*batch=*/true, mi_fwd);
+    const bool pt_it = forward_passthrough(c_it, 0, "f_it"), pt_t = forward_passthrough(c_t, 0, "f_t");
+    use_bf(dev, "mi_fwd", {c_it.GetBloomFilter(0), c_t.GetBloomFilter(0)}, {1, 0}, mi.chunks, /*batch=*/true, mi_fwd,
+           pt_it && pt_t);
     // ---- backward pass (root -> leaves) ----
     // mi's two CREATE_BFs stacked into one operator with two build columns
     rpt::CreateBF c_mi(dev, est.at("f_mi"), {1, 0}, 1 << 17);

@@ -3,6 +3,7 @@ partitioned / bucketed insert whose slice merge owns every slice stores the slic
 included), every other operation zeroes the words first. Each case fills the filter with keys A, clears
 it, then runs one operation: the result must equal the oracle's for an EMPTY filter followed by that
 operation (no bit of A survives), and the filter must keep composing with later inserts. Bit-exact."""
+import gc
 import numpy as np
 import pytest
 import torch
@@ -233,13 +234,21 @@ def test_graph_capture_of_a_cleared_filter(rpt, log_nb, n, mode):
     graph, exe = ctypes.c_void_p(), ctypes.c_void_p()
 
     def capture():
+        # as torch.cuda.graph prepares a capture: collect garbage first (a filter an earlier test left to the cycle
+        # collector is freed by rpt_bf_destroy -> hipFree, which would invalidate a global-mode capture from any
+        # thread of the process) and keep the collector off inside the capture window
+        gc.collect()
+        torch.cuda.synchronize()
+        gc.disable()
         assert hip.hipStreamBeginCapture(sh, mode) == 0
         err = None
         try:
             bf.probe_async(kp, n=n, out_sel=out_sel, out_count=out_count, workspace=ws, stream=s)
         except RptError as e:
             err = e
-        assert hip.hipStreamEndCapture(sh, ctypes.byref(graph)) == 0  # still a valid capture
+        st = hip.hipStreamEndCapture(sh, ctypes.byref(graph))
+        gc.enable()
+        assert st == 0  # still a valid capture
         return err
 
     err = capture()
@@ -297,10 +306,14 @@ def test_graph_capture_of_inserts(rpt, strategy, log_nb, mode):
     graph, exe = ctypes.c_void_p(), ctypes.c_void_p()
 
     def capture(op):
+        gc.collect()  # see test_graph_capture_of_a_cleared_filter
         torch.cuda.synchronize()
+        gc.disable()
         assert hip.hipStreamBeginCapture(sh, mode) == 0
         st = op()
-        assert hip.hipStreamEndCapture(sh, ctypes.byref(graph)) == 0  # still a valid capture
+        end = hip.hipStreamEndCapture(sh, ctypes.byref(graph))
+        gc.enable()
+        assert end == 0  # still a valid capture
         return st
 
     def insert_b():
