@@ -106,6 +106,9 @@ def parse():
                          "in one process against one filter and sample, with the cgroup's CPU throttling and the "
                          "host's load average around each measurement (VERDICT r05 item 6)")
     ap.add_argument("--cpu-sweep-rounds", type=int, default=3)
+    ap.add_argument("--cpu-pin-sweep", default="0",
+                    help="with --cpu-lag-sweep: comma-separated thread placements (0 the OS's, 1 compact: thread t on "
+                         "the t-th CPU of the affinity mask, 2 spread over the mask), crossed with the lags")
     ap.add_argument("--cpu-baseline-only", action="store_true",
                     help="print only the cpu_baseline object for this config (no GPU; e.g. to put the CPU "
                          "restatement at T threads beside the host-resident GPU path of tools/host_bench)")
@@ -423,7 +426,6 @@ def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, thre
     import numpy as np
     import rpt_oracle as orc
 
-    orc.set_probe_lag(lag)
     lnb = orc.log_num_blocks(n_filter)
     words = orc.new_words(lnb)
     as_i32 = (lambda k: k.astype(np.int32).view(np.uint32).astype(np.int64)) if key_type == "i32" else (lambda k: k)
@@ -431,9 +433,18 @@ def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, thre
     build_s = orc.build_mt(words, lnb, build_keys, threads)
     del build_keys
     keys = as_i32(orc.synth_probe_keys(sample, n_build, p_permille))
-    orc.probe_mt(words, lnb, keys, threads)  # warm-up
-    runs = [orc.probe_mt(words, lnb, keys, threads) for _ in range(5)]
-    med = statistics.median(r[0] for r in runs)
+    # the loop's prefetch distance: which of 24 rows and the whole vector (2048) is faster depends on the box's
+    # thread placement and neighbours, not on the filter (CPU baseline), so both run and the faster is
+    # the baseline (--cpu-lag pins one)
+    by_lag = {}
+    for lg in ([lag] if lag else [24, 2048]):
+        orc.set_probe_lag(lg)
+        orc.probe_mt(words, lnb, keys, threads)  # warm-up
+        runs = [orc.probe_mt(words, lnb, keys, threads) for _ in range(5)]
+        by_lag[lg] = (statistics.median(r[0] for r in runs), runs)
+    best = min(by_lag, key=lambda g: by_lag[g][0])
+    med, runs = by_lag[best]
+    orc.set_probe_lag(best)
     return {
         "value": sample / med,
         "unit": "keys/s",
@@ -444,10 +455,12 @@ def cpu_baseline(n_build: int, n_filter: int, p_permille: int, sample: int, thre
                    f"({n_build:.0e} keys inserted, sized for {n_filter:.0e} rows: 2^{lnb} blocks), {threads} "
                    f"std::threads ({threads_src}), 2048-row vectors, "
                    f"{'int32 keys zero-extended (same hashes), ' if key_type == 'i32' else ''}"
-                   f"hash included; median of 5 after 1 warm-up; build of the filter {n_build / build_s:.3e} keys/s"),
+                   f"hash included; median of 5 after 1 warm-up, the faster of the prefetch distances "
+                   f"{sorted(by_lag)}; build of the filter {n_build / build_s:.3e} keys/s"),
         "cpu_model": _cpu_model(),
         "survivors": runs[0][1],
         "prefetch_lag_rows": int(orc.lib().rpt_oracle_probe_lag()),
+        "keys_per_s_by_lag": {str(g): sample / v[0] for g, v in by_lag.items()},
     }
 
 
@@ -460,7 +473,7 @@ def _cgroup_cpu_stat() -> dict:
 
 
 def cpu_lag_sweep(n_build: int, n_filter: int, p_permille: int, sample: int, threads: int, lags: list,
-                  rounds: int) -> dict:
+                  rounds: int, pins: list = (0,)) -> dict:
     """The CPU baseline's probe loop at several prefetch lags, interleaved round by round in one process (same filter,
     same sample), so a neighbour's load on the shared host or the cgroup's CPU quota shows up in every lag alike
     instead of as a difference between them; each measurement is the median of 5 runs after a warm-up."""
@@ -473,19 +486,21 @@ def cpu_lag_sweep(n_build: int, n_filter: int, p_permille: int, sample: int, thr
     keys = orc.synth_probe_keys(sample, n_build, p_permille)
     out = []
     for r in range(rounds):
-        for lag in lags:
+        for pin, lag in ((p, g) for p in pins for g in lags):
+            orc.set_pin_mode(pin)
             orc.set_probe_lag(lag)
             orc.probe_mt(words, lnb, keys, threads)  # warm-up
             st0, la0, t0 = _cgroup_cpu_stat(), os.getloadavg(), time.perf_counter()
             runs = [orc.probe_mt(words, lnb, keys, threads) for _ in range(5)]
             st1, wall = _cgroup_cpu_stat(), time.perf_counter() - t0
             d = {k: st1[k] - st0.get(k, 0) for k in st1}
-            out.append({"round": r, "lag": lag, "keys_per_s": sample / statistics.median(x[0] for x in runs),
+            out.append({"round": r, "lag": lag, "pin": pin, "keys_per_s": sample / statistics.median(x[0] for x in runs),
                         "runs_s": [x[0] for x in runs], "wall_s": wall, "loadavg_1m_before": la0[0],
                         "cpu_usage_s": d.get("usage_usec", 0) / 1e6,
                         "throttled_s": d.get("throttled_usec", 0) / 1e6, "nr_throttled": d.get("nr_throttled", 0),
                         "survivors": runs[0][1]})
     orc.set_probe_lag(0)
+    orc.set_pin_mode(0)
     return {"threads": threads, "sample": sample, "filter_log_blocks": lnb, "cpu_model": _cpu_model(),
             "host_cpus": os.cpu_count(), "cpu_share": cpu_share(), "measurements": out}
 
@@ -559,7 +574,7 @@ def main():
         if args.cpu_lag_sweep:
             lags = [int(x) for x in args.cpu_lag_sweep.split(",")]
             sw = cpu_lag_sweep(n_build, n_filter, int(round(args.p * 1000)), sample, threads, lags,
-                               args.cpu_sweep_rounds)
+                               args.cpu_sweep_rounds, [int(x) for x in args.cpu_pin_sweep.split(",")])
             print(json.dumps({"cpu_lag_sweep": sw, "config": cfg}), flush=True)
             return
         if args.cpu_chain:

@@ -28,6 +28,9 @@
 //   * CPU baseline: morsel-parallel build/probe in 2048-row vectors, like DuckDB's parallel sink
 //     (physical_create_bf.hpp:43-45) and parallel operator (physical_use_bf.hpp:47-49), with an
 //     atomic fetch_or insert (README.md:32).
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -369,6 +372,29 @@ void rpt_oracle_synth_probe_keys(uint64_t n_build, uint32_t p_permille, uint64_t
 // Filters above 256 KiB prefetch each row's block while the vector is hashed, as Arrow's Find does
 // (bloom_filter.h:220-224): per core this matches libarrow_acero's Find (cpu_crosscheck.sh), so the
 // baseline is not a strawman.
+// Thread placement of the CPU baseline: 0 = the OS places the threads (the default); 1 = thread
+// t is pinned to the t-th CPU of the process's affinity mask, in mask order (on the GPU box's EPYC: consecutive
+// physical cores of one CCD, then the next); 2 = thread t to the (t * stride)-th CPU, spreading the threads over the
+// whole mask. The box grants 16 CPUs of quota with an affinity of all 256 hardware threads.
+static std::atomic<int> g_pin_mode{0};
+void rpt_oracle_set_pin_mode(int mode) { g_pin_mode.store(mode); }
+static void pin_thread(int t, int threads) {
+  const int mode = g_pin_mode.load();
+  if (mode == 0) return;
+  cpu_set_t all;
+  CPU_ZERO(&all);
+  if (sched_getaffinity(0, sizeof all, &all) != 0) return;
+  std::vector<int> cpus;
+  for (int c = 0; c < CPU_SETSIZE; c++)
+    if (CPU_ISSET(c, &all)) cpus.push_back(c);
+  if (cpus.empty()) return;
+  const size_t stride = mode == 2 ? std::max<size_t>(1, cpus.size() / static_cast<size_t>(std::max(1, threads))) : 1;
+  cpu_set_t one;
+  CPU_ZERO(&one);
+  CPU_SET(cpus[(static_cast<size_t>(t) * stride) % cpus.size()], &one);
+  (void)pthread_setaffinity_np(pthread_self(), sizeof one, &one);
+}
+
 constexpr uint64_t kPrefetchMinWords = (256u << 10) / 8;
 double rpt_oracle_build_mt(uint64_t* words, int log_nb, const int64_t* keys, uint64_t n, int threads) {
   const uint64_t nb = 1ULL << log_nb;
@@ -376,7 +402,8 @@ double rpt_oracle_build_mt(uint64_t* words, int log_nb, const int64_t* keys, uin
   auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> ts;
   for (int t = 0; t < std::max(1, threads); t++) {
-    ts.emplace_back([&] {
+    ts.emplace_back([&, t] {
+      pin_thread(t, threads);
       uint64_t hashes[kVectorSize];
       for (;;) {
         uint64_t base = next.fetch_add(kVectorSize, std::memory_order_relaxed);
@@ -425,7 +452,8 @@ double rpt_oracle_probe_chain_mt(const uint64_t* const* words, const int* log_nb
   auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> ts;
   for (int t = 0; t < std::max(1, threads); t++) {
-    ts.emplace_back([&] {
+    ts.emplace_back([&, t] {
+      pin_thread(t, threads);
       uint64_t hashes[kVectorSize];
       uint32_t sel[kVectorSize];
       uint64_t local = 0;

@@ -47,6 +47,7 @@ _SIG = {
     "rpt_oracle_probe_mt": (c_double, [c_void_p, c_int, c_void_p, c_uint64, c_int, POINTER(c_uint64)]),
     "rpt_oracle_probe_chain_mt": (c_double, [c_void_p, c_void_p, c_void_p, c_int, c_uint64, c_int, POINTER(c_uint64)]),
     "rpt_oracle_set_probe_lag": (None, [c_uint64]),
+    "rpt_oracle_set_pin_mode": (None, [c_int]),
     "rpt_oracle_probe_lag": (c_uint64, []),
 }
 
@@ -211,6 +212,11 @@ def probe_mt(words: np.ndarray, log_nb: int, keys: np.ndarray, threads: int) -> 
 def set_probe_lag(lag: int) -> None:
     """Rows between a row's hash + prefetch and its test in the CPU-baseline probe loop (0: the default, 24)."""
     lib().rpt_oracle_set_probe_lag(int(lag))
+
+
+def set_pin_mode(mode: int) -> None:
+    """CPU-baseline thread placement: 0 the OS's, 1 compact (mask order), 2 spread over the affinity mask."""
+    lib().rpt_oracle_set_pin_mode(int(mode))
 
 
 def probe_chain_mt(words: list, log_nbs: list, keys: list, threads: int) -> tuple[float, int]:
