@@ -339,6 +339,7 @@ def run_c5_merge(args, rank: int, world: int, device, comm, barrier, reduce_max,
         torch.cuda.synchronize()
         merge_s.append(time.perf_counter() - t0)
     del ws
+    mem.sample("merge_timed")
     torch.cuda.empty_cache()  # the merge's staging (RCCL rounds, or the torch composition's word copy)
     # untimed: the merged filter against a single build of all world * rows rows (inserted piece by piece),
     # compared on the device (rpt_bf_is_same_as: no word copies, so a rank holds its filter + the reference)

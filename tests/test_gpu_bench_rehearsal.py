@@ -82,9 +82,9 @@ def test_bench_multi_rank_rehearsal(world, tmp_path):
     # each rank holds at least its filter and the merge check's reference filter at once
     assert all(p >= 2 * C5_FILTER_BYTES for p in mem["section_peak_bytes_per_rank"]), mem
     assert all(p <= mem["device_total_bytes"] for p in mem["device_peak_used_bytes_per_rank"]), mem
-    assert set(mem["rank0_phase_used_bytes"]) == {"insert", "merge", "merge_check", "probe"}
+    assert set(mem["rank0_phase_used_bytes"]) == {"insert", "merge", "merge_timed", "merge_check", "probe"}
     # each rank's own footprint: at least its filter + the reference filter, and the 8 ranks' sum fits the device
     own = mem["rank_own_peak_bytes_per_rank"]
     assert len(own) == world and all(2 * C5_FILTER_BYTES <= p for p in own), own
-    assert set(mem["rank0_own_phase_bytes"]) == {"insert", "merge", "merge_check", "probe"}
+    assert set(mem["rank0_own_phase_bytes"]) == {"insert", "merge", "merge_timed", "merge_check", "probe"}
     assert 0 < c5["wall_s"] < time.monotonic() - t0
