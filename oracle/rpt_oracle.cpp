@@ -425,9 +425,10 @@ double rpt_oracle_build_mt(uint64_t* words, int log_nb, const int64_t* keys, uin
 }
 
 // Probe: per 2048-row vector hash -> LookupHashes into a per-thread SelectionVector
-// (physical_use_bf.hpp:16,23): the filter loop below with one filter. (Until r05 it had a loop of its own that
-// ran at half this rate at 16 threads on the GPU box's EPYC 9575F, same filter, keys and survivors, cause not
-// isolated: profiles/r05/cpu_baseline_check*.jsonl.) The survivors are counted (*out_count).
+// (physical_use_bf.hpp:16,23): the filter loop below with one filter. Until r05 it had a loop of its own, the
+// shape of rpt_oracle_set_probe_lag(2048), which ran at half this rate at 16 threads on r05's box; on r06's boxes it
+// is 1.4-1.8x faster. Which distance wins depends on the host's thread placement and neighbours, not on the loop
+// ("Why the CPU baseline moved 2x"), so bench.py runs both. The survivors are counted (*out_count).
 double rpt_oracle_probe_chain_mt(const uint64_t* const* words, const int* log_nb, const int64_t* const* keys, int k,
                                  uint64_t n, int threads, uint64_t* out_count);
 double rpt_oracle_probe_mt(const uint64_t* words, int log_nb, const int64_t* keys, uint64_t n, int threads,
