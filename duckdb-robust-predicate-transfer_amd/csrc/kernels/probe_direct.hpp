@@ -19,6 +19,13 @@ namespace rpt {
 #ifndef RPT_PROBE_PREFETCH
 #define RPT_PROBE_PREFETCH 2  // segments per prefetched group (0: off)
 #endif
+#ifndef RPT_LDS_I64_GROUP
+#define RPT_LDS_I64_GROUP 1  // segments per group in the int64 whole-filter LDS probe (r02: 2 and 3 were slower)
+#endif
+#ifndef RPT_PROBE_RING
+#define RPT_PROBE_RING 2  // register buffers of prefetched groups: 2 = ping-pong (group g + 1 in flight while g is
+                          // probed), 3 = groups g + 1 and g + 2 in flight
+#endif
 template <int K> struct RawSeg {
   static constexpr int V = KeyTraits<K>::kVec;
   static constexpr int kLoads = 8 / V;
@@ -83,10 +90,11 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
       // group is probed. Addresses past the last full segment are clamped and their rows discarded.
       // measured (ms per 1e9 keys, S = 1 / 2 / 3): 128 KiB LDS int64 1.68 / 1.79 / 1.77, int32 1.09 /
       // 1.05 / 1.06; 256 KiB gather 4.48 / 4.33 / 4.30
-      constexpr int S = (FILTER_IN_LDS && KeyTraits<K>::kVec == 2) ? 1 : RPT_PROBE_PREFETCH;
+      constexpr int S = (FILTER_IN_LDS && KeyTraits<K>::kVec == 2) ? RPT_LDS_I64_GROUP : RPT_PROBE_PREFETCH;
+      constexpr int NB = RPT_PROBE_RING;
       const bool ok[8] = {true, true, true, true, true, true, true, true};
       const uint64_t first = seg;
-      RawSeg<K> A[S], B[S];
+      RawSeg<K> R[NB][S];
       auto load_group = [&](RawSeg<K>(&R)[S], uint64_t g) {
 #pragma unroll
         for (int q = 0; q < S; q++) {
@@ -108,18 +116,22 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
         }
       };
       const uint64_t step = S * total_waves;
-      load_group(A, seg);
-      for (;;) {
-        load_group(B, seg + step);
-        asm volatile("" ::: "memory");  // issue the next group's loads before this one's work
-        probe_group(A, seg);
-        seg += step;
-        if (seg >= n_full) break;
-        load_group(A, seg + step);
-        asm volatile("" ::: "memory");
-        probe_group(B, seg);
-        seg += step;
-        if (seg >= n_full) break;
+#pragma unroll
+      for (int b = 0; b < NB - 1; b++) load_group(R[b], seg + b * step);
+      bool more = true;
+      while (more) {
+        // buffer b holds group seg; before probing it, the group NB - 1 steps ahead goes into the buffer the
+        // previous iteration freed (compile-time indices: the loop over b is unrolled)
+#pragma unroll
+        for (int b = 0; b < NB; b++) {
+          if (more) {
+            load_group(R[(b + NB - 1) % NB], seg + (NB - 1) * step);
+            asm volatile("" ::: "memory");  // issue the next group's loads before this one's work
+            probe_group(R[b], seg);
+            seg += step;
+            more = seg < n_full;
+          }
+        }
       }
       // the general loop resumes at this wave's first segment past the full ones
       seg = first + (n_full - first + total_waves - 1) / total_waves * total_waves;
