@@ -51,7 +51,7 @@ def _worker(rank, world, port, n_build, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])  # 8: the driver's largest scaling run
 def test_sharded_build_or_merge_and_probe(world):
     n_build = 30011
     ctx = mp.get_context("spawn")
@@ -111,7 +111,7 @@ def _rounds_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_or_allreduce_in_bounded_rounds(world):
     """The torch composition of the OR all-reduce in rounds (what bench's gloo rehearsal and --merge torch run on
     C5's 8 GiB filter: 256 MiB rounds): every round size, including one word per rank and one round over
