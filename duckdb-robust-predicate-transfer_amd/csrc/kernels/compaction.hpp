@@ -5,7 +5,7 @@
 
 namespace rpt {
 
-// ---- P2a: survivor count per group of 1024 segments --------------------------------------------
+// ---- P2a: survivor count per group of kGroupSegs (256) segments --------------------------------------------
 __global__ __launch_bounds__(kBlockThreads) void group_sum_kernel(const uint32_t* __restrict__ seg_counts,
                                                                  uint64_t n_segs, uint32_t* __restrict__ group_sums) {
   static_assert(kGroupSegs == kBlockThreads, "one segment count per thread");
@@ -56,6 +56,12 @@ __global__ __launch_bounds__(1024) void group_scan_kernel(const uint32_t* __rest
 constexpr uint32_t kCompactStage = RPT_COMPACT_STAGE;
 static_assert(kCompactStage == 8 * kSegRows || (RPT_SEL_BALLOT_EXPAND && kCompactStage >= 8 * RPT_COMPACT_BALLOT_MIN),
               "the LDS staging must hold every sparse step's survivors");
+// Group `group`'s 256 segments expanded into the sel, given the group's sel offset (s_off: every segment's offset,
+// filled by the caller); every wave of the workgroup calls it.
+__device__ __forceinline__ void compact_group(const uint64_t* __restrict__ bits, uint64_t n_segs, uint64_t group,
+                                              const uint32_t* s_off, uint16_t (*s_stage)[kCompactStage],
+                                              const uint32_t* __restrict__ row_sel, uint32_t* __restrict__ out_sel);
+
 __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* __restrict__ bits,
                                                                const uint32_t* __restrict__ seg_counts, uint64_t n_segs,
                                                                const uint32_t* __restrict__ group_offs,
@@ -77,6 +83,118 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
   for (uint32_t w = 0; w < wave; w++) off += s_wave[w];
   s_off[threadIdx.x] = off;
   __syncthreads();
+  compact_group(bits, n_segs, blockIdx.x, s_off, s_stage, row_sel, out_sel);
+}
+
+// ---- P2 + P3 in one launch: the groups' sel offsets by a decoupled look-back ------------------------
+// The direct probes' tail (gather / whole-filter LDS strategies) without group_sum_kernel and group_scan_kernel:
+// each workgroup takes the next group in order from a ticket counter (so every group it waits on belongs to a
+// workgroup that is already running), sums its 256 segment counts, publishes that aggregate at once, then walks
+// back over its predecessors' states 64 at a time (one wave) until it meets an inclusive prefix. A group's
+// aggregate needs only its 1 KiB of counts, so the predecessors publish within microseconds and the walk is short.
+// state[g]: bits 62-63 = 1 (aggregate) / 2 (inclusive prefix), bits 0-61 = the value; state[n_groups] = the
+// ticket counter. The probe kernel that wrote the counts zeroed them (phase 1), so no extra launch clears them.
+// Every wait is bounded: a walk that does not complete in kLookbackSpins polls falls back to summing its
+// predecessors' segment counts itself (correct, slow, never a hang).
+#ifndef RPT_LB_TICKET
+#define RPT_LB_TICKET 1  // groups taken from a ticket counter (1) or by blockIdx (0)
+#endif
+constexpr uint64_t kLbAgg = 1ULL << 62, kLbIncl = 2ULL << 62, kLbValue = (1ULL << 62) - 1;
+constexpr uint32_t kLookbackSpins = 1u << 16;
+// A state word carries its own value, so relaxed device-scope atomics suffice: nothing else is published with it.
+// (Release / acquire at agent scope would write back / invalidate the XCD's L2 on every publish and poll: a
+// first version with them took 0.95 ms instead of 0.15.)
+__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+  for (int d = 32; d >= 1; d >>= 1) v += static_cast<uint64_t>(__shfl_xor(static_cast<unsigned long long>(v), d, 64));
+  return v;
+}
+__global__ __launch_bounds__(kBlockThreads) void compact_lookback_kernel(const uint64_t* __restrict__ bits,
+                                                                        const uint32_t* __restrict__ seg_counts,
+                                                                        uint64_t n_segs, uint32_t n_groups,
+                                                                        uint64_t* __restrict__ state,
+                                                                        const uint32_t* __restrict__ row_sel,
+                                                                        uint32_t* __restrict__ out_sel,
+                                                                        uint64_t* __restrict__ out_count) {
+  __shared__ uint32_t s_off[kGroupSegs];
+  __shared__ uint32_t s_wave[kWavesPerBlock];
+  __shared__ uint16_t s_stage[kWavesPerBlock][kCompactStage];
+  __shared__ uint32_t s_group;
+  __shared__ uint64_t s_prefix;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#if RPT_LB_TICKET
+  if (threadIdx.x == 0)
+    s_group = __hip_atomic_fetch_add(reinterpret_cast<uint32_t*>(state + n_groups), 1u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint32_t g = s_group;
+#else
+  // workgroups are dispatched in blockIdx order, so every group a workgroup waits on is already running (and the
+  // bounded wait would fall back to a direct sum if that ever failed)
+  const uint32_t g = blockIdx.x;
+  (void)s_group;
+#endif
+  const uint64_t sidx = static_cast<uint64_t>(g) * kGroupSegs + threadIdx.x;
+  const uint32_t c = sidx < n_segs ? seg_counts[sidx] : 0u;
+  const uint32_t incl = wave_inclusive_sum(c);
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  if (wave == 0) {
+    const uint64_t total = static_cast<uint64_t>(s_wave[0]) + s_wave[1] + s_wave[2] + s_wave[3];
+    if (lane == 0)
+      lb_store(state + g, (g == 0 ? kLbIncl : kLbAgg) | total);
+    uint64_t prefix = 0;
+    if (g > 0) {
+      int64_t top = static_cast<int64_t>(g) - 1;  // the window is groups top - 63 .. top, lane l reads top - l
+      uint32_t spins = 0;
+      bool done = false;
+      while (!done) {
+        const int64_t idx = top - static_cast<int64_t>(lane);
+        const uint64_t v = idx >= 0 ? lb_load(state + idx) : kLbIncl;  // before group 0: an inclusive 0
+        const uint64_t incl_mask = __ballot((v & ~kLbValue) == kLbIncl);
+        const uint64_t ready_mask = __ballot((v & ~kLbValue) != 0);
+        // lanes up to the nearest inclusive prefix (all 64 if none) must have published
+        const uint64_t need = incl_mask ? (incl_mask & (0ULL - incl_mask)) * 2 - 1 : ~0ULL;
+        if ((ready_mask & need) != need) {
+          if (++spins >= kLookbackSpins) break;  // fall back below
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += wave_sum64(((need >> lane) & 1) ? (v & kLbValue) : 0);
+        if (incl_mask) done = true;
+        else top -= 64;
+      }
+      if (!done) {  // bounded wait exceeded: sum every predecessor's segment counts directly
+        uint64_t s = 0;
+        for (uint64_t i = lane; i < static_cast<uint64_t>(g) * kGroupSegs; i += 64) s += seg_counts[i];
+        prefix = wave_sum64(s);
+      }
+      if (lane == 0)
+        lb_store(state + g, kLbIncl | (prefix + total));
+    }
+    if (lane == 0) {
+      s_prefix = prefix;
+      if (g == n_groups - 1) *out_count = prefix + total;
+    }
+  }
+  __syncthreads();
+  uint32_t off = static_cast<uint32_t>(s_prefix) + incl - c;
+  for (uint32_t w = 0; w < wave; w++) off += s_wave[w];
+  s_off[threadIdx.x] = off;
+  __syncthreads();
+  compact_group(bits, n_segs, g, s_off, s_stage, row_sel, out_sel);
+}
+
+__device__ __forceinline__ void compact_group(const uint64_t* __restrict__ bits, uint64_t n_segs, uint64_t group,
+                                              const uint32_t* s_off, uint16_t (*s_stage)[kCompactStage],
+                                              const uint32_t* __restrict__ row_sel, uint32_t* __restrict__ out_sel) {
+  const uint64_t g0 = group * kGroupSegs;
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t n_words = n_segs * kWordsPerSeg;
   // Each wave expands 8 segments (64 words = 4096 rows) per step: survivors are first written to the
   // wave's LDS buffer in row order, then streamed out with coalesced stores.

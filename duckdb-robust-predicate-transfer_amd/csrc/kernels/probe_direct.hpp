@@ -64,13 +64,17 @@ __device__ __forceinline__ void probe8(const uint64_t* __restrict__ words, const
   for (int j = 0; j < 8; j++) pass[j] = ok[j] && (w[j] & m[j]) == m[j];
 }
 
+// zero[0 .. n_zero): words the selection-vector tail's look-back needs cleared (compact_lookback_kernel's group
+// states and ticket), cleared here so the tail needs no launch of its own; nullptr when there is no such tail.
 template <int K, bool DENSE, bool FILTER_IN_LDS, int THREADS = kBlockThreads>
 __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __restrict__ words,
                                                                   uint64_t block_mask, KeyArgs a, uint64_t n,
                                                                   uint64_t n_segs, uint64_t* __restrict__ out_bits,
-                                                                  uint32_t* __restrict__ seg_counts) {
+                                                                  uint32_t* __restrict__ seg_counts,
+                                                                  uint64_t* __restrict__ zero, uint32_t n_zero) {
   __shared__ uint64_t s_masks[kNumMasks];
   extern __shared__ uint64_t s_filter[];
+  for (uint32_t i = blockIdx.x * THREADS + threadIdx.x; i < n_zero; i += gridDim.x * THREADS) zero[i] = 0;
   fill_mask_table(s_masks);
   if constexpr (FILTER_IN_LDS) {
     for (uint64_t i = threadIdx.x; i <= block_mask; i += blockDim.x) s_filter[i] = words[i];

@@ -58,6 +58,10 @@
 #define RPT_L1_FIXED_PCT 0
 #endif
 
+#ifndef RPT_LOOKBACK_TAIL
+#define RPT_LOOKBACK_TAIL 0  // 1: the direct strategies' sel tail in one look-back launch (measured slower, DESIGN §5 rejected list)
+#endif
+
 // The product build runs the tuning macros at the defaults the GPU suite tests. Other values exist for
 // A/B timing only (tools/build_variants.sh builds them under other names, without RPT_PRODUCT_BUILD);
 // several were never run through the parity suite (tuning macros).
@@ -66,7 +70,7 @@ static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG 
                   RPT_L1_FIXED_PCT == 0 && RPT_BUCKET_UNPERMUTE_THREADS == 256 && RPT_SLICE_UNROLL == 4 &&
                   RPT_PARTITION_MIN_WAVES == 8 && RPT_PROBE_PREFETCH == 2 && RPT_SEL_BALLOT_MIN == 192 &&
                   RPT_COMPACT_BALLOT_MIN == 384 && RPT_COMPACT_STAGE == 3072 && RPT_LDS_I64_GROUP == 1 &&
-                  RPT_PROBE_RING == 2,
+                  RPT_PROBE_RING == 2 && RPT_LOOKBACK_TAIL == 0,
               "product build: tuning macros must keep their tested defaults (use tools/build_variants.sh)");
 static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
                   RPT_NT_REC_LOADS == 0 && RPT_NT_SLICE_LOADS == 1 && RPT_PARK_LANE_MAJOR == 1 && RPT_SLICE_XCD_MAP == 1 &&
@@ -419,6 +423,7 @@ struct ProbeWorkspace {
   uint16_t* pos1;          // row -> position in its level-1 tile's bucket-sorted order
   uint64_t* bits2;         // level-2 result bits (w-space order)
   uint32_t* heavy;         // partitioned: [slice] epoch stamp of a slice skewed probe keys overload (rpt::SkewItems)
+  uint64_t* lb_state;      // gather / LDS: [group] look-back states + [n_groups] ticket (compact_lookback_kernel)
 };
 
 uint32_t slice_count(int log_num_blocks) {
@@ -533,14 +538,21 @@ uint32_t tile_mult_of(uint32_t n_slices) {
 // Layout (all 256-aligned): bits | seg_counts | group_sums | group_offs, then for the partitioned
 // strategy recs | pos | passb | runs | runs_tm (whole 16 Ki-row tiles), and for the bucketed one the
 // same level-2 arrays over level2_tiles_max tiles of 256 slices plus the level-1 arrays.
+// RPT_LOOKBACK_TAIL = 1 runs the direct strategies' selection-vector tail as one look-back launch
+// (compact_lookback_kernel) instead of group sums + their scan + the compaction; measured slower, so off.
+bool lookback_tail(int strategy) {
+  return RPT_LOOKBACK_TAIL && (strategy == RPT_PROBE_GATHER || strategy == RPT_PROBE_LDS);
+}
+
 size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base, ProbeWorkspace* ws) {
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
   const uint64_t T = rpt::kTileRows;
-  constexpr int kParts = 21;
+  constexpr int kParts = 22;
   size_t sz[kParts] = {align256(n_segs * rpt::kWordsPerSeg * 8), align256(n_groups * rpt::kGroupSegs * 4),
                        align256(n_groups * 4), align256(n_groups * 4)};
   const bool part = strategy == RPT_PROBE_PARTITIONED, buck = strategy == RPT_PROBE_BUCKETED;
+  if (lookback_tail(strategy)) sz[21] = align256((n_groups + 1) * 8);
   if (part || buck) {
     const uint32_t slices = part ? slice_count(log_num_blocks) : rpt::kBucketSlices;
     const uint32_t tm = part ? tile_mult_of(slices) : 1u;
@@ -595,6 +607,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
     ws->bits2 = static_cast<uint64_t*>(at(18));
     ws->hash_hi = static_cast<uint8_t*>(at(19));
     ws->heavy = static_cast<uint32_t*>(at(20));
+    ws->lb_state = static_cast<uint64_t*>(at(21));
   }
   return total;
 }
@@ -701,10 +714,11 @@ unsigned persistent_grid(int device, uint64_t n_segs) {
 
 template <int K, bool D>
 void launch_probe_bits_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
-                         uint64_t n_segs, uint64_t* bits, uint32_t* counts) {
+                         uint64_t n_segs, uint64_t* bits, uint32_t* counts, uint64_t* zero = nullptr,
+                         uint32_t n_zero = 0) {
   ProfScope prof(inst_name<K, D, false, rpt::kBlockThreads>("probe_bits_kernel"), s);
   hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, false>), dim3(grid), dim3(rpt::kBlockThreads), 0, s, bf->words,
-                     (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+                     (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts, zero, n_zero);
   prof.end();
 }
 
@@ -723,13 +737,13 @@ void launch_probe_small_t(hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a
 void allow_dynamic_lds(const void* fn);
 template <int K, bool D>
 void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
-                             uint64_t n_segs, uint64_t* bits, uint32_t* counts) {
+                             uint64_t n_segs, uint64_t* bits, uint32_t* counts, uint64_t* zero, uint32_t n_zero) {
   const size_t lds = 8ULL << bf->log_num_blocks;
   static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::probe_bits_kernel<K, D, true, rpt::kLdsProbeThreads>)); });
   ProfScope prof(inst_name<K, D, true, rpt::kLdsProbeThreads>("probe_bits_kernel"), s);
   hipLaunchKernelGGL((rpt::probe_bits_kernel<K, D, true, rpt::kLdsProbeThreads>), dim3(grid), dim3(rpt::kLdsProbeThreads), lds,
-                     s, bf->words, (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts);
+                     s, bf->words, (1ULL << bf->log_num_blocks) - 1, a, n, n_segs, bits, counts, zero, n_zero);
   prof.end();
 }
 
@@ -1393,9 +1407,12 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, row_sel};
   const bool dense = dense_ok(col, row_sel);
+  // the look-back tail's group states and ticket, cleared by the probe kernel (compact_lookback_kernel)
+  const uint32_t lb_words = ws.lb_state ? static_cast<uint32_t>(ceil_div(n_segs, rpt::kGroupSegs) + 1) : 0u;
   if (strategy == RPT_PROBE_GATHER) {
     const unsigned grid = persistent_grid(bf->device, n_segs);
-    RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
+    RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts,
+                    ws.lb_state, lb_words);
     RPT_LAUNCHED("probe_bits_kernel");
   } else if (strategy == RPT_PROBE_LDS) {
     const uint64_t lds = (8ULL << L) + 8ULL * rpt::kNumMasks;
@@ -1403,7 +1420,8 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
     const uint64_t waves = rpt::kLdsProbeThreads / 64;  // launch_probe_bits_lds_t
     const unsigned grid = static_cast<unsigned>(
         std::max<uint64_t>(1, std::min(ceil_div(n_segs, waves), num_cus(bf->device) * per_cu)));
-    RPT_DISPATCH_KD(launch_probe_bits_lds_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts);
+    RPT_DISPATCH_KD(launch_probe_bits_lds_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts,
+                    ws.lb_state, lb_words);
     RPT_LAUNCHED("probe_bits_kernel<lds>");
   } else {
     // PARTITIONED: the key column, tiles of slice_count(L) slices. BUCKETED: level 1 first, then the
@@ -1563,6 +1581,16 @@ int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, u
   workspace_layout(n, L, strategy, workspace, &ws);
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
+  if (lookback_tail(strategy)) {
+    // one launch: group offsets by look-back (phase 1's probe kernel cleared the states and the ticket)
+    ProfScope prof10_("compact_lookback_kernel", s);
+    hipLaunchKernelGGL(rpt::compact_lookback_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,
+                       ws.bits, ws.seg_counts, n_segs, static_cast<uint32_t>(n_groups), ws.lb_state, row_sel, out_sel,
+                       out_count_dev);
+    prof10_.end();
+    RPT_LAUNCHED("compact_lookback_kernel");
+    return RPT_OK;
+  }
   ProfScope prof8_("group_sum_kernel", s);
   hipLaunchKernelGGL(rpt::group_sum_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,
                      ws.seg_counts, n_segs, ws.group_sums);

@@ -5,7 +5,7 @@ set -o pipefail
 mkdir -p gpurun_out/ab
 V=$PWD/duckdb-robust-predicate-transfer_amd/build/variants
 for rep in 1 2 3; do
-for args in "--config JOBDIM" "--config JOBDIM --key-type i32" "--build-rows 2e5 --filter-rows 2e5"; do
+for args in "--config JOBDIM" "--config JOBDIM --key-type i32" "--build-rows 2e5 --filter-rows 2e5 --strategy gather"; do
 for v in "$@"; do
   tag=$(echo "$v $args" | tr -c 'A-Za-z0-9\n' _)
   RPT_GPU_LIB=$V/librpt_gpu_$v.so timeout -k 10 200 python bench.py $args --steps 10 --warmup 2 --no-cpu-baseline --no-stream-calibration > gpurun_out/ab/$tag.$rep.json 2> gpurun_out/ab/$tag.$rep.err || { echo "bench $v $args failed"; tail -5 gpurun_out/ab/$tag.$rep.err; exit 1; }
