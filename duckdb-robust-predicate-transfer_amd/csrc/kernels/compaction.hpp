@@ -54,12 +54,22 @@ __global__ __launch_bounds__(1024) void group_scan_kernel(const uint32_t* __rest
 #define RPT_COMPACT_STAGE (RPT_SEL_BALLOT_EXPAND ? 8 * RPT_COMPACT_BALLOT_MIN : 8 * 512)
 #endif
 constexpr uint32_t kCompactStage = RPT_COMPACT_STAGE;
+// RPT_COMPACT_V16 = 1: sparse steps write their staged survivors as 16-B units aligned to the destination (4-B
+// stores only at the region's two ends) instead of one 4-B store per lane. A plain 4-B-per-lane write stream runs
+// at 4.4 TB/s, a 16-B one at 6.6, and compact's region pattern gains 0.01 ms from them with placeholder values
+// (tools/ubench/ubench_compact.hip) -- but the kernel itself measured 0.155-0.159 vs 0.147-0.152 ms with them
+// (profiles/r06/ab_compact_v16.txt), so off.
+#ifndef RPT_COMPACT_V16
+#define RPT_COMPACT_V16 0
+#endif
+// a staging row holds kCompactStage survivors behind up to 3 entries of alignment shift
+constexpr uint32_t kCompactStageRow = kCompactStage + (RPT_COMPACT_V16 ? 4 : 0);
 static_assert(kCompactStage == 8 * kSegRows || (RPT_SEL_BALLOT_EXPAND && kCompactStage >= 8 * RPT_COMPACT_BALLOT_MIN),
               "the LDS staging must hold every sparse step's survivors");
 // Group `group`'s 256 segments expanded into the sel, given the group's sel offset (s_off: every segment's offset,
 // filled by the caller); every wave of the workgroup calls it.
 __device__ __forceinline__ void compact_group(const uint64_t* __restrict__ bits, uint64_t n_segs, uint64_t group,
-                                              const uint32_t* s_off, uint16_t (*s_stage)[kCompactStage],
+                                              const uint32_t* s_off, uint16_t (*s_stage)[kCompactStageRow],
                                               const uint32_t* __restrict__ row_sel, uint32_t* __restrict__ out_sel);
 
 __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* __restrict__ bits,
@@ -71,7 +81,7 @@ __global__ __launch_bounds__(kBlockThreads) void compact_kernel(const uint64_t* 
   __shared__ uint32_t s_wave[kWavesPerBlock];
   // one 4096-row step's survivors per wave (row offsets); a step only stages when it has fewer than
   // 8 * RPT_COMPACT_BALLOT_MIN survivors (denser steps expand word by word), so that many entries suffice
-  __shared__ uint16_t s_stage[kWavesPerBlock][kCompactStage];
+  __shared__ __attribute__((aligned(16))) uint16_t s_stage[kWavesPerBlock][kCompactStageRow];
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * kGroupSegs;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t sidx = g0 + threadIdx.x;
@@ -123,7 +133,7 @@ __global__ __launch_bounds__(kBlockThreads) void compact_lookback_kernel(const u
                                                                         uint64_t* __restrict__ out_count) {
   __shared__ uint32_t s_off[kGroupSegs];
   __shared__ uint32_t s_wave[kWavesPerBlock];
-  __shared__ uint16_t s_stage[kWavesPerBlock][kCompactStage];
+  __shared__ __attribute__((aligned(16))) uint16_t s_stage[kWavesPerBlock][kCompactStageRow];
   __shared__ uint32_t s_group;
   __shared__ uint64_t s_prefix;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -191,7 +201,7 @@ __global__ __launch_bounds__(kBlockThreads) void compact_lookback_kernel(const u
 }
 
 __device__ __forceinline__ void compact_group(const uint64_t* __restrict__ bits, uint64_t n_segs, uint64_t group,
-                                              const uint32_t* s_off, uint16_t (*s_stage)[kCompactStage],
+                                              const uint32_t* s_off, uint16_t (*s_stage)[kCompactStageRow],
                                               const uint32_t* __restrict__ row_sel, uint32_t* __restrict__ out_sel) {
   const uint64_t g0 = group * kGroupSegs;
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -230,19 +240,47 @@ __device__ __forceinline__ void compact_group(const uint64_t* __restrict__ bits,
       continue;
     }
 #endif
+    uint32_t* dst = out_sel + s_off[b * 8];
+    const uint32_t step_row = static_cast<uint32_t>(seg0 * kSegRows);
+#if RPT_COMPACT_V16
+    // entry j of the region is staged at buf[a + j], a = the destination's 4-B offset within its 16-B unit, so
+    // staging unit u (buf[4u .. 4u+3], one 8-B LDS read) maps onto the aligned 16-B destination unit u
+    const uint32_t a = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(dst) >> 2) & 3u;
+    uint32_t p = incl - pc + a;
+#else
     uint32_t p = incl - pc;
+#endif
     while (word) {
       buf[p++] = static_cast<uint16_t>(lane * 64 + __builtin_ctzll(word));
       word &= word - 1;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    uint32_t* dst = out_sel + s_off[b * 8];
-    const uint32_t step_row = static_cast<uint32_t>(seg0 * kSegRows);
+#if RPT_COMPACT_V16
+    uint32_t* base = dst - a;  // 16-B aligned
+    const uint32_t end = a + total, n_units = (end + 3) >> 2;
+    for (uint32_t u = lane; u < n_units; u += 64) {
+      const uint64_t v4 = *reinterpret_cast<const uint64_t*>(buf + 4 * u);
+      uint32_t r[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        r[e] = step_row + static_cast<uint32_t>((v4 >> (16 * e)) & 0xffffu);
+        if (row_sel && 4 * u + e >= a && 4 * u + e < end) r[e] = row_sel[r[e]];
+      }
+      if (4 * u >= a && 4 * u + 4 <= end) {
+        *reinterpret_cast<u32x4*>(base + 4 * u) = u32x4{r[0], r[1], r[2], r[3]};
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++)
+          if (4 * u + e >= a && 4 * u + e < end) base[4 * u + e] = r[e];
+      }
+    }
+#else
     for (uint32_t q = lane; q < total; q += 64) {
       const uint32_t row = step_row + buf[q];
       dst[q] = row_sel ? row_sel[row] : row;
     }
+#endif
     __builtin_amdgcn_wave_barrier();
   }
 }
