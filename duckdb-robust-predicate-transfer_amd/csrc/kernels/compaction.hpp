@@ -45,6 +45,96 @@ __global__ __launch_bounds__(1024) void group_scan_kernel(const uint32_t* __rest
   }
 }
 
+// ---- P2a + P2b in one launch (direct strategies; RPT_SUMSCAN_TAIL=1, off) -------------------------
+// group_sum_kernel's work, after which the highest-numbered workgroup scans the group sums as group_scan_kernel
+// does: one dependent launch fewer. Built because a kernel trace showed ~10 us of idle GPU before each dependent
+// launch (profiles/r06/jobdim_kernel_gaps.txt) -- but those gaps were the profiling events' own: without them the
+// step's kernels run back to back (profiles/r06/kernel_events_overhead.txt), and this kernel (0.024 ms with the
+// scan's tile in registers, 0.030-0.035 with this LDS-staged tile) is slower than the two it replaces (0.016 ms),
+// so it stays off. state[g] = kSumValid | group g's sum; the probe kernel cleared the words and the scanning workgroup clears them again as it reads them (a repeated
+// phase 2 also works). Workgroups are dispatched in index order, so when the last one runs every other one is
+// running or done and its wait is short. Measured on the way (tools/ubench/ubench_sumscan.hip,
+// profiles/r06/ubench_sumscan.txt): a release per workgroup (an L2 write-back) made the kernel 0.17 ms, and a
+// "last workgroup done" counter 0.09 ms more (7630 same-address atomics serialize at ~12 ns each), against 0.007
+// for the sums alone. Each sum carries its own valid bit, so relaxed agent-scope atomics suffice; the scanning
+// workgroup reads them with atomic exchanges (performed at the coherence point, and clearing as they read), and a
+// sum still invalid after kSumSpins polls is recomputed from the segment counts (correct, slow, never a hang).
+#ifndef RPT_SCAN_ROWS
+#define RPT_SCAN_ROWS 32
+#endif
+constexpr uint32_t kScanRows = RPT_SCAN_ROWS;  // the scanning workgroup's tiles: kScanRows x 256 group sums in LDS
+constexpr uint32_t kSumValid = 1u << 31, kSumSpins = 1u << 12;
+__global__ __launch_bounds__(kBlockThreads) void group_sum_scan_kernel(const uint32_t* __restrict__ seg_counts,
+                                                                      uint64_t n_segs, uint32_t n_groups,
+                                                                      uint32_t* __restrict__ state,
+                                                                      uint32_t* __restrict__ group_offs,
+                                                                      uint64_t* __restrict__ out_count) {
+  static_assert(kGroupSegs == kBlockThreads, "one segment count per thread");
+  constexpr uint32_t kTile = kScanRows * kBlockThreads;
+  __shared__ uint32_t s_part[kWavesPerBlock];
+  __shared__ uint32_t s_wt[kWavesPerBlock][kScanRows];
+  __shared__ uint32_t s_tile[kTile];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kGroupSegs + threadIdx.x;
+  uint32_t s = i < n_segs ? seg_counts[i] : 0u;
+  s = wave_sum(s);
+  if (lane == 0) s_part[wave] = s;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(state + blockIdx.x, kSumValid | (s_part[0] + s_part[1] + s_part[2] + s_part[3]),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (blockIdx.x != n_groups - 1) return;
+  // tile element (row k, thread t) is group base + k * 256 + t: all of a tile's exchanges are in flight at once;
+  // the scan runs along rows (one wave scan per row) then down the row totals
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < n_groups; base += kTile) {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanRows; k++) {
+      const uint32_t g = base + k * kBlockThreads + threadIdx.x;
+      s_tile[k * kBlockThreads + threadIdx.x] =
+          g < n_groups ? __hip_atomic_exchange(state + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kSumValid;
+    }
+    // sums not visible yet (rare): wait for them, bounded, then recompute from the segment counts
+    for (uint32_t k = 0; k < kScanRows; k++) {
+      const uint32_t g = base + k * kBlockThreads + threadIdx.x;
+      uint32_t v = s_tile[k * kBlockThreads + threadIdx.x];
+      if (v & kSumValid) continue;
+      for (uint32_t spins = 0; !(v & kSumValid) && spins < kSumSpins; spins++) {
+        __builtin_amdgcn_s_sleep(1);
+        v = __hip_atomic_exchange(state + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (!(v & kSumValid)) {
+        uint32_t c = 0;
+        for (uint64_t q = static_cast<uint64_t>(g) * kGroupSegs; q < n_segs && q < (g + 1ULL) * kGroupSegs; q++)
+          c += seg_counts[q];
+        v = kSumValid | c;
+      }
+      s_tile[k * kBlockThreads + threadIdx.x] = v;
+    }
+    // row totals per wave first, the rows' wave scans again afterwards (recomputing 6 DPP adds per row instead of
+    // holding 32 more registers: this kernel's register count sets the occupancy of its short sum phase)
+#pragma unroll
+    for (uint32_t k = 0; k < kScanRows; k++) {
+      const uint32_t tot = wave_sum(s_tile[k * kBlockThreads + threadIdx.x] & ~kSumValid);
+      if (lane == 0) s_wt[wave][k] = tot;
+    }
+    __syncthreads();
+    uint32_t row_base = carry;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanRows; k++) {
+      const uint32_t v = s_tile[k * kBlockThreads + threadIdx.x] & ~kSumValid;
+      uint32_t before = 0;
+      for (uint32_t w = 0; w < wave; w++) before += s_wt[w][k];
+      const uint32_t g = base + k * kBlockThreads + threadIdx.x;
+      if (g < n_groups) group_offs[g] = row_base + before + wave_inclusive_sum(v) - v;
+      row_base += s_wt[0][k] + s_wt[1][k] + s_wt[2][k] + s_wt[3][k];
+    }
+    carry = row_base;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out_count = carry;
+}
+
 // ---- P3: expand result bits into an ascending selection vector ----------------------------------
 // Entries of each wave's staging buffer. 8 * RPT_COMPACT_BALLOT_MIN (3072, 6 KiB per wave) rather than a whole
 // step's 4096 rows: 24 KiB of LDS per workgroup lets 6 workgroups share a CU instead of 4 (the kernel waits on

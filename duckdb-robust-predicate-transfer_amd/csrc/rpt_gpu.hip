@@ -61,6 +61,9 @@
 #ifndef RPT_LOOKBACK_TAIL
 #define RPT_LOOKBACK_TAIL 0  // 1: the direct strategies' sel tail in one look-back launch (measured slower, DESIGN §5 rejected list)
 #endif
+#ifndef RPT_SUMSCAN_TAIL
+#define RPT_SUMSCAN_TAIL 0  // 1: the direct strategies' group sums and their scan in one launch (measured: no gain)
+#endif
 
 // The product build runs the tuning macros at the defaults the GPU suite tests. Other values exist for
 // A/B timing only (tools/build_variants.sh builds them under other names, without RPT_PRODUCT_BUILD);
@@ -70,7 +73,7 @@ static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG 
                   RPT_L1_FIXED_PCT == 0 && RPT_BUCKET_UNPERMUTE_THREADS == 256 && RPT_SLICE_UNROLL == 4 &&
                   RPT_PARTITION_MIN_WAVES == 8 && RPT_PROBE_PREFETCH == 2 && RPT_SEL_BALLOT_MIN == 192 &&
                   RPT_COMPACT_BALLOT_MIN == 384 && RPT_COMPACT_STAGE == 3072 && RPT_LDS_I64_GROUP == 1 &&
-                  RPT_PROBE_RING == 2 && RPT_LOOKBACK_TAIL == 0 && RPT_COMPACT_V16 == 0,
+                  RPT_PROBE_RING == 2 && RPT_LOOKBACK_TAIL == 0 && RPT_COMPACT_V16 == 0 && RPT_SUMSCAN_TAIL == 0,
               "product build: tuning macros must keep their tested defaults (use tools/build_variants.sh)");
 static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
                   RPT_NT_REC_LOADS == 0 && RPT_NT_SLICE_LOADS == 1 && RPT_PARK_LANE_MAJOR == 1 && RPT_SLICE_XCD_MAP == 1 &&
@@ -423,7 +426,8 @@ struct ProbeWorkspace {
   uint16_t* pos1;          // row -> position in its level-1 tile's bucket-sorted order
   uint64_t* bits2;         // level-2 result bits (w-space order)
   uint32_t* heavy;         // partitioned: [slice] epoch stamp of a slice skewed probe keys overload (rpt::SkewItems)
-  uint64_t* lb_state;      // gather / LDS: [group] look-back states + [n_groups] ticket (compact_lookback_kernel)
+  uint64_t* lb_state;      // gather / LDS: [group] look-back states + [n_groups] ticket (compact_lookback_kernel),
+                           // or group_sum_scan_kernel's flagged group sums (u32); cleared by the probe kernel
 };
 
 uint32_t slice_count(int log_num_blocks) {
@@ -543,6 +547,11 @@ uint32_t tile_mult_of(uint32_t n_slices) {
 bool lookback_tail(int strategy) {
   return RPT_LOOKBACK_TAIL && (strategy == RPT_PROBE_GATHER || strategy == RPT_PROBE_LDS);
 }
+// RPT_SUMSCAN_TAIL: the direct strategies' group sums + scan as one launch whose highest-numbered workgroup scans
+// (flagged group sums the probe kernel clears), then the compaction: two dependent launches after the probe, not three.
+bool sumscan_tail(int strategy) {
+  return RPT_SUMSCAN_TAIL && !lookback_tail(strategy) && (strategy == RPT_PROBE_GATHER || strategy == RPT_PROBE_LDS);
+}
 
 size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base, ProbeWorkspace* ws) {
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
@@ -553,6 +562,7 @@ size_t workspace_layout(uint64_t n, int log_num_blocks, int strategy, void* base
                        align256(n_groups * 4), align256(n_groups * 4)};
   const bool part = strategy == RPT_PROBE_PARTITIONED, buck = strategy == RPT_PROBE_BUCKETED;
   if (lookback_tail(strategy)) sz[21] = align256((n_groups + 1) * 8);
+  if (sumscan_tail(strategy)) sz[21] = align256(n_groups * 4);
   if (part || buck) {
     const uint32_t slices = part ? slice_count(log_num_blocks) : rpt::kBucketSlices;
     const uint32_t tm = part ? tile_mult_of(slices) : 1u;
@@ -1407,8 +1417,12 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
   const uint64_t n_segs = ceil_div(n, rpt::kSegRows);
   const rpt::KeyArgs a{col->keys, col->key_sel, col->validity, row_sel};
   const bool dense = dense_ok(col, row_sel);
-  // the look-back tail's group states and ticket, cleared by the probe kernel (compact_lookback_kernel)
-  const uint32_t lb_words = ws.lb_state ? static_cast<uint32_t>(ceil_div(n_segs, rpt::kGroupSegs) + 1) : 0u;
+  // the look-back tail's group states and ticket (compact_lookback_kernel) or the sum+scan tail's flagged group
+  // sums (group_sum_scan_kernel), cleared by the probe kernel (64-bit words)
+  const uint64_t n_groups = ceil_div(n_segs, rpt::kGroupSegs);
+  const uint32_t lb_words = !ws.lb_state ? 0u
+                            : lookback_tail(strategy) ? static_cast<uint32_t>(n_groups + 1)
+                                                      : static_cast<uint32_t>(ceil_div(n_groups, 2));
   if (strategy == RPT_PROBE_GATHER) {
     const unsigned grid = persistent_grid(bf->device, n_segs);
     RPT_DISPATCH_KD(launch_probe_bits_t, col->key_type, dense, grid, s, bf, a, n, n_segs, ws.bits, ws.seg_counts,
@@ -1589,6 +1603,21 @@ int rpt_bf_probe_phase2(const rpt_bf* bf, const uint32_t* row_sel, uint64_t n, u
                        out_count_dev);
     prof10_.end();
     RPT_LAUNCHED("compact_lookback_kernel");
+    return RPT_OK;
+  }
+  if (sumscan_tail(strategy)) {
+    // group sums + scan in one launch (phase 1's probe kernel cleared the done counter), then the compaction
+    ProfScope prof8_("group_sum_scan_kernel", s);
+    hipLaunchKernelGGL(rpt::group_sum_scan_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,
+                       ws.seg_counts, n_segs, static_cast<uint32_t>(n_groups), reinterpret_cast<uint32_t*>(ws.lb_state),
+                       ws.group_offs, out_count_dev);
+    prof8_.end();
+    RPT_LAUNCHED("group_sum_scan_kernel");
+    ProfScope prof10_("compact_kernel", s);
+    hipLaunchKernelGGL(rpt::compact_kernel, dim3(static_cast<unsigned>(n_groups)), dim3(rpt::kBlockThreads), 0, s,
+                       ws.bits, ws.seg_counts, n_segs, ws.group_offs, row_sel, out_sel);
+    prof10_.end();
+    RPT_LAUNCHED("compact_kernel");
     return RPT_OK;
   }
   ProfScope prof8_("group_sum_kernel", s);
