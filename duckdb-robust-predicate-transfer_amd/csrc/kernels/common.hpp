@@ -7,7 +7,8 @@
 // the A/B variants tools/build_variants.sh builds under other names (build/variants/). The product build
 // (Makefile: RPT_PRODUCT_BUILD, which HIPFLAGS cannot drop) refuses them.
 #if defined(RPT_PRODUCT_BUILD) && (defined(RPT_EXP_PART_STOP) || defined(RPT_EXP_SCATTER_SKIP) || \
-                                   defined(RPT_EXP_STORE_SKIP_ZERO) || defined(RPT_EXP_NO_PASS_WRITE))
+                                   defined(RPT_EXP_STORE_SKIP_ZERO) || defined(RPT_EXP_NO_PASS_WRITE) || \
+                                   defined(RPT_EXP_PROBE_NO_LDS) || defined(RPT_EXP_PROBE_NO_HASH))
 #error "RPT_EXP_* measurement macros are not allowed in the product build (use tools/build_variants.sh)"
 #endif
 
@@ -403,9 +404,33 @@ __device__ __forceinline__ void publish_minmax(int64_t mn, int64_t mx, int64_t* 
   }
 }
 constexpr int64_t kMinInit = INT64_MAX, kMaxInit = INT64_MIN;  // "no value yet"
+// RPT_PROBE_BUFSTORE = 1 (measured, off): a few lanes' stores (a segment's 8 result words from lanes 0-7, its count
+// from lane 0) as buffer stores through a descriptor covering only those bytes, so the other lanes' stores are
+// dropped by the descriptor's range check instead of being skipped by a branch. A store behind an exec-skip branch
+// leaves the compiler's count of outstanding memory operations unknown at the pipelined probe loop's head, where it
+// then waits for all of them (s_waitcnt vmcnt(0)). Removing that wait did not speed the probe (JOBDIM int64 probe
+// 1.567-1.570 vs 1.577-1.579 ms, int32 and the gather probe unchanged, profiles/r06/ab_pipeline.txt): its skeleton
+// is bound by the result words' HBM writes inside the key stream (tools/ubench/ubench_skeleton.hip). Global memory
+// only (not LDS).
+#ifndef RPT_PROBE_BUFSTORE
+#define RPT_PROBE_BUFSTORE 0
+#endif
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+constexpr int kRawBufferWord3 = 0x00020000;  // gfx9 raw buffer descriptor word 3: 32-bit data format, no swizzle
+__device__ __forceinline__ void store_lanes_b64(uint64_t* base, uint32_t valid_bytes, uint32_t lane, uint64_t v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(valid_bytes), kRawBufferWord3);
+  __builtin_amdgcn_raw_buffer_store_b64(u32x2{static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32)}, r,
+                                        static_cast<int>(lane * 8), 0, 0);
+}
+__device__ __forceinline__ void store_lanes_b32(uint32_t* base, uint32_t valid_bytes, uint32_t lane, uint32_t v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, static_cast<int>(valid_bytes), kRawBufferWord3);
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, static_cast<int>(lane * 4), 0, 0);
+}
+
 // The 8 pass flags a lane holds for a 512-row segment, in load_hashes<K, DENSE> order -> the segment's
-// row-ordered result words (8 x 64 bits, Arrow Find layout) and its survivor count.
-template <int K, bool DENSE>
+// row-ordered result words (8 x 64 bits, Arrow Find layout) and its survivor count. BUF: global outputs, written by
+// buffer stores (store_lanes_*); seg_counts may then be null (its store covers no bytes).
+template <int K, bool DENSE, bool BUF = false>
 __device__ __forceinline__ void store_segment_bits(const bool (&pass)[8], uint32_t lane, uint64_t seg,
                                                    uint64_t* __restrict__ out_bits, uint32_t* __restrict__ seg_counts) {
   uint64_t word[8];
@@ -430,8 +455,13 @@ __device__ __forceinline__ void store_segment_bits(const bool (&pass)[8], uint32
       if constexpr (V == 2) mine |= spread2(src >> (32 * q)) << e;
       else mine |= spread4(src >> (16 * q)) << e;
     }
-    if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
-    if (seg_counts != nullptr && lane == 0) seg_counts[seg] = cnt;
+    if constexpr (BUF) {
+      store_lanes_b64(out_bits + seg * kWordsPerSeg, kWordsPerSeg * 8, lane, mine);
+      store_lanes_b32(seg_counts + seg, seg_counts != nullptr ? 4u : 0u, lane, cnt);
+    } else {
+      if (lane < kWordsPerSeg) out_bits[seg * kWordsPerSeg + lane] = mine;
+      if (seg_counts != nullptr && lane == 0) seg_counts[seg] = cnt;
+    }
     return;
   } else if constexpr (DENSE) {
     constexpr int V = KeyTraits<K>::kVec;

@@ -22,6 +22,9 @@ namespace rpt {
 #ifndef RPT_LDS_I64_GROUP
 #define RPT_LDS_I64_GROUP 1  // segments per group in the int64 whole-filter LDS probe (r02: 2 and 3 were slower)
 #endif
+#ifndef RPT_PROBE_SCHED_BARRIER
+#define RPT_PROBE_SCHED_BARRIER 0  // 1: scheduling barrier after the prefetch loads (measured: no gain, see the loop)
+#endif
 #ifndef RPT_PROBE_RING
 #define RPT_PROBE_RING 2  // register buffers of prefetched groups: 2 = ping-pong (group g + 1 in flight while g is
                           // probed), 3 = groups g + 1 and g + 2 in flight
@@ -113,9 +116,21 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
           if (sg < n_full) {
             uint64_t h[8];
             bool pass[8];
+#if defined(RPT_EXP_PROBE_NO_HASH)  // measurement only: pass = a key bit (no hash, no filter lookups)
+#pragma unroll
+            for (int c = 0; c < RawSeg<K>::kLoads; c++)
+#pragma unroll
+              for (int e = 0; e < RawSeg<K>::V; e++) pass[c * RawSeg<K>::V + e] = (R[q].r[c][e] >> 7) & 1;
+            (void)h;
+#elif defined(RPT_EXP_PROBE_NO_LDS)  // measurement only: pass = a hash bit (hash kept, no filter lookups)
+            R[q].hashes(h);
+#pragma unroll
+            for (int j = 0; j < 8; j++) pass[j] = (h[j] >> 21) & 1;
+#else
             R[q].hashes(h);
             probe8<FILTER_IN_LDS>(words, s_filter, s_masks, block_mask, h, ok, pass);
-            store_segment_bits<K, DENSE>(pass, lane, sg, out_bits, seg_counts);
+#endif
+            store_segment_bits<K, DENSE, RPT_PROBE_BUFSTORE>(pass, lane, sg, out_bits, seg_counts);
           }
         }
       };
@@ -131,6 +146,12 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
           if (more) {
             load_group(R[(b + NB - 1) % NB], seg + (NB - 1) * step);
             asm volatile("" ::: "memory");  // issue the next group's loads before this one's work
+#if RPT_PROBE_SCHED_BARRIER
+            // ... and keep the scheduler from hoisting this group's hashing above them: it does in the second half of
+            // the unrolled int64 ping-pong, whose wait for its data then finds no loads in flight. Pinning the order
+            // measured no faster (profiles/r06/ab_pipeline.txt): 16 waves per CU hide that wait.
+            __builtin_amdgcn_sched_barrier(0);
+#endif
             probe_group(R[b], seg);
             seg += step;
             more = seg < n_full;
