@@ -217,7 +217,7 @@ __global__ __launch_bounds__(T) void skeleton_bufstore(const u64x2* __restrict__
 
 // the product's structure with the stores varied: MODE 1 = non-temporal stores, MODE 2 = plain stores into a 4 MiB
 // ring of result words (counts: 256 KiB) that stays in the caches -- does the cost come from writing to HBM?
-template <int T, int MODE>
+template <int T, int MODE, int RING_LOG = 16>
 __global__ __launch_bounds__(T) void skeleton_storemode(const u64x2* __restrict__ keys, uint64_t n_segs,
                                                         uint64_t* __restrict__ bits, uint32_t* __restrict__ counts,
                                                         uint64_t* __restrict__ sink) {
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(T) void skeleton_storemode(const u64x2* __restrict_
         uint64_t mine = 0;
 #pragma unroll
         for (int j = 0; j < 8; j++) mine = lane == static_cast<uint32_t>(j) ? word[j] : mine;
-        const uint64_t ws = MODE == 2 ? (seg & 65535) : seg;
+        const uint64_t ws = MODE == 2 ? (seg & ((1ULL << RING_LOG) - 1)) : seg;
         if (lane < 8) {
           if (MODE == 1) __builtin_nontemporal_store(mine, bits + ws * 8 + lane);
           else bits[ws * 8 + lane] = mine;
@@ -342,6 +342,11 @@ int main() {
   run("strided NB=2 plain stores (mode 0)", skeleton_storemode<1024, 0>, 1024, 1);
   run("strided NB=2 nt stores", skeleton_storemode<1024, 1>, 1024, 1);
   run("strided NB=2 stores into 4 MiB ring", skeleton_storemode<1024, 2>, 1024, 1);
+  // rings of 2^L segments' 64-B words: 16 / 32 / 64 / 128 MiB
+  run("stores into 16 MiB ring", skeleton_storemode<1024, 2, 18>, 1024, 1);
+  run("stores into 32 MiB ring", skeleton_storemode<1024, 2, 19>, 1024, 1);
+  run("stores into 64 MiB ring", skeleton_storemode<1024, 2, 20>, 1024, 1);
+  run("stores into 128 MiB ring", skeleton_storemode<1024, 2, 21>, 1024, 1);
   run("strided NB=2 nt stores", skeleton_storemode<256, 1>, 256, 8);
   run("strided NB=2 stores into 4 MiB ring", skeleton_storemode<256, 2>, 256, 8);
   run("strided NB=3 buffer stores", skeleton_bufstore<1024, 3>, 1024, 1);
