@@ -137,5 +137,14 @@ int main(int argc, char** argv) {
            mode ? "queued" : "synchronized", (unsigned long long)n, (unsigned long long)cnt, med(ev), med(d[0]));
     for (int p = 1; p < kPhases; p++) printf("  %-26s %.2f\n", names[p - 1], med(d[p]));
   }
+  // the product kernel on the same inputs, queued back to back (its duration: run under rocprofv3 --kernel-trace
+  // --stats and compare with phases_kernel's)
+  for (int it = 0; it < 2000; it++)
+    hipLaunchKernelGGL((rpt::probe_small_kernel<rpt::kKeyI64, true>), dim3(1), dim3(rpt::kSmallThreads), 0, 0, d_words,
+                       n_words - 1, a, n, static_cast<const uint32_t*>(nullptr), d_sel, d_count);
+  CHECK(hipDeviceSynchronize());
+  uint64_t cnt2 = 0;
+  CHECK(hipMemcpy(&cnt2, d_count, 8, hipMemcpyDeviceToHost));
+  printf("product probe_small_kernel: %llu pass\n", (unsigned long long)cnt2);
   return 0;
 }
