@@ -105,3 +105,11 @@ def test_c5_merge_flags(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--c5-merge", "--c5-rows-per-rank", "1e7", "--collective-timeout-ms", "5000"])
     a = bench.parse()
     assert a.c5_merge and a.c5_rows_per_rank == 1e7 and a.collective_timeout_ms == 5000
+
+
+def test_kernel_events_flag(monkeypatch):
+    # per-kernel timing events run in a second pass by default (they cost ~25 us per step inside the timed steps)
+    monkeypatch.setattr(sys, "argv", ["bench.py"])
+    assert not bench.parse().kernel_events_in_timed_region
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--kernel-events-in-timed-region"])
+    assert bench.parse().kernel_events_in_timed_region
