@@ -153,7 +153,9 @@ def test_chain_argument_errors(rpt):
         rpt.probe_chain([f, f], [p])  # one column per filter
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("RPT_FUZZ_SEEDS", "16"))))
+# RPT_FUZZ_SEEDS seeds from RPT_FUZZ_SEED_BASE (tools/gpu_soak.sh sweeps more of them)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("RPT_FUZZ_SEED_BASE", "0")),
+                                       int(os.environ.get("RPT_FUZZ_SEED_BASE", "0")) + int(os.environ.get("RPT_FUZZ_SEEDS", "16"))))
 def test_chain_random(rpt, seed):
     """Seeded sweep: 1..8 filters of random sizes (128 B..64 MiB), each over its own column with a random
     key type (int64 / int32 / precomputed hashes), NULL rate, dictionary; random row counts and row

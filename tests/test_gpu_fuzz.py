@@ -55,7 +55,9 @@ def case(seed):
                 use_dict=use_dict, use_rowsel=use_rowsel, rng=rng)
 
 
-@pytest.mark.parametrize("seed", range(int(os.environ.get("RPT_FUZZ_SEEDS", "24"))))
+# RPT_FUZZ_SEEDS seeds from RPT_FUZZ_SEED_BASE (tools/gpu_soak.sh sweeps more of them)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("RPT_FUZZ_SEED_BASE", "0")),
+                                       int(os.environ.get("RPT_FUZZ_SEED_BASE", "0")) + int(os.environ.get("RPT_FUZZ_SEEDS", "24"))))
 def test_random_configuration(rpt, seed):
     c = case(seed)
     lnb, rng = c["log_nb"], c["rng"]
