@@ -63,6 +63,8 @@ CONFIGS = {  # name -> (global build rows at N GPUs, filter sized for)
     # supplementary (not a BASELINE config): a JOB-sized dimension filter, 1e5 keys -> 128 KiB, the whole filter
     # in LDS
     "JOBDIM": (lambda n: 10**5, lambda n: 10**5),
+    # supplementary: a 2e5-key dimension filter (256 KiB: JOB's keyword / company_name tables), the hybrid LDS probe
+    "JOBDIM256": (lambda n: 2 * 10**5, lambda n: 2 * 10**5),
 }
 STREAM_CAL_BYTES = 8 << 30  # stream calibration buffer (>= 8 GB: well past the 256 MiB Infinity Cache)
 
@@ -859,9 +861,10 @@ def main():
                              f"per GPU against a blocked Bloom filter built from {n_build:.0e} keys (sized for "
                              f"{n_filter:.0e}: 2^{bf.log_num_blocks} blocks = {filter_bytes / 2**20:.0f} MiB), p={args.p}"),
                 "config": cfg,
-                "supplementary": (None if cfg != "JOBDIM" else
-                                  "not a BASELINE config: a JOB-sized dimension filter (1e5 keys, 128 KiB, whole "
-                                  "filter in LDS), where the 60 % whole-probe target is plausible"),
+                "supplementary": {"JOBDIM": "not a BASELINE config: a JOB-sized dimension filter (1e5 keys, 128 KiB, whole "
+                                            "filter in LDS), where the 60 % whole-probe target is plausible",
+                                  "JOBDIM256": "not a BASELINE config: a 2e5-key dimension filter (256 KiB), the first "
+                                               "128 KiB in LDS and the rest gathered from L2"}.get(cfg),
                 "probe_rows_per_gpu": n_probe,
                 "build_rows": n_build,
                 "filter_bytes": filter_bytes,

@@ -49,7 +49,10 @@ template <int K> struct RawSeg {
   }
 };
 
-template <bool FILTER_IN_LDS>
+// HYBRID (filters of 256 KiB .. 2^RPT_LDS_HYBRID_MAX_LOG blocks): the filter's first kHybridWords words are staged in
+// LDS, the rest gathered from L2.
+constexpr uint64_t kHybridWords = 1ULL << kLdsDirectMaxLog;
+template <bool FILTER_IN_LDS, bool HYBRID = false>
 __device__ __forceinline__ void probe8(const uint64_t* __restrict__ words, const uint64_t* s_filter,
                                        const uint64_t* s_masks, uint64_t block_mask, const uint64_t (&h)[8],
                                        const bool (&ok)[8], bool (&pass)[8]) {
@@ -57,7 +60,10 @@ __device__ __forceinline__ void probe8(const uint64_t* __restrict__ words, const
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     m[j] = mask_of(s_masks, h[j]);
-    if constexpr (FILTER_IN_LDS) {
+    if constexpr (FILTER_IN_LDS && HYBRID) {
+      const uint64_t blk = block_of(h[j], block_mask);
+      w[j] = blk < kHybridWords ? s_filter[blk] : (ok[j] ? words[blk] : 0ULL);
+    } else if constexpr (FILTER_IN_LDS) {
       w[j] = s_filter[block_of(h[j], block_mask)];
     } else {
       w[j] = ok[j] ? words[block_of(h[j], block_mask)] : 0ULL;
@@ -69,18 +75,20 @@ __device__ __forceinline__ void probe8(const uint64_t* __restrict__ words, const
 
 // zero[0 .. n_zero): words the selection-vector tail's look-back needs cleared (compact_lookback_kernel's group
 // states and ticket), cleared here so the tail needs no launch of its own; nullptr when there is no such tail.
-template <int K, bool DENSE, bool FILTER_IN_LDS, int THREADS = kBlockThreads>
-__global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __restrict__ words,
-                                                                  uint64_t block_mask, KeyArgs a, uint64_t n,
-                                                                  uint64_t n_segs, uint64_t* __restrict__ out_bits,
-                                                                  uint32_t* __restrict__ seg_counts,
-                                                                  uint64_t* __restrict__ zero, uint32_t n_zero) {
+// The body of probe_bits_kernel (HYBRID = false) and probe_bits_hybrid_kernel (HYBRID = true: filters of 256 KiB,
+// the first 128 KiB staged in LDS, the rest gathered from L2).
+template <int K, bool DENSE, bool FILTER_IN_LDS, int THREADS, bool HYBRID>
+__device__ __forceinline__ void probe_bits_body(const uint64_t* __restrict__ words, uint64_t block_mask, KeyArgs a,
+                                                uint64_t n, uint64_t n_segs, uint64_t* __restrict__ out_bits,
+                                                uint32_t* __restrict__ seg_counts, uint64_t* __restrict__ zero,
+                                                uint32_t n_zero) {
   __shared__ uint64_t s_masks[kNumMasks];
   extern __shared__ uint64_t s_filter[];
   for (uint32_t i = blockIdx.x * THREADS + threadIdx.x; i < n_zero; i += gridDim.x * THREADS) zero[i] = 0;
   fill_mask_table(s_masks);
   if constexpr (FILTER_IN_LDS) {
-    for (uint64_t i = threadIdx.x; i <= block_mask; i += blockDim.x) s_filter[i] = words[i];
+    const uint64_t staged = HYBRID ? kHybridWords - 1 : block_mask;
+    for (uint64_t i = threadIdx.x; i <= staged; i += blockDim.x) s_filter[i] = words[i];
   }
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
@@ -128,7 +136,7 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
             for (int j = 0; j < 8; j++) pass[j] = (h[j] >> 21) & 1;
 #else
             R[q].hashes(h);
-            probe8<FILTER_IN_LDS>(words, s_filter, s_masks, block_mask, h, ok, pass);
+            probe8<FILTER_IN_LDS, HYBRID>(words, s_filter, s_masks, block_mask, h, ok, pass);
 #endif
             store_segment_bits<K, DENSE, RPT_PROBE_BUFSTORE>(pass, lane, sg, out_bits, seg_counts);
           }
@@ -167,9 +175,28 @@ __global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __r
     uint64_t h[8];
     bool ok[8], pass[8];
     load_hashes<K, DENSE>(a, seg * kSegRows, n, lane, h, ok);
-    probe8<FILTER_IN_LDS>(words, s_filter, s_masks, block_mask, h, ok, pass);
+    probe8<FILTER_IN_LDS, HYBRID>(words, s_filter, s_masks, block_mask, h, ok, pass);
     store_segment_bits<K, DENSE>(pass, lane, seg, out_bits, seg_counts);
   }
+}
+
+template <int K, bool DENSE, bool FILTER_IN_LDS, int THREADS = kBlockThreads>
+__global__ __launch_bounds__(THREADS) void probe_bits_kernel(const uint64_t* __restrict__ words,
+                                                                  uint64_t block_mask, KeyArgs a, uint64_t n,
+                                                                  uint64_t n_segs, uint64_t* __restrict__ out_bits,
+                                                                  uint32_t* __restrict__ seg_counts,
+                                                                  uint64_t* __restrict__ zero, uint32_t n_zero) {
+  probe_bits_body<K, DENSE, FILTER_IN_LDS, THREADS, false>(words, block_mask, a, n, n_segs, out_bits, seg_counts, zero,
+                                                           n_zero);
+}
+template <int K, bool DENSE>
+__global__ __launch_bounds__(kLdsProbeThreads) void probe_bits_hybrid_kernel(const uint64_t* __restrict__ words,
+                                                                             uint64_t block_mask, KeyArgs a, uint64_t n,
+                                                                             uint64_t n_segs, uint64_t* __restrict__ out_bits,
+                                                                             uint32_t* __restrict__ seg_counts,
+                                                                             uint64_t* __restrict__ zero, uint32_t n_zero) {
+  probe_bits_body<K, DENSE, true, kLdsProbeThreads, true>(words, block_mask, a, n, n_segs, out_bits, seg_counts, zero,
+                                                          n_zero);
 }
 
 // ---- small batches: probe + compaction in ONE workgroup ----------------------------------------

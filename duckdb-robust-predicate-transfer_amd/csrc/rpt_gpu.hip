@@ -61,6 +61,12 @@
 #ifndef RPT_LOOKBACK_TAIL
 #define RPT_LOOKBACK_TAIL 0  // 1: the direct strategies' sel tail in one look-back launch (measured slower, DESIGN §5 rejected list)
 #endif
+#ifndef RPT_LDS_HYBRID_MAX_LOG
+#define RPT_LDS_HYBRID_MAX_LOG 15  // the LDS strategy up to 2^this blocks; above 2^14 the first 128 KiB in LDS, the rest
+                                   // gathered from L2 (probe_direct.hpp). 256 KiB filters, ms per 1e9 keys against AUTO's
+                                   // previous pick (partitioned): int64 3.08 vs 3.80, int32 2.30 vs 3.38; 512 KiB: int64
+                                   // 4.01 vs 3.82, int32 3.24 vs 3.43; 1 MiB slower (profiles/r06/ab_hybrid.txt)
+#endif
 #ifndef RPT_SUMSCAN_TAIL
 #define RPT_SUMSCAN_TAIL 0  // 1: the direct strategies' group sums and their scan in one launch (measured: no gain)
 #endif
@@ -74,7 +80,7 @@ static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG 
                   RPT_PARTITION_MIN_WAVES == 8 && RPT_PROBE_PREFETCH == 2 && RPT_SEL_BALLOT_MIN == 192 &&
                   RPT_COMPACT_BALLOT_MIN == 384 && RPT_COMPACT_STAGE == 3072 && RPT_LDS_I64_GROUP == 1 &&
                   RPT_PROBE_RING == 2 && RPT_LOOKBACK_TAIL == 0 && RPT_COMPACT_V16 == 0 && RPT_SUMSCAN_TAIL == 0 &&
-                  RPT_PROBE_BUFSTORE == 0 && RPT_PROBE_SCHED_BARRIER == 0,
+                  RPT_PROBE_BUFSTORE == 0 && RPT_PROBE_SCHED_BARRIER == 0 && RPT_LDS_HYBRID_MAX_LOG == 15,
               "product build: tuning macros must keep their tested defaults (use tools/build_variants.sh)");
 static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
                   RPT_NT_REC_LOADS == 0 && RPT_NT_SLICE_LOADS == 1 && RPT_PARK_LANE_MAJOR == 1 && RPT_SLICE_XCD_MAP == 1 &&
@@ -454,7 +460,7 @@ int strategy_supported(int strategy, int log_num_blocks) {
   constexpr int kBucketLog = rpt::kSliceLog + rpt::kBucketSliceLog;  // log2 blocks per bucket (22)
   switch (strategy) {
     case RPT_PROBE_GATHER: return 1;
-    case RPT_PROBE_LDS: return log_num_blocks <= rpt::kLdsDirectMaxLog;
+    case RPT_PROBE_LDS: return log_num_blocks <= std::max(rpt::kLdsDirectMaxLog, RPT_LDS_HYBRID_MAX_LOG);
     case RPT_PROBE_PARTITIONED:
       return log_num_blocks >= rpt::kSliceLog && slice_count(log_num_blocks) <= static_cast<uint32_t>(rpt::kMaxSliceCount);
     case RPT_PROBE_BUCKETED:  // 1..512 buckets of 32 MiB (filters of 32 MiB..16 GiB)
@@ -465,8 +471,9 @@ int strategy_supported(int strategy, int log_num_blocks) {
 }
 
 // AUTO, from measured crossovers (tools/strategy_crossover.py, profiles/r01/strategy_crossover.jsonl):
-//   <= 64 KiB   LDS: the whole filter in each workgroup's LDS;
-//   <= 256 KiB  GATHER: the filter stays resident in every XCD's L2 (~5 ps/key at any batch size);
+//   <= 128 KiB  LDS: the whole filter in each workgroup's LDS;
+//   256 KiB     LDS, hybrid (r06): the first 128 KiB in LDS, the other half gathered from L2 -- faster than the
+//               gather and than the partitioned probe (tools/ab_hybrid.sh, profiles/r06/ab_hybrid.txt);
 //   <= 128 MiB  PARTITIONED for batches of >= 4 Mi rows (>= 32 Mi below 8 MiB filters, where the L2
 //               still serves the gather well), else GATHER: routing has ~50 us of fixed cost;
 //   <= 16 GiB   BUCKETED for batches of >= max(blocks/8, 32 Mi) rows (it stages the whole filter in
@@ -475,7 +482,7 @@ int strategy_supported(int strategy, int log_num_blocks) {
 int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_PROBE_AUTO) return requested;
   const int L = log_num_blocks;
-  if (L <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
+  if (L <= std::max(rpt::kLdsDirectMaxLog, RPT_LDS_HYBRID_MAX_LOG)) return RPT_PROBE_LDS;
   // measured crossovers (tools/strategy_crossover.py --mid, profiles/r01/strategy_crossover_mid.jsonl):
   // the partitioned probe overtakes the (partly L2-resident) gather from 2^25 rows for 256 KiB..2 MiB
   // filters and from 2^22 rows above
@@ -749,6 +756,19 @@ void allow_dynamic_lds(const void* fn);
 template <int K, bool D>
 void launch_probe_bits_lds_t(unsigned grid, hipStream_t s, const rpt_bf* bf, const rpt::KeyArgs& a, uint64_t n,
                              uint64_t n_segs, uint64_t* bits, uint32_t* counts, uint64_t* zero, uint32_t n_zero) {
+  if (bf->log_num_blocks > rpt::kLdsDirectMaxLog) {  // hybrid: the first 128 KiB in LDS, the rest from L2
+    const size_t lds = 8ULL << rpt::kLdsDirectMaxLog;
+    static std::once_flag once_h;
+    std::call_once(once_h, [] {
+      allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::probe_bits_hybrid_kernel<K, D>));
+    });
+    ProfScope prof(inst_name<K, D>("probe_bits_hybrid_kernel"), s);
+    hipLaunchKernelGGL((rpt::probe_bits_hybrid_kernel<K, D>), dim3(grid),
+                       dim3(rpt::kLdsProbeThreads), lds, s, bf->words, (1ULL << bf->log_num_blocks) - 1, a, n, n_segs,
+                       bits, counts, zero, n_zero);
+    prof.end();
+    return;
+  }
   const size_t lds = 8ULL << bf->log_num_blocks;
   static std::once_flag once;  // > 64 KiB of dynamic LDS must be opted into
   std::call_once(once, [] { allow_dynamic_lds(reinterpret_cast<const void*>(&rpt::probe_bits_kernel<K, D, true, rpt::kLdsProbeThreads>)); });
@@ -1430,7 +1450,7 @@ static int probe_phase1_impl(const rpt_bf* bf, const rpt_key_column* col, const 
                     ws.lb_state, lb_words);
     RPT_LAUNCHED("probe_bits_kernel");
   } else if (strategy == RPT_PROBE_LDS) {
-    const uint64_t lds = (8ULL << L) + 8ULL * rpt::kNumMasks;
+    const uint64_t lds = (8ULL << std::min(L, rpt::kLdsDirectMaxLog)) + 8ULL * rpt::kNumMasks;
     const uint64_t per_cu = std::max<uint64_t>(1, std::min<uint64_t>(rpt::kBlocksPerCU, (160ULL << 10) / lds));
     const uint64_t waves = rpt::kLdsProbeThreads / 64;  // launch_probe_bits_lds_t
     const unsigned grid = static_cast<unsigned>(
