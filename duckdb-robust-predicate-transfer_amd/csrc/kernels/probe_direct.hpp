@@ -25,6 +25,10 @@ namespace rpt {
 #ifndef RPT_PROBE_SCHED_BARRIER
 #define RPT_PROBE_SCHED_BARRIER 0  // 1: scheduling barrier after the prefetch loads (measured: no gain, see the loop)
 #endif
+#ifndef RPT_HYBRID_I64_GROUP
+#define RPT_HYBRID_I64_GROUP 2  // segments per group in the int64 hybrid LDS/L2 probe (1 / 2 / 3: 2.82 / 2.59 / 2.87 ms
+                                // per 1e9 keys, profiles/r06/ab_hybrid_group.txt; int32 takes RPT_PROBE_PREFETCH = 2)
+#endif
 #ifndef RPT_PROBE_RING
 #define RPT_PROBE_RING 2  // register buffers of prefetched groups: 2 = ping-pong (group g + 1 in flight while g is
                           // probed), 3 = groups g + 1 and g + 2 in flight
@@ -105,7 +109,8 @@ __device__ __forceinline__ void probe_bits_body(const uint64_t* __restrict__ wor
       // group is probed. Addresses past the last full segment are clamped and their rows discarded.
       // measured (ms per 1e9 keys, S = 1 / 2 / 3): 128 KiB LDS int64 1.68 / 1.79 / 1.77, int32 1.09 /
       // 1.05 / 1.06; 256 KiB gather 4.48 / 4.33 / 4.30
-      constexpr int S = (FILTER_IN_LDS && KeyTraits<K>::kVec == 2) ? RPT_LDS_I64_GROUP : RPT_PROBE_PREFETCH;
+      constexpr int S = (FILTER_IN_LDS && KeyTraits<K>::kVec == 2) ? (HYBRID ? RPT_HYBRID_I64_GROUP : RPT_LDS_I64_GROUP)
+                                                                   : RPT_PROBE_PREFETCH;
       constexpr int NB = RPT_PROBE_RING;
       const bool ok[8] = {true, true, true, true, true, true, true, true};
       const uint64_t first = seg;

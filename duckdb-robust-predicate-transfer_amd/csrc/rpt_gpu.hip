@@ -80,7 +80,8 @@ static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG 
                   RPT_PARTITION_MIN_WAVES == 8 && RPT_PROBE_PREFETCH == 2 && RPT_SEL_BALLOT_MIN == 192 &&
                   RPT_COMPACT_BALLOT_MIN == 384 && RPT_COMPACT_STAGE == 3072 && RPT_LDS_I64_GROUP == 1 &&
                   RPT_PROBE_RING == 2 && RPT_LOOKBACK_TAIL == 0 && RPT_COMPACT_V16 == 0 && RPT_SUMSCAN_TAIL == 0 &&
-                  RPT_PROBE_BUFSTORE == 0 && RPT_PROBE_SCHED_BARRIER == 0 && RPT_LDS_HYBRID_MAX_LOG == 15,
+                  RPT_PROBE_BUFSTORE == 0 && RPT_PROBE_SCHED_BARRIER == 0 && RPT_LDS_HYBRID_MAX_LOG == 15 &&
+                  RPT_HYBRID_I64_GROUP == 2,
               "product build: tuning macros must keep their tested defaults (use tools/build_variants.sh)");
 static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
                   RPT_NT_REC_LOADS == 0 && RPT_NT_SLICE_LOADS == 1 && RPT_PARK_LANE_MAJOR == 1 && RPT_SLICE_XCD_MAP == 1 &&
