@@ -65,6 +65,7 @@ CONFIGS = {  # name -> (global build rows at N GPUs, filter sized for)
     "JOBDIM": (lambda n: 10**5, lambda n: 10**5),
     # supplementary: a 2e5-key dimension filter (256 KiB: JOB's keyword / company_name tables), the hybrid LDS probe
     "JOBDIM256": (lambda n: 2 * 10**5, lambda n: 2 * 10**5),
+    "JOBDIM512": (lambda n: 4 * 10**5, lambda n: 4 * 10**5),  # 512 KiB, the hybrid probe's upper size
 }
 STREAM_CAL_BYTES = 8 << 30  # stream calibration buffer (>= 8 GB: well past the 256 MiB Infinity Cache)
 
@@ -864,6 +865,8 @@ def main():
                 "supplementary": {"JOBDIM": "not a BASELINE config: a JOB-sized dimension filter (1e5 keys, 128 KiB, whole "
                                             "filter in LDS), where the 60 % whole-probe target is plausible",
                                   "JOBDIM256": "not a BASELINE config: a 2e5-key dimension filter (256 KiB), the first "
+                                               "128 KiB in LDS and the rest gathered from L2",
+                                  "JOBDIM512": "not a BASELINE config: a 4e5-key dimension filter (512 KiB), the first "
                                                "128 KiB in LDS and the rest gathered from L2"}.get(cfg),
                 "probe_rows_per_gpu": n_probe,
                 "build_rows": n_build,

@@ -62,10 +62,11 @@
 #define RPT_LOOKBACK_TAIL 0  // 1: the direct strategies' sel tail in one look-back launch (measured slower, DESIGN §5 rejected list)
 #endif
 #ifndef RPT_LDS_HYBRID_MAX_LOG
-#define RPT_LDS_HYBRID_MAX_LOG 15  // the LDS strategy up to 2^this blocks; above 2^14 the first 128 KiB in LDS, the rest
-                                   // gathered from L2 (probe_direct.hpp). 256 KiB filters, ms per 1e9 keys against AUTO's
-                                   // previous pick (partitioned): int64 3.08 vs 3.80, int32 2.30 vs 3.38; 512 KiB: int64
-                                   // 4.01 vs 3.82, int32 3.24 vs 3.43; 1 MiB slower (profiles/r06/ab_hybrid.txt)
+#define RPT_LDS_HYBRID_MAX_LOG 16  // the LDS strategy up to 2^this blocks; above 2^14 the first 128 KiB in LDS, the rest
+                                   // gathered from L2 (probe_direct.hpp). ms per 1e9 keys against AUTO's previous pick
+                                   // (partitioned) with 2-segment int64 groups: 256 KiB int64 2.77 vs 3.81, int32 2.27 vs
+                                   // 3.43; 512 KiB int64 3.64 vs 3.81, int32 3.23 vs 3.43 (gather: 4.66 / 4.27); 1 MiB
+                                   // slower than partitioned (profiles/r06/ab_hybrid2.txt, first pass ab_hybrid.txt)
 #endif
 #ifndef RPT_SUMSCAN_TAIL
 #define RPT_SUMSCAN_TAIL 0  // 1: the direct strategies' group sums and their scan in one launch (measured: no gain)
@@ -80,7 +81,7 @@ static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG 
                   RPT_PARTITION_MIN_WAVES == 8 && RPT_PROBE_PREFETCH == 2 && RPT_SEL_BALLOT_MIN == 192 &&
                   RPT_COMPACT_BALLOT_MIN == 384 && RPT_COMPACT_STAGE == 3072 && RPT_LDS_I64_GROUP == 1 &&
                   RPT_PROBE_RING == 2 && RPT_LOOKBACK_TAIL == 0 && RPT_COMPACT_V16 == 0 && RPT_SUMSCAN_TAIL == 0 &&
-                  RPT_PROBE_BUFSTORE == 0 && RPT_PROBE_SCHED_BARRIER == 0 && RPT_LDS_HYBRID_MAX_LOG == 15 &&
+                  RPT_PROBE_BUFSTORE == 0 && RPT_PROBE_SCHED_BARRIER == 0 && RPT_LDS_HYBRID_MAX_LOG == 16 &&
                   RPT_HYBRID_I64_GROUP == 2,
               "product build: tuning macros must keep their tested defaults (use tools/build_variants.sh)");
 static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
@@ -473,8 +474,8 @@ int strategy_supported(int strategy, int log_num_blocks) {
 
 // AUTO, from measured crossovers (tools/strategy_crossover.py, profiles/r01/strategy_crossover.jsonl):
 //   <= 128 KiB  LDS: the whole filter in each workgroup's LDS;
-//   256 KiB     LDS, hybrid (r06): the first 128 KiB in LDS, the other half gathered from L2 -- faster than the
-//               gather and than the partitioned probe (tools/ab_hybrid.sh, profiles/r06/ab_hybrid.txt);
+//   256-512 KiB LDS, hybrid (r06): the first 128 KiB in LDS, the rest gathered from L2 -- faster than the
+//               gather and than the partitioned probe (tools/ab_hybrid.sh, profiles/r06/ab_hybrid2.txt);
 //   <= 128 MiB  PARTITIONED for batches of >= 4 Mi rows (>= 32 Mi below 8 MiB filters, where the L2
 //               still serves the gather well), else GATHER: routing has ~50 us of fixed cost;
 //   <= 16 GiB   BUCKETED for batches of >= max(blocks/8, 32 Mi) rows (it stages the whole filter in

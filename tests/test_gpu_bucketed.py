@@ -113,11 +113,11 @@ def test_auto_routes_large_filters(rpt):
     assert bf.probe_strategy_for(1 << 25) == BUCKETED and bf.probe_strategy_for(10**7) == GATHER
     tiny = rpt.BloomFilter(log_num_blocks=14)  # 128 KiB: the whole filter in each CU's LDS
     assert tiny.probe_strategy_for(1 << 28) == 2 and tiny.probe_strategy_for(1 << 16) == 2
-    small = rpt.BloomFilter(log_num_blocks=15)  # 256 KiB: the hybrid LDS probe (first 128 KiB in LDS) at any size
+    small = rpt.BloomFilter(log_num_blocks=15)  # 256 KiB (512 KiB too): the hybrid LDS probe at any size
     assert small.probe_strategy_for(1 << 24) == 2 and small.probe_strategy_for(1 << 28) == 2
-    small16 = rpt.BloomFilter(log_num_blocks=16)  # 512 KiB: L2 gathers below 32 Mi rows, routed above
-    assert small16.probe_strategy_for(1 << 24) == GATHER and small16.probe_strategy_for(1 << 28) == PARTITIONED
-    small16.close()
+    small17 = rpt.BloomFilter(log_num_blocks=17)  # 1 MiB: L2 gathers below 32 Mi rows, routed above
+    assert small17.probe_strategy_for(1 << 24) == GATHER and small17.probe_strategy_for(1 << 28) == PARTITIONED
+    small17.close()
     mid19 = rpt.BloomFilter(log_num_blocks=19)  # 4 MiB: routed from 4 Mi rows
     assert mid19.probe_strategy_for(1 << 22) == PARTITIONED and mid19.probe_strategy_for(1 << 21) == GATHER
     mid = rpt.BloomFilter(log_num_blocks=21)  # 16 MiB (C2): routed from 4 Mi rows

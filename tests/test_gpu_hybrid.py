@@ -1,7 +1,7 @@
-"""The hybrid LDS/L2 direct probe (`probe_bits_hybrid_kernel`: 256 KiB filters, 2^15 blocks, the first 2^14 words
-staged in each workgroup's LDS and the rest gathered from L2) against the oracle, bit-exact: dense int64 / int32
-columns with ragged tails (the pipelined loop and the general loop), NULLs, and a dictionary vector through a row
-selection; and AUTO's choice of it for 256 KiB filters only."""
+"""The hybrid LDS/L2 direct probe (`probe_bits_hybrid_kernel`: 256 / 512 KiB filters, 2^15 / 2^16 blocks, the first
+2^14 words staged in each workgroup's LDS and the rest gathered from L2) against the oracle, bit-exact: dense int64 /
+int32 columns with ragged tails (the pipelined loop and the general loop), NULLs, and a dictionary vector through a
+row selection; and AUTO's choice of it for those two sizes only."""
 import numpy as np
 import pytest
 import torch
@@ -12,7 +12,7 @@ import rpt_oracle as orc
 pytestmark = pytest.mark.gpu
 
 GATHER, LDS, PARTITIONED = 1, 2, 3
-LOG_NB = 15  # 256 KiB
+LOG_NBS = [15, 16]  # 256 KiB, 512 KiB
 
 
 @pytest.fixture(scope="module")
@@ -32,7 +32,7 @@ def dev(a: np.ndarray) -> torch.Tensor:
     return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
 
 
-def built(rpt, dtype, n_build, seed):
+def built(rpt, dtype, n_build, seed, LOG_NB):
     info = np.iinfo(dtype)
     rng = np.random.default_rng(seed)
     build = rng.integers(info.min, info.max, size=n_build, dtype=dtype, endpoint=True)
@@ -46,18 +46,19 @@ def built(rpt, dtype, n_build, seed):
     return bf, build, w, rng
 
 
-def test_auto_picks_hybrid_for_256k_only(rpt):
-    for log_nb, expect in ((14, LDS), (15, LDS), (16, GATHER)):
+def test_auto_picks_hybrid_for_256k_and_512k_only(rpt):
+    for log_nb, expect in ((14, LDS), (15, LDS), (16, LDS), (17, GATHER)):
         bf = rpt.BloomFilter(log_num_blocks=log_nb)
         assert bf.probe_strategy_for(1 << 24) == expect, log_nb
         bf.close()
-    assert rpt.BloomFilter(log_num_blocks=16).probe_strategy_for(1 << 28) == PARTITIONED
+    assert rpt.BloomFilter(log_num_blocks=17).probe_strategy_for(1 << 28) == PARTITIONED
 
 
+@pytest.mark.parametrize("LOG_NB", LOG_NBS)
 @pytest.mark.parametrize("dtype", [np.int64, np.int32])
 @pytest.mark.parametrize("n", [16385, 100_003, 1 << 20, 3_000_001])
-def test_hybrid_dense_vs_oracle(rpt, dtype, n):
-    bf, build, w, rng = built(rpt, dtype, 150_000, n)
+def test_hybrid_dense_vs_oracle(rpt, dtype, n, LOG_NB):
+    bf, build, w, rng = built(rpt, dtype, 150_000 << (LOG_NB - 15), n, LOG_NB)
     info = np.iinfo(dtype)
     probe = np.where(rng.random(n) < 0.3, build[rng.integers(0, build.size, n)],
                      rng.integers(info.min, info.max, size=n, dtype=dtype, endpoint=True)).astype(dtype)
@@ -67,10 +68,11 @@ def test_hybrid_dense_vs_oracle(rpt, dtype, n):
     bf.close()
 
 
+@pytest.mark.parametrize("LOG_NB", LOG_NBS)
 @pytest.mark.parametrize("dtype", [np.int64, np.int32])
-def test_hybrid_nulls_vs_oracle(rpt, dtype):
+def test_hybrid_nulls_vs_oracle(rpt, dtype, LOG_NB):
     n = 200_001
-    bf, build, w, rng = built(rpt, dtype, 150_000, 77)
+    bf, build, w, rng = built(rpt, dtype, 150_000 << (LOG_NB - 15), 77, LOG_NB)
     probe = build[rng.integers(0, build.size, n)]
     valid = rng.random(n) > 0.1
     vw = gu.validity_words(valid)
@@ -80,7 +82,8 @@ def test_hybrid_nulls_vs_oracle(rpt, dtype):
     bf.close()
 
 
-def test_hybrid_dictionary_rowsel_vs_oracle(rpt):
+@pytest.mark.parametrize("LOG_NB", LOG_NBS)
+def test_hybrid_dictionary_rowsel_vs_oracle(rpt, LOG_NB):
     rng = np.random.default_rng(15)
     dict_vals = rng.integers(-10**12, 10**12, size=60_000, dtype=np.int64)
     n = 90_000
