@@ -474,17 +474,21 @@ int strategy_supported(int strategy, int log_num_blocks) {
 
 // AUTO, from measured crossovers (tools/strategy_crossover.py, profiles/r01/strategy_crossover.jsonl):
 //   <= 128 KiB  LDS: the whole filter in each workgroup's LDS;
-//   256-512 KiB LDS, hybrid (r06): the first 128 KiB in LDS, the rest gathered from L2 -- faster than the
-//               gather and than the partitioned probe (tools/ab_hybrid.sh, profiles/r06/ab_hybrid2.txt);
+//   256-512 KiB LDS, hybrid (r06), for batches of >= 4 Mi rows: the first 128 KiB in LDS, the rest gathered from
+//               L2 -- faster than the gather and than the partitioned probe (tools/ab_hybrid.sh,
+//               profiles/r06/ab_hybrid2.txt). Below 4 Mi rows its 128 KiB staging per workgroup costs more than it
+//               saves: GATHER (1 Mi rows: 37.5 vs 35.7 us, 4 Mi: 43.8 vs 51.6 us, profiles/r06/ab_hybrid_small.txt);
 //   <= 128 MiB  PARTITIONED for batches of >= 4 Mi rows (>= 32 Mi below 8 MiB filters, where the L2
 //               still serves the gather well), else GATHER: routing has ~50 us of fixed cost;
 //   <= 16 GiB   BUCKETED for batches of >= max(blocks/8, 32 Mi) rows (it stages the whole filter in
 //               LDS once), else GATHER.
 // n = ~0 is "a batch of unknown, large size" (rpt_bf_probe_strategy).
+constexpr uint64_t kHybridMinRows = 1ULL << 22;
 int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_PROBE_AUTO) return requested;
   const int L = log_num_blocks;
-  if (L <= std::max(rpt::kLdsDirectMaxLog, RPT_LDS_HYBRID_MAX_LOG)) return RPT_PROBE_LDS;
+  if (L <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
+  if (L <= RPT_LDS_HYBRID_MAX_LOG) return n >= kHybridMinRows ? RPT_PROBE_LDS : RPT_PROBE_GATHER;
   // measured crossovers (tools/strategy_crossover.py --mid, profiles/r01/strategy_crossover_mid.jsonl):
   // the partitioned probe overtakes the (partly L2-resident) gather from 2^25 rows for 256 KiB..2 MiB
   // filters and from 2^22 rows above

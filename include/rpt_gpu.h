@@ -53,7 +53,8 @@ typedef enum rpt_key_type {
 
 /* How a probe reaches the filter blocks (rpt_bf_set_probe_strategy). All give identical results. */
 typedef enum rpt_probe_strategy {
-  RPT_PROBE_AUTO = 0,        /* by filter and batch size (measured crossovers): LDS (<= 512 KiB);
+  RPT_PROBE_AUTO = 0,        /* by filter and batch size (measured crossovers): LDS (<= 128 KiB, and
+                                256 / 512 KiB for n >= 4 Mi);
                                 PARTITIONED (<= 128 MiB) for n >= 32 Mi (256 KiB..2 MiB) or n >= 4 Mi
                                 (4 MiB and up); BUCKETED (<= 16 GiB, n >= max(blocks/8, 32 Mi));
                                 otherwise GATHER */

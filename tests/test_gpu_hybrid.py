@@ -47,22 +47,25 @@ def built(rpt, dtype, n_build, seed, LOG_NB):
 
 
 def test_auto_picks_hybrid_for_256k_and_512k_only(rpt):
+    # from 4 Mi rows (below, its LDS staging costs more than it saves: the gather)
     for log_nb, expect in ((14, LDS), (15, LDS), (16, LDS), (17, GATHER)):
         bf = rpt.BloomFilter(log_num_blocks=log_nb)
         assert bf.probe_strategy_for(1 << 24) == expect, log_nb
+        assert bf.probe_strategy_for(1 << 22) == expect, log_nb
+        assert bf.probe_strategy_for((1 << 22) - 1) == (LDS if log_nb == 14 else GATHER), log_nb
         bf.close()
     assert rpt.BloomFilter(log_num_blocks=17).probe_strategy_for(1 << 28) == PARTITIONED
 
 
 @pytest.mark.parametrize("LOG_NB", LOG_NBS)
 @pytest.mark.parametrize("dtype", [np.int64, np.int32])
-@pytest.mark.parametrize("n", [16385, 100_003, 1 << 20, 3_000_001])
+@pytest.mark.parametrize("n", [16385, 100_003, 1 << 20, 3_000_001, (1 << 22) + 77])
 def test_hybrid_dense_vs_oracle(rpt, dtype, n, LOG_NB):
     bf, build, w, rng = built(rpt, dtype, 150_000 << (LOG_NB - 15), n, LOG_NB)
     info = np.iinfo(dtype)
     probe = np.where(rng.random(n) < 0.3, build[rng.integers(0, build.size, n)],
                      rng.integers(info.min, info.max, size=n, dtype=dtype, endpoint=True)).astype(dtype)
-    assert bf.probe_strategy_for(n) == LDS
+    bf.probe_strategy = LDS  # AUTO takes it from 4 Mi rows; smaller batches exercise the same kernel here
     sel = bf.lookup_sel(dev(probe)).cpu().numpy().view(np.uint32)
     assert np.array_equal(sel, orc.probe_keys(w, LOG_NB, probe))
     bf.close()
