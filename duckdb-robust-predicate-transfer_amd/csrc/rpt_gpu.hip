@@ -62,11 +62,13 @@
 #define RPT_LOOKBACK_TAIL 0  // 1: the direct strategies' sel tail in one look-back launch (measured slower, DESIGN §5 rejected list)
 #endif
 #ifndef RPT_LDS_HYBRID_MAX_LOG
-#define RPT_LDS_HYBRID_MAX_LOG 16  // the LDS strategy up to 2^this blocks; above 2^14 the first 128 KiB in LDS, the rest
+#define RPT_LDS_HYBRID_MAX_LOG 17  // the LDS strategy up to 2^this blocks; above 2^14 the first 128 KiB in LDS, the rest
                                    // gathered from L2 (probe_direct.hpp). ms per 1e9 keys against AUTO's previous pick
                                    // (partitioned) with 2-segment int64 groups: 256 KiB int64 2.77 vs 3.81, int32 2.27 vs
                                    // 3.43; 512 KiB int64 3.64 vs 3.81, int32 3.23 vs 3.43 (gather: 4.66 / 4.27); 1 MiB
-                                   // slower than partitioned (profiles/r06/ab_hybrid2.txt, first pass ab_hybrid.txt)
+                                   // slower than partitioned but faster than the gather from 4 Mi rows (1 MiB,
+                                   // 16 Mi rows: 107 vs 112 us int64, 99 vs 106 us int32; profiles/r06/ab_hybrid2.txt,
+                                   // ab_hybrid_1m.txt, first pass ab_hybrid.txt)
 #endif
 #ifndef RPT_SUMSCAN_TAIL
 #define RPT_SUMSCAN_TAIL 0  // 1: the direct strategies' group sums and their scan in one launch (measured: no gain)
@@ -81,7 +83,7 @@ static_assert(RPT_SLICE_LOG == 14 && RPT_RUN_ALIGN == 8 && RPT_BUCKET_SLICE_LOG 
                   RPT_PARTITION_MIN_WAVES == 8 && RPT_PROBE_PREFETCH == 2 && RPT_SEL_BALLOT_MIN == 192 &&
                   RPT_COMPACT_BALLOT_MIN == 384 && RPT_COMPACT_STAGE == 3072 && RPT_LDS_I64_GROUP == 1 &&
                   RPT_PROBE_RING == 2 && RPT_LOOKBACK_TAIL == 0 && RPT_COMPACT_V16 == 0 && RPT_SUMSCAN_TAIL == 0 &&
-                  RPT_PROBE_BUFSTORE == 0 && RPT_PROBE_SCHED_BARRIER == 0 && RPT_LDS_HYBRID_MAX_LOG == 16 &&
+                  RPT_PROBE_BUFSTORE == 0 && RPT_PROBE_SCHED_BARRIER == 0 && RPT_LDS_HYBRID_MAX_LOG == 17 &&
                   RPT_HYBRID_I64_GROUP == 2,
               "product build: tuning macros must keep their tested defaults (use tools/build_variants.sh)");
 static_assert(RPT_FUSED_SEL == 1 && RPT_NT_KEY_LOADS == 1 && RPT_NT_PART_STORES == 1 && RPT_NT_PROBE_LOADS == 1 &&
@@ -478,6 +480,8 @@ int strategy_supported(int strategy, int log_num_blocks) {
 //               L2 -- faster than the gather and than the partitioned probe (tools/ab_hybrid.sh,
 //               profiles/r06/ab_hybrid2.txt). Below 4 Mi rows its 128 KiB staging per workgroup costs more than it
 //               saves: GATHER (1 Mi rows: 37.5 vs 35.7 us, 4 Mi: 43.8 vs 51.6 us, profiles/r06/ab_hybrid_small.txt);
+//   1 MiB       LDS, hybrid, for 4 Mi .. 32 Mi rows (over the gather: 1-8 %, profiles/r06/ab_hybrid_1m.txt); the
+//               partitioned probe from 32 Mi rows as below (1e9 keys: 3.89 vs 4.22 ms);
 //   <= 128 MiB  PARTITIONED for batches of >= 4 Mi rows (>= 32 Mi below 8 MiB filters, where the L2
 //               still serves the gather well), else GATHER: routing has ~50 us of fixed cost;
 //   <= 16 GiB   BUCKETED for batches of >= max(blocks/8, 32 Mi) rows (it stages the whole filter in
@@ -488,7 +492,8 @@ int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
   if (requested != RPT_PROBE_AUTO) return requested;
   const int L = log_num_blocks;
   if (L <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
-  if (L <= RPT_LDS_HYBRID_MAX_LOG) return n >= kHybridMinRows ? RPT_PROBE_LDS : RPT_PROBE_GATHER;
+  if (L <= RPT_LDS_HYBRID_MAX_LOG && n >= kHybridMinRows && (L <= 16 || n < (1ULL << 25))) return RPT_PROBE_LDS;
+  if (L <= 16) return RPT_PROBE_GATHER;
   // measured crossovers (tools/strategy_crossover.py --mid, profiles/r01/strategy_crossover_mid.jsonl):
   // the partitioned probe overtakes the (partly L2-resident) gather from 2^25 rows for 256 KiB..2 MiB
   // filters and from 2^22 rows above

@@ -54,13 +54,13 @@ typedef enum rpt_key_type {
 /* How a probe reaches the filter blocks (rpt_bf_set_probe_strategy). All give identical results. */
 typedef enum rpt_probe_strategy {
   RPT_PROBE_AUTO = 0,        /* by filter and batch size (measured crossovers): LDS (<= 128 KiB, and
-                                256 / 512 KiB for n >= 4 Mi);
+                                256 / 512 KiB for n >= 4 Mi, 1 MiB for 4 Mi <= n < 32 Mi);
                                 PARTITIONED (<= 128 MiB) for n >= 32 Mi (256 KiB..2 MiB) or n >= 4 Mi
                                 (4 MiB and up); BUCKETED (<= 16 GiB, n >= max(blocks/8, 32 Mi));
                                 otherwise GATHER */
   RPT_PROBE_GATHER = 1,      /* one random 8-byte gather per key from L2 / Infinity Cache / HBM */
   RPT_PROBE_LDS = 2,         /* filter staged in each workgroup's LDS: whole (<= 128 KiB), or its first 128 KiB
-                                with the rest gathered from L2 (256 / 512 KiB) */
+                                with the rest gathered from L2 (256 KiB .. 1 MiB) */
   RPT_PROBE_PARTITIONED = 3, /* rows bucketed per 16 Ki-row tile by 128 KiB filter slice; each slice is
                                 probed from LDS, then row order is restored (filters 128 KiB..128 MiB) */
   RPT_PROBE_BUCKETED = 4     /* two levels: rows first bucketed by 32 MiB filter region into contiguous

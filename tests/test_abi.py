@@ -119,8 +119,8 @@ def test_strategy_support_rules():
     for L in range(0, 30):
         assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_GATHER, L) == 1
         assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_AUTO, L) == 1
-        # whole filter in LDS up to 2^14 blocks (128 KiB); 2^15..2^16 (256 / 512 KiB): the hybrid, first 128 KiB in LDS
-        assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_LDS, L) == (L <= 16)
+        # whole filter in LDS up to 2^14 blocks (128 KiB); 2^15..2^17 (256 KiB..1 MiB): the hybrid, first 128 KiB in LDS
+        assert lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_LDS, L) == (L <= 17)
     # partitioned: at least one full LDS slice, at most 1024 slices (128 KiB .. 128 MiB)
     part = [L for L in range(0, 34) if lib.rpt_probe_strategy_supported(_lib.RPT_PROBE_PARTITIONED, L)]
     assert part == list(range(14, 25))

@@ -115,8 +115,9 @@ def test_auto_routes_large_filters(rpt):
     assert tiny.probe_strategy_for(1 << 28) == 2 and tiny.probe_strategy_for(1 << 16) == 2
     small = rpt.BloomFilter(log_num_blocks=15)  # 256 KiB (512 KiB too): the hybrid LDS probe at any size
     assert small.probe_strategy_for(1 << 24) == 2 and small.probe_strategy_for(1 << 28) == 2
-    small17 = rpt.BloomFilter(log_num_blocks=17)  # 1 MiB: L2 gathers below 32 Mi rows, routed above
-    assert small17.probe_strategy_for(1 << 24) == GATHER and small17.probe_strategy_for(1 << 28) == PARTITIONED
+    small17 = rpt.BloomFilter(log_num_blocks=17)  # 1 MiB: gathers below 4 Mi rows, the hybrid to 32 Mi, routed above
+    assert small17.probe_strategy_for(1 << 21) == GATHER and small17.probe_strategy_for(1 << 24) == 2
+    assert small17.probe_strategy_for(1 << 28) == PARTITIONED
     small17.close()
     mid19 = rpt.BloomFilter(log_num_blocks=19)  # 4 MiB: routed from 4 Mi rows
     assert mid19.probe_strategy_for(1 << 22) == PARTITIONED and mid19.probe_strategy_for(1 << 21) == GATHER

@@ -1,7 +1,7 @@
-"""The hybrid LDS/L2 direct probe (`probe_bits_hybrid_kernel`: 256 / 512 KiB filters, 2^15 / 2^16 blocks, the first
-2^14 words staged in each workgroup's LDS and the rest gathered from L2) against the oracle, bit-exact: dense int64 /
-int32 columns with ragged tails (the pipelined loop and the general loop), NULLs, and a dictionary vector through a
-row selection; and AUTO's choice of it for those two sizes only."""
+"""The hybrid LDS/L2 direct probe (`probe_bits_hybrid_kernel`: 256 KiB .. 1 MiB filters, 2^15 .. 2^17 blocks, the
+first 2^14 words staged in each workgroup's LDS and the rest gathered from L2) against the oracle, bit-exact: dense
+int64 / int32 columns with ragged tails (the pipelined loop and the general loop), NULLs, and a dictionary vector
+through a row selection; and AUTO's choice of it."""
 import numpy as np
 import pytest
 import torch
@@ -12,7 +12,7 @@ import rpt_oracle as orc
 pytestmark = pytest.mark.gpu
 
 GATHER, LDS, PARTITIONED = 1, 2, 3
-LOG_NBS = [15, 16]  # 256 KiB, 512 KiB
+LOG_NBS = [15, 16, 17]  # 256 KiB, 512 KiB, 1 MiB
 
 
 @pytest.fixture(scope="module")
@@ -46,15 +46,18 @@ def built(rpt, dtype, n_build, seed, LOG_NB):
     return bf, build, w, rng
 
 
-def test_auto_picks_hybrid_for_256k_and_512k_only(rpt):
-    # from 4 Mi rows (below, its LDS staging costs more than it saves: the gather)
-    for log_nb, expect in ((14, LDS), (15, LDS), (16, LDS), (17, GATHER)):
+def test_auto_picks_hybrid(rpt):
+    # from 4 Mi rows (below, its LDS staging costs more than it saves: the gather); 1 MiB only up to 32 Mi rows
+    for log_nb, expect in ((14, LDS), (15, LDS), (16, LDS), (17, LDS), (18, GATHER)):
         bf = rpt.BloomFilter(log_num_blocks=log_nb)
         assert bf.probe_strategy_for(1 << 24) == expect, log_nb
         assert bf.probe_strategy_for(1 << 22) == expect, log_nb
         assert bf.probe_strategy_for((1 << 22) - 1) == (LDS if log_nb == 14 else GATHER), log_nb
         bf.close()
-    assert rpt.BloomFilter(log_num_blocks=17).probe_strategy_for(1 << 28) == PARTITIONED
+    for log_nb in (15, 16):
+        assert rpt.BloomFilter(log_num_blocks=log_nb).probe_strategy_for(1 << 28) == LDS
+    assert rpt.BloomFilter(log_num_blocks=17).probe_strategy_for((1 << 25) - 1) == LDS
+    assert rpt.BloomFilter(log_num_blocks=17).probe_strategy_for(1 << 25) == PARTITIONED
 
 
 @pytest.mark.parametrize("LOG_NB", LOG_NBS)
