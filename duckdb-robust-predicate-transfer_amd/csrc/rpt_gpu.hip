@@ -493,7 +493,7 @@ int resolve_strategy(int requested, int log_num_blocks, uint64_t n) {
   const int L = log_num_blocks;
   if (L <= rpt::kLdsDirectMaxLog) return RPT_PROBE_LDS;
   if (L <= RPT_LDS_HYBRID_MAX_LOG && n >= kHybridMinRows && (L <= 16 || n < (1ULL << 25))) return RPT_PROBE_LDS;
-  if (L <= 16) return RPT_PROBE_GATHER;
+  if (L <= 16 && L <= RPT_LDS_HYBRID_MAX_LOG) return RPT_PROBE_GATHER;  // 256 / 512 KiB below 4 Mi rows
   // measured crossovers (tools/strategy_crossover.py --mid, profiles/r01/strategy_crossover_mid.jsonl):
   // the partitioned probe overtakes the (partly L2-resident) gather from 2^25 rows for 256 KiB..2 MiB
   // filters and from 2^22 rows above
