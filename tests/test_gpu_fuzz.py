@@ -37,7 +37,7 @@ def dev(a):
 
 def case(seed):
     rng = np.random.default_rng(seed)
-    log_nb = int(rng.choice([4, 9, 13, 14, 16, 18, 21, 22, 23, 24]))
+    log_nb = int(rng.choice([4, 9, 13, 14, 15, 16, 17, 18, 21, 22, 23, 24]))  # 15-17: the hybrid LDS/L2 probe too
     dtype = np.int64 if rng.random() < 0.6 else np.int32
     n_build = int(rng.integers(1, 400_000))
     n_probe = int(rng.choice([1, 63, 511, 513, 16383, 16385, int(rng.integers(1, 700_000))]))
